@@ -1,0 +1,130 @@
+/*
+ * sgnn.h — C-ABI of libsgnn_hip.so, the MI355X (gfx950) implementation of
+ * sgnn's single-scale LearnedSimulator hot path.
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t
+ * (passed as void* so the header needs no HIP include), launches
+ * asynchronously on that stream, never synchronises, never allocates, and
+ * returns an sgnn_status.  All buffers are owned by the caller.  Float data
+ * is fp32; graph indices are int32 (N*K < 2^31).  Weights are passed in
+ * torch.nn.Linear layout [out][in], row-major.
+ *
+ * Reference interfaces each group replaces are cited per function
+ * (paths relative to the xrkong/sgnn repository root).
+ */
+#ifndef SGNN_H_
+#define SGNN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum sgnn_status {
+  SGNN_OK = 0,
+  SGNN_ERR_INVALID = 1,     /* bad pointer / size / dimension */
+  SGNN_ERR_UNSUPPORTED = 2, /* shape this build has no kernel for (e.g. hidden != 64/128) */
+  SGNN_ERR_HIP = 3          /* a HIP launch failed; see sgnn_last_error() */
+} sgnn_status;
+
+/* One build_mlp(...) (+ optional LayerNorm) parameter set,
+ * sgnn/single_scale/graph_network.py:7-45 and :86-96 / :139-148.
+ * nlin = number of Linear layers (nmlp_layers + 1). ln_g/ln_b may be NULL
+ * (the Decoder has no LayerNorm, graph_network.py:321). */
+typedef struct sgnn_mlp {
+  const float* w1; const float* b1; /* [hidden][in_dim] */
+  const float* w2; const float* b2; /* [out_dim][hidden] (nlin == 2) */
+  const float* ln_g; const float* ln_b; /* [out_dim] or NULL */
+  int32_t in_dim, hidden, out_dim, nlin;
+} sgnn_mlp;
+
+const char* sgnn_version(void);
+const char* sgnn_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Neighbour search.  Replaces torch_geometric.nn.radius_graph(x, r, batch,
+ * loop, max_num_neighbors) -> torch_cluster.radius, called at
+ * sgnn/single_scale/learned_simulator.py:116-117 (batch ids :104-106).
+ * Output is a receiver-sorted CSR: for receiver i (query), senders
+ * send[rowptr[i] .. rowptr[i+1]) ascending, each with ||p_j - p_i||^2 < r^2
+ * (fp32, dims summed in order), same example (ex_ptr), at most K kept
+ * (first K ascending; K+1 then self dropped when loop == 0).  recv[e] = i.
+ * The reference's edge_index = [send ; recv] (int64) in the same order.
+ * Capacity: edge_cap >= n * (loop ? K : K + 1); K + !loop <= 32.
+ * pos: particle i at pos + i * pos_stride (so the last frame of a [N,T,d]
+ * sequence can be passed without a copy).  ex_ptr: device int64 [n_ex+1].
+ * workspace: sgnn_radius_workspace_bytes(n, K, loop) bytes, 256-B aligned.
+ * ------------------------------------------------------------------------- */
+size_t sgnn_radius_workspace_bytes(int64_t n, int32_t K, int32_t loop);
+int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n, int32_t dim,
+                      const int64_t* ex_ptr, int32_t n_ex, float radius, int32_t K,
+                      int32_t loop, void* workspace, int32_t* rowptr, int32_t* send,
+                      int32_t* recv, int64_t edge_cap, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Encoder, node side: node features of LearnedSimulator._encoder_preprocessor
+ * (learned_simulator.py:256-290: normalised velocity history, wall distance
+ * clamp(x+2, 0, R), optional type embedding) fused with Encoder.node_fn
+ * (graph_network.py:86-90, :111) and with the receiver/sender projections of
+ * the first InteractionNetwork's edge MLP:
+ *   u = x0 W1[:, 0:H]^T + b1,  v = x0 W1[:, H:2H]^T   (W1 of edge0)
+ * pos_seq: [n][T][dim].  types/emb_w only read when use_emb != 0.
+ * ------------------------------------------------------------------------- */
+int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int32_t dim,
+                      const int64_t* types, const float* emb_w, int32_t emb_dim,
+                      int32_t use_emb, const float* vel_mean, const float* vel_std,
+                      float radius, const sgnn_mlp* enc, const sgnn_mlp* edge0,
+                      float* x0, float* u, float* v, void* stream);
+
+/* Encoder, edge side: edge features (learned_simulator.py:299-312:
+ * (p_s - p_r)/R and its norm) fused with Encoder.edge_fn (graph_network.py:
+ * 92-96).  Output e0 in the tiled layout (sgnn_edge_tile_floats(H) floats per
+ * 32-edge tile) that sgnn_edge_layer reads. */
+int64_t sgnn_edge_latent_floats(int64_t edge_cap, int32_t hidden);
+int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t dim, float radius,
+                      const int32_t* rowptr, const int32_t* send, const int32_t* recv,
+                      int64_t n, int64_t edge_cap, const sgnn_mlp* enc, float* e0t,
+                      void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Processor, edge half of one InteractionNetwork (graph_network.py:150-199):
+ *   m_e  = LN(W2 relu(u[recv] + v[send] + e_scale * W1[:, 2H:3H] e0_e) + b2)
+ *   agg_i = sum over edges e with recv == i of m_e   (aggr='add', :136)
+ * e_scale = 2^k reproduces the edge-latent doubling (update returns the input
+ * edge features, :176/:222).  agg rows whose edges straddle a 32-edge tile
+ * are left in cin/cout ([ceil(edge_cap/32)][H] each); sgnn_node_layer*
+ * resolves them (deterministic, no atomics).
+ * ------------------------------------------------------------------------- */
+int sgnn_edge_layer(const float* u, const float* v, const float* e0t, float e_scale,
+                    const int32_t* rowptr, const int32_t* send, const int32_t* recv,
+                    int64_t n, int64_t edge_cap, const sgnn_mlp* edge_fn, float* agg,
+                    float* cin, float* cout, void* stream);
+
+/* Processor, node half (graph_network.py:201-222 and the residual :176):
+ *   x_out = x_in + LN(W2 relu(W1 [agg, x_in] + b1) + b2)
+ * fused with the next layer's projections (u, v as sgnn_encode_nodes). */
+int sgnn_node_layer(const float* x_in, const float* agg, const float* cin, const float* cout,
+                    const int32_t* rowptr, int64_t n, const sgnn_mlp* node_fn,
+                    const sgnn_mlp* next_edge, float* x_out, float* u, float* v, void* stream);
+
+/* Last processor node half fused with the Decoder (graph_network.py:321-333,
+ * no LayerNorm) and LearnedSimulator._decoder_postprocessor
+ * (learned_simulator.py:381-411, Euler with dt = 1):
+ *   pred = decoder(x_out) [n][dim+1];  a = pred[:, :dim] * acc_std + acc_mean
+ *   next_pos = p_T + ((p_T - p_{T-1}) + a)          (pos_seq [n][T][dim])
+ * x_out may be NULL (inference).  If window_out is not NULL it receives the
+ * next input window of the autoregressive rollout, cat([pos_seq[:, 1:],
+ * next_pos[:, None]], 1) (sgnn/single_scale/evaluate.py:136-139). */
+int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin,
+                           const float* cout, const int32_t* rowptr, int64_t n,
+                           const sgnn_mlp* node_fn, const sgnn_mlp* decoder,
+                           const float* pos_seq, int32_t T, int32_t dim,
+                           const float* acc_mean, const float* acc_std, float* x_out,
+                           float* pred, float* next_pos, float* window_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGNN_H_ */

@@ -1,0 +1,97 @@
+"""ctypes binding of libsgnn_hip.so (the C-ABI declared in include/sgnn.h).
+
+The library is the product: if it is missing or no GPU is visible, every
+entry point raises — there is no CPU or eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libsgnn_hip.so")
+
+SGNN_OK, SGNN_ERR_INVALID, SGNN_ERR_UNSUPPORTED, SGNN_ERR_HIP = 0, 1, 2, 3
+
+c_void_p, c_int64, c_int32, c_float = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
+
+
+class SgnnMlp(ctypes.Structure):
+    """struct sgnn_mlp (include/sgnn.h)."""
+    _fields_ = [("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p), ("b2", c_void_p),
+                ("ln_g", c_void_p), ("ln_b", c_void_p),
+                ("in_dim", c_int32), ("hidden", c_int32), ("out_dim", c_int32), ("nlin", c_int32)]
+
+
+P_MLP = ctypes.POINTER(SgnnMlp)
+
+# name -> (restype, argtypes); every symbol include/sgnn.h declares
+SIGNATURES = {
+    "sgnn_version": (ctypes.c_char_p, []),
+    "sgnn_last_error": (ctypes.c_char_p, []),
+    "sgnn_radius_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int32, c_int32]),
+    "sgnn_radius_graph": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int32,
+                                         c_float, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_int64, c_void_p]),
+    "sgnn_encode_nodes": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
+                                         c_int32, c_int32, c_void_p, c_void_p, c_float, P_MLP,
+                                         P_MLP, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sgnn_edge_latent_floats": (c_int64, [c_int64, c_int32]),
+    "sgnn_encode_edges": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
+                                         c_void_p, c_int64, c_int64, P_MLP, c_void_p, c_void_p]),
+    "sgnn_edge_layer": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                       c_void_p, c_int64, c_int64, P_MLP, c_void_p, c_void_p,
+                                       c_void_p, c_void_p]),
+    "sgnn_node_layer": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                       P_MLP, P_MLP, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sgnn_node_layer_decode": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_int64, P_MLP, P_MLP, c_void_p, c_int32, c_int32,
+                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p]),
+}
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+class SgnnError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """dlopen the library and bind every symbol (no GPU needed)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise SgnnError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                        "(the HIP library is required; there is no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def lib() -> ctypes.CDLL:
+    return _LIB if _LIB is not None else load_library()
+
+
+def check(status: int, what: str) -> None:
+    if status != SGNN_OK:
+        msg = lib().sgnn_last_error().decode()
+        kind = {SGNN_ERR_INVALID: ValueError, SGNN_ERR_UNSUPPORTED: NotImplementedError}.get(status, SgnnError)
+        raise kind(f"{what}: {msg} (status {status})")
+
+
+def stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu_tensor(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor (sgnn_amd runs on MI355X only; no CPU path)")

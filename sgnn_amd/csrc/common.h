@@ -1,0 +1,198 @@
+// Shared device helpers for the sgnn gfx950 kernels.
+//
+// MFMA convention used everywhere ("items on lanes"):
+//   D[unit][item] = sum_k W[unit][k] * In[item][k]      (v_mfma_f32_32x32x2_f32)
+// A operand (lane l) = W[unit0 + (l&31)][kappa(s, l>>5)]  -- read from LDS
+// B operand (lane l) = In[item0 + (l&31)][kappa(s, l>>5)] -- per-lane register
+// D/C layout: lane l holds item (l&31); register r of tile t holds unit
+//   32 t + crow(r, l>>5), crow(r, h) = (r&3) + 8 (r>>2) + 4 h.
+// Because every item sits on one lane with its units in registers, an
+// accumulator is directly the B operand of the next product (the k order is
+// the crow permutation; the W read uses the same permutation), a row-wise
+// LayerNorm is a register sum plus one lane^32 exchange, and nothing crosses
+// LDS between the two Linear layers of an MLP.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define SGNN_DEV __device__ __forceinline__
+
+SGNN_DEV int lane_id() { return threadIdx.x & 63; }
+
+SGNN_DEV int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+SGNN_DEV f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+SGNN_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+SGNN_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+SGNN_DEV float wave_xor32(float v) { return __shfl_xor(v, 32, 64); }
+
+// Copy a [rows x cols] row-major global matrix (leading dim ldg) into LDS
+// with leading dimension lds_ld, zero-filling rows >= rows_valid and columns
+// >= cols_valid up to [rows_pad x cols_pad].  Optional scale.
+SGNN_DEV void stage_matrix(float* lds, int lds_ld, const float* g, int ldg, int rows_valid,
+                           int cols_valid, int rows_pad, int cols_pad, float scale = 1.0f) {
+  const int total = rows_pad * cols_pad;
+  for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    const int r = idx / cols_pad, c = idx - r * cols_pad;
+    float v = 0.0f;
+    if (r < rows_valid && c < cols_valid) v = g[(int64_t)r * ldg + c] * scale;
+    lds[r * lds_ld + c] = v;
+  }
+}
+
+SGNN_DEV void stage_vec(float* lds, const float* g, int n_valid, int n_pad) {
+  for (int idx = threadIdx.x; idx < n_pad; idx += blockDim.x)
+    lds[idx] = (g != nullptr && idx < n_valid) ? g[idx] : 0.0f;
+}
+
+// acc[t] += W[32t + lane][kappa] * b for one k-step; W rows in LDS with
+// leading dim ld, k offset `koff` already including the lane-half term.
+template <int TH>
+SGNN_DEV void mfma_step(f32x16 (&acc)[TH], const float* wl, int ld, int koff, float b) {
+  const int l = lane_id() & 31;
+#pragma unroll
+  for (int t = 0; t < TH; ++t) acc[t] = mfma32(wl[(32 * t + l) * ld + koff], b, acc[t]);
+}
+
+// Product with the B operand in C layout (a previous accumulator X, TK
+// tiles): acc[t] += sum_{k} W[32t+lane][k] X[k][item] over K = 32*TK units.
+template <int TH, int TK>
+SGNN_DEV void mfma_from_acc(f32x16 (&acc)[TH], const float* wl, int ld, int kbase,
+                            const f32x16 (&x)[TK]) {
+  const int l = lane_id() & 31, h = lane_id() >> 5;
+#pragma unroll
+  for (int tk = 0; tk < TK; ++tk) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 w[TH];
+#pragma unroll
+      for (int t = 0; t < TH; ++t) w[t] = ld4(wl + (32 * t + l) * ld + kbase + 32 * tk + 8 * g + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int t = 0; t < TH; ++t) acc[t] = mfma32(w[t][c], x[tk][4 * g + c], acc[t]);
+      }
+    }
+  }
+}
+
+// Same, but the B operand comes as float4 groups in the C-layout order that
+// the caller loads from memory: xg[tk*4+g] holds units 32tk+8g+4h+(0..3).
+template <int TH, int TK>
+SGNN_DEV void mfma_from_groups(f32x16 (&acc)[TH], const float* wl, int ld, int kbase,
+                               const f32x4 (&xg)[TK * 4], float scale) {
+  const int l = lane_id() & 31, h = lane_id() >> 5;
+#pragma unroll
+  for (int tk = 0; tk < TK; ++tk) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 w[TH];
+#pragma unroll
+      for (int t = 0; t < TH; ++t) w[t] = ld4(wl + (32 * t + l) * ld + kbase + 32 * tk + 8 * g + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float b = xg[tk * 4 + g][c] * scale;
+#pragma unroll
+        for (int t = 0; t < TH; ++t) acc[t] = mfma32(w[t][c], b, acc[t]);
+      }
+    }
+  }
+}
+
+// Initialise acc with a per-unit bias (LDS vector, may be null -> 0).
+template <int TH>
+SGNN_DEV void acc_bias(f32x16 (&acc)[TH], const float* bias_lds) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = bias_lds ? bias_lds[32 * t + crow(r, h)] : 0.0f;
+}
+
+template <int TH>
+SGNN_DEV void acc_relu(f32x16 (&acc)[TH]) {
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = fmaxf(acc[t][r], 0.0f);
+}
+
+// Row-wise LayerNorm over the 32*TH units of each item (one lane pair), eps
+// 1e-5, two-pass mean / biased variance as torch.nn.LayerNorm.
+template <int TH>
+SGNN_DEV void acc_layernorm(f32x16 (&acc)[TH], const float* gamma_lds, const float* beta_lds) {
+  const int h = lane_id() >> 5;
+  constexpr float inv_n = 1.0f / (32.0f * TH);
+  float s = 0.0f;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += acc[t][r];
+  s += wave_xor32(s);
+  const float mean = s * inv_n;
+  float v = 0.0f;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float d = acc[t][r] - mean;
+      v += d * d;
+    }
+  v += wave_xor32(v);
+  const float rstd = 1.0f / sqrtf(v * inv_n + 1e-5f);
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u = 32 * t + crow(r, h);
+      acc[t][r] = (acc[t][r] - mean) * rstd * gamma_lds[u] + beta_lds[u];
+    }
+}
+
+// Load a node-major row (row-major [N][32*TH]) in C layout into f32x16 regs.
+template <int TH>
+SGNN_DEV void load_row_clayout(f32x16 (&x)[TH], const float* row) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = ld4(row + 32 * t + 8 * g + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[t][4 * g + c] = v[c];
+    }
+}
+
+template <int TH>
+SGNN_DEV void add_row_clayout(f32x16 (&x)[TH], const float* row) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = ld4(row + 32 * t + 8 * g + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[t][4 * g + c] += v[c];
+    }
+}
+
+template <int TH>
+SGNN_DEV void store_row_clayout(float* row, const f32x16 (&x)[TH]) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = x[t][4 * g + c];
+      st4(row + 32 * t + 8 * g + 4 * h, v);
+    }
+}

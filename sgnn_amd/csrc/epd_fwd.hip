@@ -1,0 +1,578 @@
+// Encode-Process-Decode forward for gfx950 (fp32 MFMA v_mfma_f32_32x32x2_f32).
+//
+// Replaces, per step, the PyG/torch op chain of
+//   sgnn/single_scale/learned_simulator.py:231-316 (features),
+//   sgnn/single_scale/graph_network.py:86-96 (Encoder), :150-222 (L x
+//   InteractionNetwork), :321-333 (Decoder) and learned_simulator.py:381-411
+//   (Euler integrator)
+// with 2 + 2L launches:
+//   k_encode_nodes  features -> node MLP+LN -> x0, and layer-0 u/v
+//   k_encode_edges  edge features -> edge MLP+LN -> e0 (tiled layout)
+//   per layer k:
+//     k_edge_layer  gather u[recv] + v[send] + 2^k W1e e0 -> ReLU -> W2 -> LN
+//                   -> wave-segmented sum over the receiver-sorted CSR
+//     k_node_layer  [agg, x] -> MLP+LN -> residual, then the NEXT layer's
+//                   u/v projections, or (last layer) decoder + integrator.
+//
+// The edge MLP's first Linear is split by input block (x_i | x_j | e):
+// W1 [x_i; x_j; e] = (W1_i x)[recv] + (W1_j x)[send] + W1_e e, so the two
+// node blocks are computed once per NODE (u, v) instead of once per edge:
+// the per-edge work drops from 3H^2+H^2 to H^2+H^2 multiply-adds.
+#include "common.h"
+#include "../../include/sgnn.h"
+#include "sgnn_internal.h"
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves; each wave owns 32 items at a time
+constexpr int kWaves = kBlock / 64;
+
+struct EncNodeArgs {
+  const float* pos_seq;
+  int64_t n;
+  int T, dim;
+  const int64_t* types;
+  const float* emb_w;
+  int emb_dim, use_emb;
+  const float* vel_mean;
+  const float* vel_std;
+  float radius;
+  int feat;  // number of real node features
+  const float *w1, *b1, *w2, *b2, *g, *bb;  // encoder node MLP
+  const float *we, *be;                     // edge0 W1 [H][3H], b1
+  float *x0, *u, *v;
+};
+
+template <int TH>
+SGNN_DEV void store_uv(const float* Wi, const float* Wj, const float* b1e, int ldh,
+                       const f32x16 (&x)[TH], float* u_row, float* v_row, bool valid) {
+  f32x16 acc[TH];
+  acc_bias<TH>(acc, b1e);
+  mfma_from_acc<TH, TH>(acc, Wi, ldh, 0, x);
+  if (valid) store_row_clayout<TH>(u_row, acc);
+  acc_bias<TH>(acc, nullptr);
+  mfma_from_acc<TH, TH>(acc, Wj, ldh, 0, x);
+  if (valid) store_row_clayout<TH>(v_row, acc);
+}
+
+template <int TH, int TKF>
+__global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4, ldf = 32 * TKF + 4;
+  extern __shared__ float lds[];
+  float* W1 = lds;
+  float* W2 = W1 + H * ldf;
+  float* Wi = W2 + H * ldh;
+  float* Wj = Wi + H * ldh;
+  float* b1 = Wj + H * ldh;
+  float* b2 = b1 + H;
+  float* g = b2 + H;
+  float* bb = g + H;
+  float* b1e = bb + H;
+  stage_matrix(W1, ldf, a.w1, a.feat, H, a.feat, H, 32 * TKF);
+  stage_matrix(W2, ldh, a.w2, H, H, H, H, H);
+  stage_matrix(Wi, ldh, a.we, 3 * H, H, H, H, H);
+  stage_matrix(Wj, ldh, a.we + H, 3 * H, H, H, H, H);
+  stage_vec(b1, a.b1, H, H);
+  stage_vec(b2, a.b2, H, H);
+  stage_vec(g, a.g, H, H);
+  stage_vec(bb, a.bb, H, H);
+  stage_vec(b1e, a.be, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  const int nvel = (a.T - 1) * a.dim;
+  for (int64_t blk = blockIdx.x; blk * (32 * kWaves) < a.n; blk += gridDim.x) {
+    const int64_t node0 = blk * (32 * kWaves) + 32 * w;
+    if (node0 >= a.n) continue;
+    const int64_t i = node0 + j;
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    const float* p = a.pos_seq + ic * a.T * a.dim;
+    f32x16 xf[TKF];
+#pragma unroll
+    for (int tk = 0; tk < TKF; ++tk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = 32 * tk + crow(r, h);
+        float val = 0.0f;
+        if (f < nvel) {  // learned_simulator.py:258,272-278
+          const int t = f / a.dim, c = f - t * a.dim;
+          const float vel = __fsub_rn(p[(t + 1) * a.dim + c], p[t * a.dim + c]);
+          val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[c]), a.vel_std[c]);
+        } else if (f == nvel) {  // :282-284
+          val = fminf(fmaxf(__fadd_rn(p[(a.T - 1) * a.dim], 2.0f), 0.0f), a.radius);
+        } else if (a.use_emb && f < nvel + 1 + a.emb_dim) {  // :287-290
+          val = a.emb_w[a.types[ic] * a.emb_dim + (f - nvel - 1)];
+        }
+        xf[tk][r] = val;
+      }
+    f32x16 hacc[TH];
+    acc_bias<TH>(hacc, b1);
+    mfma_from_acc<TH, TKF>(hacc, W1, ldf, 0, xf);
+    acc_relu<TH>(hacc);
+    f32x16 y[TH];
+    acc_bias<TH>(y, b2);
+    mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
+    acc_layernorm<TH>(y, g, bb);
+    if (valid) store_row_clayout<TH>(a.x0 + i * H, y);
+    store_uv<TH>(Wi, Wj, b1e, ldh, y, a.u + i * H, a.v + i * H, valid);
+  }
+}
+
+struct EncEdgeArgs {
+  const float* pos;
+  int64_t stride;
+  int dim;
+  float radius;
+  const int32_t *rowptr, *send, *recv;
+  int64_t n;
+  const float *w1, *b1, *w2, *b2, *g, *bb;
+  float* e0t;
+};
+
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4, ld1 = 5;
+  extern __shared__ float lds[];
+  float* W1 = lds;
+  float* W2 = W1 + H * ld1;
+  float* b1 = W2 + H * ldh;
+  float* b2 = b1 + H;
+  float* g = b2 + H;
+  float* bb = g + H;
+  stage_matrix(W1, ld1, a.w1, a.dim + 1, H, a.dim + 1, H, 4);
+  stage_matrix(W2, ldh, a.w2, H, H, H, H, H);
+  stage_vec(b1, a.b1, H, H);
+  stage_vec(b2, a.b2, H, H);
+  stage_vec(g, a.g, H, H);
+  stage_vec(bb, a.bb, H, H);
+  __syncthreads();
+  const int64_t E = a.rowptr[a.n];
+  const int64_t ntiles = (E + 31) / 32;
+  const int l = lane_id(), j = l & 31, h = l >> 5;
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t tile = gw; tile < ntiles; tile += nw) {
+    const int64_t e = tile * 32 + j;
+    const int64_t ec = e < E ? e : E - 1;
+    const int64_t s = a.send[ec], r = a.recv[ec];
+    float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float ss = 0.0f;
+    for (int c = 0; c < a.dim; ++c) {  // learned_simulator.py:299-312
+      const float d = __fdiv_rn(__fsub_rn(a.pos[s * a.stride + c], a.pos[r * a.stride + c]), a.radius);
+      f[c] = d;
+      ss = __fadd_rn(ss, __fmul_rn(d, d));
+    }
+    f[a.dim] = sqrtf(ss);
+    f32x16 hacc[TH];
+    acc_bias<TH>(hacc, b1);
+    mfma_step<TH>(hacc, W1, ld1, h, h ? f[1] : f[0]);
+    mfma_step<TH>(hacc, W1, ld1, 2 + h, h ? f[3] : f[2]);
+    acc_relu<TH>(hacc);
+    f32x16 y[TH];
+    acc_bias<TH>(y, b2);
+    mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
+    acc_layernorm<TH>(y, g, bb);
+    float* dst = a.e0t + tile * (32 * H) + l * 4;
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        f32x4 v4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v4[c] = y[t][4 * gg + c];
+        st4(dst + (t * 4 + gg) * 256, v4);
+      }
+  }
+}
+
+struct EdgeLayerArgs {
+  const float *u, *v, *e0t;
+  float e_scale;
+  const int32_t *rowptr, *send, *recv;
+  int64_t n;
+  const float *we, *w2, *b2, *g, *bb;  // we = edge W1 + 2H (ld 3H)
+  float *agg, *cin, *cout;
+};
+
+SGNN_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4;
+  extern __shared__ float lds[];
+  float* We = lds;
+  float* W2 = We + H * ldh;
+  float* b2 = W2 + H * ldh;
+  float* g = b2 + H;
+  float* bb = g + H;
+  float* mbuf = bb + H;  // per wave [32][ldh]
+  stage_matrix(We, ldh, a.we, 3 * H, H, H, H, H);
+  stage_matrix(W2, ldh, a.w2, H, H, H, H, H);
+  stage_vec(b2, a.b2, H, H);
+  stage_vec(g, a.g, H, H);
+  stage_vec(bb, a.bb, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  float* ml = mbuf + w * 32 * ldh;
+  const int64_t E = a.rowptr[a.n];
+  const int64_t ntiles = (E + 31) / 32;
+  // contiguous tile range per wave: neighbouring tiles share sender rows
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + w;
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  const int64_t t_begin = ntiles * gw / nw, t_end = ntiles * (gw + 1) / nw;
+  for (int64_t tile = t_begin; tile < t_end; ++tile) {
+    const int64_t base = tile * 32;
+    const int64_t e = base + j;
+    const bool valid = e < E;
+    const int64_t ec = valid ? e : E - 1;
+    const int rv = a.recv[ec];
+    const int64_t s = a.send[ec];
+    f32x16 hacc[TH];
+    load_row_clayout<TH>(hacc, a.u + (int64_t)rv * H);
+    add_row_clayout<TH>(hacc, a.v + s * H);
+    f32x4 xg[TH * 4];
+    const float* src = a.e0t + tile * (32 * H) + l * 4;
+#pragma unroll
+    for (int q = 0; q < TH * 4; ++q) xg[q] = ld4(src + q * 256);
+    mfma_from_groups<TH, TH>(hacc, We, ldh, 0, xg, a.e_scale);
+    acc_relu<TH>(hacc);
+    f32x16 y[TH];
+    acc_bias<TH>(y, b2);
+    mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
+    acc_layernorm<TH>(y, g, bb);
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        f32x4 v4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v4[c] = y[t][4 * gg + c];
+        st4(ml + j * ldh + 32 * t + 8 * gg + 4 * h, v4);
+      }
+    wave_lds_sync();
+    // wave-segmented sum over the receiver-sorted CSR: lane = latent unit
+    const int nvalid = (E - base) < 32 ? (int)(E - base) : 32;
+    constexpr int UPL = H / 64 > 0 ? H / 64 : 1;  // units per lane
+    float acc[UPL];
+#pragma unroll
+    for (int q = 0; q < UPL; ++q) acc[q] = 0.0f;
+    int seg0 = 0;
+    for (int jj = 0; jj < nvalid; ++jj) {
+#pragma unroll
+      for (int q = 0; q < UPL; ++q) acc[q] += ml[jj * ldh + l + 64 * q];
+      const int rr = __builtin_amdgcn_readlane(rv, jj);
+      const int nx = (jj + 1 < nvalid) ? __builtin_amdgcn_readlane(rv, jj + 1) : -1;
+      if (nx != rr) {
+        const int64_t seg_s = base + seg0, seg_e = base + jj + 1;
+        const int64_t rp0 = a.rowptr[rr], rp1 = a.rowptr[rr + 1];
+        float* dst;
+        if (rp0 == seg_s && rp1 == seg_e) dst = a.agg + (int64_t)rr * H;
+        else if (rp0 == seg_s) dst = a.cout + tile * H;  // continues into the next tile
+        else dst = a.cin + tile * H;                      // began in the previous tile
+#pragma unroll
+        for (int q = 0; q < UPL; ++q) {
+          if (64 * q + l < H) dst[l + 64 * q] = acc[q];
+          acc[q] = 0.0f;
+        }
+        seg0 = jj + 1;
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
+struct NodeLayerArgs {
+  const float *x_in, *agg, *cin, *cout;
+  const int32_t* rowptr;
+  int64_t n;
+  const float *w1, *b1, *w2, *b2, *g, *bb;  // node MLP
+  // mode 0: next-layer projections
+  const float *we, *be;
+  float *u, *v;
+  // mode 1: decoder + integrator
+  const float *wd1, *bd1, *wd2, *bd2;
+  const float* pos_seq;
+  int T, dim;
+  const float *acc_mean, *acc_std;
+  float *pred, *next_pos, *window_out;
+  float* x_out;
+};
+
+template <int TH>
+SGNN_DEV void load_agg(f32x16 (&a)[TH], const NodeLayerArgs& p, int64_t i) {
+  constexpr int H = 32 * TH;
+  const int32_t r0 = p.rowptr[i], r1 = p.rowptr[i + 1];
+  if (r1 <= r0) {
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a[t][r] = 0.0f;
+    return;
+  }
+  const int32_t t0 = r0 >> 5, t1 = (r1 - 1) >> 5;
+  if (t0 == t1) {
+    load_row_clayout<TH>(a, p.agg + i * H);
+  } else {
+    load_row_clayout<TH>(a, p.cout + (int64_t)t0 * H);
+    add_row_clayout<TH>(a, p.cin + (int64_t)t1 * H);
+  }
+}
+
+template <int TH, int MODE>
+__global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4, ld2 = 2 * H + 4;
+  extern __shared__ float lds[];
+  float* W1 = lds;
+  float* W2 = W1 + H * ld2;
+  float* Wa = W2 + H * ldh;   // mode 0: W1e_i   mode 1: decoder W1
+  float* Wb = Wa + H * ldh;   // mode 0: W1e_j   mode 1: decoder W2 (32 rows)
+  float* b1 = Wb + H * ldh;
+  float* b2 = b1 + H;
+  float* g = b2 + H;
+  float* bb = g + H;
+  float* ba = bb + H;  // mode 0: b1e   mode 1: decoder b1
+  float* bd2 = ba + H;  // mode 1: decoder b2 (32)
+  stage_matrix(W1, ld2, a.w1, 2 * H, H, 2 * H, H, 2 * H);
+  stage_matrix(W2, ldh, a.w2, H, H, H, H, H);
+  if (MODE == 0) {
+    stage_matrix(Wa, ldh, a.we, 3 * H, H, H, H, H);
+    stage_matrix(Wb, ldh, a.we + H, 3 * H, H, H, H, H);
+    stage_vec(ba, a.be, H, H);
+  } else {
+    stage_matrix(Wa, ldh, a.wd1, H, H, H, H, H);
+    stage_matrix(Wb, ldh, a.wd2, H, a.dim + 1, H, 32, H);
+    stage_vec(ba, a.bd1, H, H);
+    stage_vec(bd2, a.bd2, a.dim + 1, 32);
+  }
+  stage_vec(b1, a.b1, H, H);
+  stage_vec(b2, a.b2, H, H);
+  stage_vec(g, a.g, H, H);
+  stage_vec(bb, a.bb, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  for (int64_t blk = blockIdx.x; blk * (32 * kWaves) < a.n; blk += gridDim.x) {
+    const int64_t node0 = blk * (32 * kWaves) + 32 * w;
+    if (node0 >= a.n) continue;
+    const int64_t i = node0 + j;
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    f32x16 ag[TH], x[TH];
+    load_agg<TH>(ag, a, ic);
+    load_row_clayout<TH>(x, a.x_in + ic * H);
+    f32x16 hacc[TH];
+    acc_bias<TH>(hacc, b1);
+    mfma_from_acc<TH, TH>(hacc, W1, ld2, 0, ag);   // graph_network.py:220 cat([aggr, x])
+    mfma_from_acc<TH, TH>(hacc, W1, ld2, H, x);
+    acc_relu<TH>(hacc);
+    f32x16 y[TH];
+    acc_bias<TH>(y, b2);
+    mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
+    acc_layernorm<TH>(y, g, bb);
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x[t][r] = y[t][r] + x[t][r];  // :176 residual
+    if (valid && a.x_out) store_row_clayout<TH>(a.x_out + i * H, x);
+    if (MODE == 0) {
+      store_uv<TH>(Wa, Wb, ba, ldh, x, a.u + i * H, a.v + i * H, valid);
+    } else {
+      f32x16 hd[TH];
+      acc_bias<TH>(hd, ba);
+      mfma_from_acc<TH, TH>(hd, Wa, ldh, 0, x);
+      acc_relu<TH>(hd);
+      f32x16 o[1];
+      acc_bias<1>(o, bd2);
+      mfma_from_acc<1, TH>(o, Wb, ldh, 0, hd);
+      if (valid && h == 0) {  // lanes with h == 0 hold units 0..3 in registers 0..3
+        const int D = a.dim;
+        for (int c = 0; c <= D; ++c) a.pred[i * (D + 1) + c] = o[0][c];
+        const float* p = a.pos_seq + i * a.T * D;
+        for (int c = 0; c < D; ++c) {  // learned_simulator.py:398-411
+          const float acc = __fadd_rn(__fmul_rn(o[0][c], a.acc_std[c]), a.acc_mean[c]);
+          const float pT = p[(a.T - 1) * D + c], pT1 = p[(a.T - 2) * D + c];
+          const float vel = __fsub_rn(pT, pT1);
+          const float np = __fadd_rn(pT, __fadd_rn(vel, acc));
+          a.next_pos[i * D + c] = np;
+          if (a.window_out) a.window_out[(i * a.T + a.T - 1) * D + c] = np;
+        }
+      } else if (valid && a.window_out) {  // evaluate.py:136-139 window shift
+        const float* p = a.pos_seq + i * a.T * a.dim;
+        float* q = a.window_out + i * a.T * a.dim;
+        for (int k = 0; k < (a.T - 1) * a.dim; ++k) q[k] = p[k + a.dim];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+int check_mlp(const sgnn_mlp* m, int in_dim, int hidden, int out_dim, bool need_ln,
+              const char* what) {
+  if (!m || !m->w1 || !m->b1 || !m->w2 || !m->b2)
+    return sgnn::set_error(SGNN_ERR_INVALID, what);
+  if (m->nlin != 2) return sgnn::set_error(SGNN_ERR_UNSUPPORTED, "only nmlp_layers=1 (2 Linear) MLPs");
+  if ((in_dim >= 0 && m->in_dim != in_dim) || m->hidden != hidden || m->out_dim != out_dim)
+    return sgnn::set_error(SGNN_ERR_INVALID, what);
+  if (need_ln && (!m->ln_g || !m->ln_b)) return sgnn::set_error(SGNN_ERR_INVALID, what);
+  return SGNN_OK;
+}
+
+template <typename K>
+void set_lds(K kernel, size_t bytes) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+constexpr size_t kLdsMax = 160 * 1024;
+
+}  // namespace
+
+extern "C" int64_t sgnn_edge_latent_floats(int64_t edge_cap, int32_t hidden) {
+  return ((edge_cap + 31) / 32) * 32 * (int64_t)hidden;
+}
+
+extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int32_t dim,
+                                 const int64_t* types, const float* emb_w, int32_t emb_dim,
+                                 int32_t use_emb, const float* vel_mean, const float* vel_std,
+                                 float radius, const sgnn_mlp* enc, const sgnn_mlp* edge0,
+                                 float* x0, float* u, float* v, void* stream) {
+  using namespace sgnn;
+  if (n <= 0) return SGNN_OK;
+  if (!pos_seq || !vel_mean || !vel_std || !x0 || !u || !v || T < 2 || dim < 1 || dim > 3)
+    return set_error(SGNN_ERR_INVALID, "encode_nodes: bad arguments");
+  if (!enc) return set_error(SGNN_ERR_INVALID, "encode_nodes: enc");
+  const int H = enc->hidden;
+  const int feat = (T - 1) * dim + 1 + (use_emb ? emb_dim : 0);
+  int st = check_mlp(enc, feat, H, H, true, "encode_nodes: encoder MLP shape");
+  if (!st) st = check_mlp(edge0, 3 * H, H, H, true, "encode_nodes: edge0 MLP shape");
+  if (st) return st;
+  if (use_emb && (!types || !emb_w)) return set_error(SGNN_ERR_INVALID, "encode_nodes: embedding");
+  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: hidden must be 64 in this build");
+  EncNodeArgs a{pos_seq, n, T, dim, types, emb_w, emb_dim, use_emb, vel_mean, vel_std, radius,
+                feat, enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, edge0->w1,
+                edge0->b1, x0, u, v};
+  const unsigned grid = persistent_grid(n, 32 * kWaves, 2);
+  const int tkf = (feat + 31) / 32;
+  const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + 3 * H * (H + 4) + 5 * H);
+  if (lds > kLdsMax) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: too many features");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (tkf) {
+    case 1: set_lds(k_encode_nodes<2, 1>, lds);
+      hipLaunchKernelGGL((k_encode_nodes<2, 1>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 2: set_lds(k_encode_nodes<2, 2>, lds);
+      hipLaunchKernelGGL((k_encode_nodes<2, 2>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 3: set_lds(k_encode_nodes<2, 3>, lds);
+      hipLaunchKernelGGL((k_encode_nodes<2, 3>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    default: return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: > 96 node features");
+  }
+  return check_launch("encode_nodes");
+}
+
+extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t dim, float radius,
+                                 const int32_t* rowptr, const int32_t* send, const int32_t* recv,
+                                 int64_t n, int64_t edge_cap, const sgnn_mlp* enc, float* e0t,
+                                 void* stream) {
+  using namespace sgnn;
+  if (n <= 0 || edge_cap <= 0) return SGNN_OK;
+  if (!pos || !rowptr || !send || !recv || !e0t || dim < 1 || dim > 3)
+    return set_error(SGNN_ERR_INVALID, "encode_edges: bad arguments");
+  if (!enc) return set_error(SGNN_ERR_INVALID, "encode_edges: enc");
+  const int H = enc->hidden;
+  int st = check_mlp(enc, dim + 1, H, H, true, "encode_edges: encoder MLP shape");
+  if (st) return st;
+  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_edges: hidden must be 64 in this build");
+  EncEdgeArgs a{pos, pos_stride, dim, radius, rowptr, send, recv, n,
+                enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, e0t};
+  const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 4);
+  const size_t lds = sizeof(float) * (size_t)(H * 5 + H * (H + 4) + 4 * H);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL((k_encode_edges<2>), dim3(grid), dim3(kBlock), lds, s, a);
+  return check_launch("encode_edges");
+}
+
+extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t, float e_scale,
+                               const int32_t* rowptr, const int32_t* send, const int32_t* recv,
+                               int64_t n, int64_t edge_cap, const sgnn_mlp* edge_fn, float* agg,
+                               float* cin, float* cout, void* stream) {
+  using namespace sgnn;
+  if (n <= 0 || edge_cap <= 0) return SGNN_OK;
+  if (!u || !v || !e0t || !rowptr || !send || !recv || !agg || !cin || !cout || !edge_fn)
+    return set_error(SGNN_ERR_INVALID, "edge_layer: null pointer");
+  const int H = edge_fn->hidden;
+  int st = check_mlp(edge_fn, 3 * H, H, H, true, "edge_layer: edge MLP shape");
+  if (st) return st;
+  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer: hidden must be 64 in this build");
+  EdgeLayerArgs a{u, v, e0t, e_scale, rowptr, send, recv, n, edge_fn->w1 + 2 * H, edge_fn->w2,
+                  edge_fn->b2, edge_fn->ln_g, edge_fn->ln_b, agg, cin, cout};
+  const size_t lds = sizeof(float) * (size_t)(2 * H * (H + 4) + 3 * H + kWaves * 32 * (H + 4));
+  const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 2);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  set_lds(k_edge_layer<2>, lds);
+  hipLaunchKernelGGL((k_edge_layer<2>), dim3(grid), dim3(kBlock), lds, s, a);
+  return check_launch("edge_layer");
+}
+
+static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode, void* stream) {
+  using namespace sgnn;
+  const int H = node_fn ? node_fn->hidden : 0;
+  int st = check_mlp(node_fn, 2 * H, H, H, true, "node_layer: node MLP shape");
+  if (st) return st;
+  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "node_layer: hidden must be 64 in this build");
+  a.w1 = node_fn->w1; a.b1 = node_fn->b1; a.w2 = node_fn->w2; a.b2 = node_fn->b2;
+  a.g = node_fn->ln_g; a.bb = node_fn->ln_b;
+  const size_t lds = sizeof(float) * (size_t)(H * (2 * H + 4) + 3 * H * (H + 4) + 5 * H + 32);
+  const unsigned grid = persistent_grid(a.n, 32 * kWaves, 1);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (mode == 0) {
+    set_lds(k_node_layer<2, 0>, lds);
+    hipLaunchKernelGGL((k_node_layer<2, 0>), dim3(grid), dim3(kBlock), lds, s, a);
+  } else {
+    set_lds(k_node_layer<2, 1>, lds);
+    hipLaunchKernelGGL((k_node_layer<2, 1>), dim3(grid), dim3(kBlock), lds, s, a);
+  }
+  return check_launch("node_layer");
+}
+
+extern "C" int sgnn_node_layer(const float* x_in, const float* agg, const float* cin,
+                               const float* cout, const int32_t* rowptr, int64_t n,
+                               const sgnn_mlp* node_fn, const sgnn_mlp* next_edge, float* x_out,
+                               float* u, float* v, void* stream) {
+  using namespace sgnn;
+  if (n <= 0) return SGNN_OK;
+  if (!x_in || !agg || !cin || !cout || !rowptr || !x_out || !u || !v || !next_edge)
+    return set_error(SGNN_ERR_INVALID, "node_layer: null pointer");
+  const int H = node_fn ? node_fn->hidden : 0;
+  int st = check_mlp(next_edge, 3 * H, H, H, true, "node_layer: next edge MLP shape");
+  if (st) return st;
+  NodeLayerArgs a{};
+  a.x_in = x_in; a.agg = agg; a.cin = cin; a.cout = cout; a.rowptr = rowptr; a.n = n;
+  a.we = next_edge->w1; a.be = next_edge->b1; a.u = u; a.v = v; a.x_out = x_out;
+  return node_layer_common(a, node_fn, 0, stream);
+}
+
+extern "C" int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin,
+                                      const float* cout, const int32_t* rowptr, int64_t n,
+                                      const sgnn_mlp* node_fn, const sgnn_mlp* decoder,
+                                      const float* pos_seq, int32_t T, int32_t dim,
+                                      const float* acc_mean, const float* acc_std, float* x_out,
+                                      float* pred, float* next_pos, float* window_out,
+                                      void* stream) {
+  using namespace sgnn;
+  if (n <= 0) return SGNN_OK;
+  if (!x_in || !agg || !cin || !cout || !rowptr || !pos_seq || !acc_mean || !acc_std || !pred ||
+      !next_pos || T < 2 || dim < 1 || dim > 3)
+    return set_error(SGNN_ERR_INVALID, "node_layer_decode: bad arguments");
+  const int H = node_fn ? node_fn->hidden : 0;
+  int st = check_mlp(decoder, H, H, dim + 1, false, "node_layer_decode: decoder MLP shape");
+  if (st) return st;
+  NodeLayerArgs a{};
+  a.x_in = x_in; a.agg = agg; a.cin = cin; a.cout = cout; a.rowptr = rowptr; a.n = n;
+  a.wd1 = decoder->w1; a.bd1 = decoder->b1; a.wd2 = decoder->w2; a.bd2 = decoder->b2;
+  a.pos_seq = pos_seq; a.T = T; a.dim = dim; a.acc_mean = acc_mean; a.acc_std = acc_std;
+  a.pred = pred; a.next_pos = next_pos; a.window_out = window_out; a.x_out = x_out;
+  if (window_out == pos_seq) return set_error(SGNN_ERR_INVALID, "node_layer_decode: window_out aliases pos_seq");
+  return node_layer_common(a, node_fn, 1, stream);
+}

@@ -1,0 +1,25 @@
+// Host-side helpers shared by the sgnn translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/sgnn.h"
+
+namespace sgnn {
+
+int set_error(int status, const char* msg);
+int check_launch(const char* where);
+int scan_exclusive(const int32_t* in, int32_t* out, int64_t len, int32_t* partials,
+                   hipStream_t stream);
+
+// Number of workgroups to launch for a grid-stride kernel: enough to fill
+// the 256 CUs `per_cu` times, never more than the work needs.
+inline unsigned persistent_grid(int64_t work_items, int64_t items_per_wg, int per_cu) {
+  const int64_t need = (work_items + items_per_wg - 1) / items_per_wg;
+  const int64_t cap = 256LL * per_cu;
+  return (unsigned)std::max<int64_t>(1, std::min(need, cap));
+}
+
+}  // namespace sgnn

@@ -1,0 +1,212 @@
+"""Host orchestration of the HIP kernels: parameter packing, HBM workspaces,
+and the per-step launch sequence.  Everything here launches on the current
+torch stream through the C-ABI (no host synchronisation inside a step, so a
+step or a whole rollout can be captured in a HIP graph).
+
+Data layout in HBM (per graph of n particles, hidden H, cap K):
+  rowptr[n+1], send[n*K], recv[n*K]   int32 receiver-sorted CSR (E = rowptr[n])
+  e0t   [ceil(nK/32)][TH][4][64][4]   fp32 encoder edge latent, 32-edge tiles in
+                                      MFMA C-layout order (one 1 KiB load per
+                                      wave instruction)
+  x_a/x_b [n][H] ping-pong node latents; u, v [n][H] per-node halves of the
+  next edge MLP's first Linear; agg [n][H]; cin/cout [nK/32][H] tile carries.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _hip
+from ._hip import SgnnMlp, check, lib, stream_ptr
+
+MAX_NUM_NEIGHBORS = 20  # learned_simulator.py:117
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _linears(seq: nn.Module) -> List[nn.Linear]:
+    return [m for m in seq.modules() if isinstance(m, nn.Linear)]
+
+
+def mlp_struct(seq: nn.Module, has_ln: bool) -> SgnnMlp:
+    """struct sgnn_mlp from a reference-layout Sequential(mlp[, LayerNorm])."""
+    if has_ln:
+        mlp, ln = seq[0], seq[1]
+    else:
+        mlp, ln = seq, None
+    lin = _linears(mlp)
+    for p in [*(l.weight for l in lin), *(l.bias for l in lin)] + ([ln.weight, ln.bias] if ln else []):
+        if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+            raise ValueError("sgnn_amd parameters must be contiguous fp32 GPU tensors "
+                             "(call simulator.to('cuda'))")
+    if len(lin) != 2:
+        raise NotImplementedError("libsgnn_hip implements nmlp_layers=1 (Linear-ReLU-Linear) MLPs")
+    return SgnnMlp(w1=lin[0].weight.data_ptr(), b1=lin[0].bias.data_ptr(),
+                   w2=lin[1].weight.data_ptr(), b2=lin[1].bias.data_ptr(),
+                   ln_g=_ptr(ln.weight) if ln is not None else 0,
+                   ln_b=_ptr(ln.bias) if ln is not None else 0,
+                   in_dim=lin[0].in_features, hidden=lin[0].out_features,
+                   out_dim=lin[-1].out_features, nlin=len(lin))
+
+
+class ParamPack:
+    """The ctypes parameter structs of one EncodeProcessDecode, rebuilt only
+    when a parameter tensor is replaced (e.g. after .to())."""
+
+    def __init__(self, epd: nn.Module):
+        self.key = tuple(p.data_ptr() for p in epd.parameters())
+        self.enc_node = mlp_struct(epd._encoder.node_fn, True)
+        self.enc_edge = mlp_struct(epd._encoder.edge_fn, True)
+        self.edge = [mlp_struct(g.edge_fn, True) for g in epd._processor.gnn_stacks]
+        self.node = [mlp_struct(g.node_fn, True) for g in epd._processor.gnn_stacks]
+        self.dec = mlp_struct(epd._decoder.node_fn, False)
+
+    @staticmethod
+    def get(epd: nn.Module) -> "ParamPack":
+        key = tuple(p.data_ptr() for p in epd.parameters())
+        pack = getattr(epd, "_sgnn_pack", None)
+        if pack is None or pack.key != key:
+            pack = ParamPack(epd)
+            epd._sgnn_pack = pack
+        return pack
+
+
+class StepWorkspace:
+    """HBM buffers for one (n, T, dim, H, K, loop) step shape."""
+
+    def __init__(self, n: int, T: int, dim: int, hidden: int, K: int, loop: bool,
+                 device: torch.device):
+        L = lib()
+        self.n, self.T, self.dim, self.H, self.K, self.loop = n, T, dim, hidden, K, loop
+        cap = K + (0 if loop else 1)
+        self.edge_cap = max(1, n * cap)
+        ntiles = (self.edge_cap + 31) // 32
+        i32 = dict(dtype=torch.int32, device=device)
+        f32 = dict(dtype=torch.float32, device=device)
+        self.radius_ws = torch.empty(int(L.sgnn_radius_workspace_bytes(n, K, int(loop))) + 256,
+                                     dtype=torch.uint8, device=device)
+        self.rowptr = torch.zeros(n + 1, **i32)
+        self.send = torch.empty(self.edge_cap, **i32)
+        self.recv = torch.empty(self.edge_cap, **i32)
+        self.e0t = torch.empty(int(L.sgnn_edge_latent_floats(self.edge_cap, hidden)), **f32)
+        self.x_a = torch.empty(n, hidden, **f32)
+        self.x_b = torch.empty(n, hidden, **f32)
+        self.u = torch.empty(n, hidden, **f32)
+        self.v = torch.empty(n, hidden, **f32)
+        self.agg = torch.empty(n, hidden, **f32)
+        self.cin = torch.empty(ntiles, hidden, **f32)
+        self.cout = torch.empty(ntiles, hidden, **f32)
+
+    def radius_ws_ptr(self) -> int:
+        p = self.radius_ws.data_ptr()
+        return (p + 255) & ~255
+
+    def num_edges(self) -> int:
+        """E (host sync) — only for API/diagnostics, never inside a step."""
+        return int(self.rowptr[self.n].item())
+
+
+def ex_ptr_tensor(counts: Sequence[int], device: torch.device) -> torch.Tensor:
+    ptr = [0]
+    for c in counts:
+        ptr.append(ptr[-1] + int(c))
+    return torch.tensor(ptr, dtype=torch.int64).to(device, non_blocking=False)
+
+
+def counts_of(nparticles_per_example) -> List[int]:
+    """learned_simulator.py:89-94 and evaluate.py:121 (`[tensor(N)]`)."""
+    if isinstance(nparticles_per_example, torch.Tensor):
+        return [int(v) for v in nparticles_per_example.detach().reshape(-1).cpu().tolist()]
+    out = []
+    for v in nparticles_per_example:
+        if isinstance(v, torch.Tensor):
+            out.extend(int(x) for x in v.detach().reshape(-1).cpu().tolist())
+        else:
+            out.append(int(v))
+    return out
+
+
+def radius_graph(ws: StepWorkspace, pos: torch.Tensor, pos_offset_floats: int, pos_stride: int,
+                 ex_ptr: torch.Tensor, n_ex: int, radius: float) -> None:
+    check(lib().sgnn_radius_graph(pos.data_ptr() + 4 * pos_offset_floats, pos_stride, ws.n, ws.dim,
+                                  ex_ptr.data_ptr(), n_ex, float(radius), ws.K, int(ws.loop),
+                                  ws.radius_ws_ptr(), ws.rowptr.data_ptr(), ws.send.data_ptr(),
+                                  ws.recv.data_ptr(), ws.edge_cap, stream_ptr(pos.device)),
+          "sgnn_radius_graph")
+
+
+@dataclass
+class StepInputs:
+    pos_seq: torch.Tensor           # [n, T, dim] fp32 contiguous, GPU
+    ex_ptr: torch.Tensor            # [n_ex+1] int64, GPU
+    n_ex: int
+    types: Optional[torch.Tensor]   # [n] int64 GPU (only with embeddings)
+    vel_mean: torch.Tensor
+    vel_std: torch.Tensor
+    acc_mean: torch.Tensor
+    acc_std: torch.Tensor
+
+
+def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bool, radius: float,
+                 inp: StepInputs, ws: StepWorkspace, pred: torch.Tensor, next_pos: torch.Tensor,
+                 window_out: Optional[torch.Tensor] = None, timers: Optional[list] = None) -> None:
+    """One LearnedSimulator.predict_positions (learned_simulator.py:413-438):
+    radius graph -> encoder -> L interaction layers -> decoder -> Euler."""
+    L = lib()
+    pk = ParamPack.get(epd)
+    n, T, d = ws.n, ws.T, ws.dim
+    s = stream_ptr(inp.pos_seq.device)
+    pos = inp.pos_seq
+    radius_graph(ws, pos, (T - 1) * d, T * d, inp.ex_ptr, inp.n_ex, radius)
+    emb_dim = emb_weight.shape[1] if (use_emb and emb_weight is not None) else 0
+    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, _ptr(inp.types) if use_emb else 0,
+                              _ptr(emb_weight) if use_emb else 0, emb_dim, int(use_emb),
+                              inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius),
+                              ctypes.byref(pk.enc_node), ctypes.byref(pk.edge[0]),
+                              ws.x_a.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), s),
+          "sgnn_encode_nodes")
+    check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius),
+                              ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
+                              ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(), s),
+          "sgnn_encode_edges")
+    x_in, x_out = ws.x_a, ws.x_b
+    nl = len(pk.edge)
+    for k in range(nl):
+        if timers is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        check(L.sgnn_edge_layer(ws.u.data_ptr(), ws.v.data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
+                                ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
+                                ws.edge_cap, ctypes.byref(pk.edge[k]), ws.agg.data_ptr(),
+                                ws.cin.data_ptr(), ws.cout.data_ptr(), s), "sgnn_edge_layer")
+        if timers is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            timers.append((ev0, ev1))
+        if k < nl - 1:
+            check(L.sgnn_node_layer(x_in.data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
+                                    ws.cout.data_ptr(), ws.rowptr.data_ptr(), n,
+                                    ctypes.byref(pk.node[k]), ctypes.byref(pk.edge[k + 1]),
+                                    x_out.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), s),
+                  "sgnn_node_layer")
+            x_in, x_out = x_out, x_in
+        else:
+            check(L.sgnn_node_layer_decode(x_in.data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
+                                           ws.cout.data_ptr(), ws.rowptr.data_ptr(), n,
+                                           ctypes.byref(pk.node[k]), ctypes.byref(pk.dec),
+                                           pos.data_ptr(), T, d, inp.acc_mean.data_ptr(),
+                                           inp.acc_std.data_ptr(), 0, pred.data_ptr(),
+                                           next_pos.data_ptr(), _ptr(window_out), s),
+                  "sgnn_node_layer_decode")
+
+
+def epd_forward(epd, x, edge_index, edge_features):
+    raise NotImplementedError(
+        "EncodeProcessDecode.forward on explicit (x, edge_index, edge_features) is not wired to the "
+        "HIP path yet; use LearnedSimulator.predict_positions / predict_accelerations")

@@ -1,0 +1,114 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's own
+golden outputs and the oracle.  Tolerances (fp32):
+  * graph (edge_index): bit-exact;
+  * decoder output / next position / strain: |got - ref| <= ATOL + RTOL*|ref|
+    with ATOL = 2e-4, RTOL = 1e-4 on the normalised decoder output (O(1)
+    values; the HIP path sums in a different order than MKL/PyG), and the
+    same bound scaled by acc_std on positions.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import golden, hparams, oracle_sim, product_sim
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 2e-4, 1e-4
+FWD_H64 = ["tiny2d_r06", "batch2d_r06", "c1_r15", "c1_r06", "types2d_r06"]
+
+
+def _close(got, ref, atol=ATOL, rtol=RTOL, what=""):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    err = np.abs(got - ref)
+    bound = atol + rtol * np.abs(ref)
+    worst = float((err / bound).max()) if err.size else 0.0
+    print(f"{what}: max|err|={err.max() if err.size else 0:.3e} worst err/bound={worst:.3f}")
+    assert worst <= 1.0, f"{what}: max abs err {err.max():.3e}"
+
+
+@pytest.mark.parametrize("case", FWD_H64 + ["tiny3d_h128"])
+def test_radius_graph_bit_exact(case):
+    z = golden(case)
+    hp = hparams(z)
+    sim = product_sim(z)
+    pos = torch.from_numpy(z["positions"][:, hp["T"] - 1]).cuda()
+    recv_name, send_name = sim._compute_graph_connectivity(pos, z["nparticles_per_example"], hp["R"])
+    ei = torch.stack([recv_name, send_name]).cpu().numpy()
+    np.testing.assert_array_equal(ei, z["edge_index"])
+
+
+@pytest.mark.parametrize("case", FWD_H64)
+def test_predict_positions_matches_reference(case):
+    z = golden(case)
+    hp = hparams(z)
+    sim = product_sim(z)
+    pos = torch.from_numpy(z["positions"][:, :hp["T"]]).cuda()
+    types_ = torch.from_numpy(z["particle_types"]).cuda()
+    nxt, strain = sim.predict_positions(pos, z["nparticles_per_example"], types_)
+    torch.cuda.synchronize()
+    _close(strain.cpu().numpy(), z["strain"], what=f"{case} strain")
+    scale = float(np.max(z["acc_std"]))
+    _close(nxt.cpu().numpy(), z["next_position"], atol=ATOL * scale, rtol=1e-6, what=f"{case} next_pos")
+
+
+def test_rollout_matches_reference():
+    from sgnn_amd import evaluate
+    z = golden("tiny2d_r06")
+    hp = hparams(z)
+    sim = product_sim(z)
+    pos = torch.from_numpy(z["positions"]).cuda()
+    n = pos.shape[0]
+    strains = torch.zeros(pos.shape[1], n, device="cuda")
+    out = evaluate.rollout(sim, pos, torch.zeros(n, dtype=torch.long, device="cuda"), torch.tensor(n),
+                           strains, nsteps=pos.shape[1] - hp["T"], particle_dim=hp["dim"], device="cuda",
+                           input_sequence_length=hp["T"])
+    scale = float(np.max(z["acc_std"]))
+    _close(out["predicted_rollout"], z["rollout_predicted"], atol=4 * ATOL * scale, rtol=1e-6,
+           what="rollout positions")
+    _close(out["predicted_strain"], z["rollout_strain"], atol=4 * ATOL, what="rollout strain")
+
+
+def _lattice_case(nx, ny, radius, seed, n_ex=1):
+    from sgnn_amd import synthetic
+    seqs = [synthetic.trajectory(synthetic.lattice_2d(nx, ny, x0=0.25 + 0.1 * k), 11, seed=seed + k)
+            for k in range(n_ex)]
+    return np.concatenate(seqs, 0), [s.shape[0] for s in seqs]
+
+
+@pytest.mark.parametrize("nx,ny,radius,n_ex", [(250, 200, 0.6, 1), (60, 40, 1.1, 3), (50, 40, 15.0, 2)])
+def test_large_against_oracle(nx, ny, radius, n_ex):
+    """C2-sized (50k) and multi-example graphs vs the oracle (same weights)."""
+    z = golden("c1_r06")
+    from oracle import sgnn_oracle as O
+    from tests.helpers import state_of, stats_of
+    seq, counts = _lattice_case(nx, ny, radius, 21, n_ex)
+    sim = product_sim(z)
+    sim._connectivity_radius = radius
+    osim = O.OracleSimulator(state_of(z), 2, 5, radius, stats_of(z))
+    pos = torch.from_numpy(seq)
+    types_ = torch.zeros(seq.shape[0], dtype=torch.long)
+    ref_next, ref_strain = osim.predict_positions(pos, counts, types_)
+    ei_ref = O.radius_graph(pos[:, -1], counts, radius)
+    r, s = sim._compute_graph_connectivity(pos[:, -1].cuda(), counts, radius)
+    np.testing.assert_array_equal(torch.stack([r, s]).cpu().numpy(), ei_ref.numpy())
+    nxt, strain = sim.predict_positions(pos.cuda(), counts, types_.cuda())
+    _close(strain.cpu().numpy(), ref_strain.numpy(), what=f"{nx}x{ny} r={radius} strain")
+
+
+def test_radius_graph_random_vs_bruteforce():
+    """Random clouds, several examples, loop on/off, cap binding, a NaN particle."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import engine
+    g = torch.Generator().manual_seed(3)
+    for trial, (n, dim, r, loop) in enumerate([(700, 2, 0.9, True), (500, 3, 1.3, True),
+                                               (600, 2, 3.0, False), (400, 3, 0.5, False)]):
+        pos = torch.rand(n, dim, generator=g) * 10.0
+        pos[5] = float("nan")
+        counts = [n // 3, n // 3, n - 2 * (n // 3)]
+        ref = O.radius_graph(pos, counts, r, loop=loop, method="bruteforce")
+        ws = engine.StepWorkspace(n, 2, dim, 64, 20, loop, torch.device("cuda"))
+        engine.radius_graph(ws, pos.cuda(), 0, dim, engine.ex_ptr_tensor(counts, "cuda"), 3, r)
+        e = ws.num_edges()
+        got = torch.stack([ws.send[:e], ws.recv[:e]]).cpu().to(torch.int64)
+        np.testing.assert_array_equal(got.numpy(), ref.numpy(), err_msg=f"trial {trial}")
