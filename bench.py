@@ -109,6 +109,21 @@ def cpu_baseline(sim, window, radius, L, steps):
             "seconds": dt}
 
 
+def profiled_traffic(workload, kernel="k_edge_layer"):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/*_summary.json, FETCH_SIZE x2 + WRITE_SIZE), newest matching tag."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
+        d = json.load(open(path))
+        if d.get("workload") != workload:
+            continue
+        for k, v in d["kernels"].items():
+            if k.startswith(kernel) and "hbm_bytes" in v:
+                best = (v["hbm_bytes"], os.path.relpath(path, ROOT))
+    return best
+
+
 def main():
     args = parse()
     world, rank, local = init_dist(args)
@@ -166,6 +181,7 @@ def main():
     edge_avg_s = float(np.mean(edge_ms)) * 1e-3
     flops_edge = E * (2 * H * H * 2)
     achieved = flops_edge / edge_avg_s
+    prof = profiled_traffic(args.workload)
     out = {
         "metric": "particle-steps/sec (2D Taylor-impact rollout)",
         "value": value,
@@ -187,7 +203,9 @@ def main():
         "M_edge_messages_per_s": E * L * args.steps * world / dt / 1e6,
         "roofline": {"bound": "mfma", "kernel": "k_edge_layer", "achieved": achieved / 1e12,
                      "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK,
-                     "traffic": None, "avg_launch_us": edge_avg_s * 1e6,
+                     "traffic": prof[0] if prof else None,
+                     "traffic_unit": "bytes/launch (rocprofv3 PMC)",
+                     "traffic_source": prof[1] if prof else None, "avg_launch_us": edge_avg_s * 1e6,
                      "flops_per_launch": flops_edge,
                      "edge_share_of_step": float(np.sum(edge_ms)) / (dt_events * 1e3)},
     }

@@ -2,13 +2,14 @@
 // reached by sgnn/single_scale/learned_simulator.py:116-117).
 //
 // Pipeline (5-9 launches, no host sync, capturable in a hipGraph):
-//   1. k_cell_assign   particle -> (example, cell = floor(p / (1.01 r))) ->
-//                      hash bucket; histogram with one atomic per particle
+//   0. k_bbox          bounding box of the finite coordinates (device atomics)
+//   1. k_cell_assign   particle -> (example, dense cell of side 1.01 r, grown
+//                      x2 until the grid fits the workspace); histogram
 //   2. scan            bucket counts -> bucket starts
 //   3. k_cell_scatter  counting-sort particle ids into bucket order
-//   4. k_radius_query  one wave per query particle: walks the 3^d neighbour
-//                      cells (each a contiguous bucket span, 64 candidates per
-//                      wave step, coalesced id loads), keeps in-range
+//   4. k_radius_query  one wave per query particle: walks the 3^(d-1) row
+//                      spans of its neighbour cells as one concatenated list
+//                      (64 candidates per wave step), keeps in-range
 //                      same-example candidates, and maintains the `cap`
 //                      smallest sender ids with a 64-lane bitonic sort +
 //                      merge in registers (torch_cluster's CUDA rule: first K
@@ -97,22 +98,113 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_add(int32_t* out, int64_t l
   }
 }
 
-SGNN_DEV int cell_coord(float x, float inv_cell) {
-  float q = floorf(x * inv_cell);
-  if (!(q == q)) q = 0.0f;
-  q = fminf(fmaxf(q, -1048576.0f), 1048576.0f);
-  return (int)q;
+// ---------------------------------------------------------------------------
+// Dense cell grid derived on the device from the particles' bounding box, so
+// no host sync: the three cells of one grid row (dx = -1..1) are contiguous in
+// cell order, a 2D query walks 3 spans (3D: 9) of the cell-sorted id array.
+struct Grid {  // 28 bytes, stored at bbox + 8 (8 words reserved)
+  float lo[3];
+  float inv_cell;
+  int g[3];
+};
+
+static_assert(sizeof(Grid) <= 32, "Grid must fit the 8 reserved words");
+
+// order-preserving float <-> uint so atomicMax/Min work on zero-initialised words
+SGNN_DEV uint32_t f2ord(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+SGNN_DEV float ord2f(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
 }
 
-SGNN_DEV uint32_t cell_hash(int cx, int cy, int cz, int ex, uint32_t mask) {
-  uint32_t h = (uint32_t)cx * 0x9E3779B1u + (uint32_t)cy * 0x85EBCA77u + (uint32_t)cz * 0xC2B2AE3Du +
-               (uint32_t)ex * 0x27D4EB2Fu;
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 12;
-  h *= 0x297A2D39u;
-  h ^= h >> 15;
-  return h & mask;
+// bbox words: [0..2] = ~ord(min_d) (atomicMax of the complement = min),
+// [3..5] = ord(max_d), [6] = arrival counter, [8..15] = the derived Grid
+// (written by the last-arriving block: agent-scope atomics + fence fan-in).
+__global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, int64_t n, int dim,
+                                              int n_ex, float cell0, int64_t max_cells,
+                                              uint32_t* bbox);
+
+// Every thread derives the same grid from the bbox (identical float ops).
+SGNN_DEV Grid make_grid(const uint32_t (&bbox)[6], int dim, int n_ex, float cell0, int64_t max_cells) {
+  Grid G;
+  float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
+  for (int d = 0; d < 3; ++d) {
+    if (d < dim && bbox[d] != 0u && bbox[3 + d] != 0u) {
+      lo[d] = ord2f(~bbox[d]);
+      hi[d] = ord2f(bbox[3 + d]);
+    }
+    G.lo[d] = lo[d];
+  }
+  float cell = cell0;
+  for (int it = 0; it < 64; ++it) {
+    int64_t tot = n_ex;
+    for (int d = 0; d < 3; ++d) {
+      const float ext = (hi[d] - lo[d]) / cell;
+      G.g[d] = d < dim ? (int)fminf(ext, 1.0e7f) + 1 : 1;
+      tot *= G.g[d];
+    }
+    if (tot <= max_cells) break;
+    cell *= 2.0f;
+  }
+  G.inv_cell = 1.0f / cell;
+  return G;
+}
+
+__global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, int64_t n, int dim,
+                                              int n_ex, float cell0, int64_t max_cells,
+                                              uint32_t* bbox) {
+  __shared__ uint32_t red[6][4];
+  __shared__ bool last;
+  uint32_t v[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    for (int d = 0; d < dim; ++d) {
+      const float x = pos[i * stride + d];
+      if (isfinite(x)) {
+        const uint32_t o = f2ord(x);
+        v[d] = max(v[d], ~o);
+        v[3 + d] = max(v[3 + d], o);
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    uint32_t a = v[k];
+    for (int o = 32; o > 0; o >>= 1) a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
+    if (lane == 0) red[k][w] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    uint32_t a = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) a = max(a, red[threadIdx.x][k]);
+    if (a) atomicMax(&bbox[threadIdx.x], a);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t t = __hip_atomic_fetch_add(&bbox[6], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    uint32_t b[6];
+    for (int k = 0; k < 6; ++k)
+      b[k] = __hip_atomic_load(&bbox[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const Grid G = make_grid(b, dim, n_ex, cell0, max_cells);
+    Grid* out = reinterpret_cast<Grid*>(bbox + 8);
+    *out = G;
+  }
+}
+
+SGNN_DEV int cell_of(float x, float lo, float inv_cell, int g) {
+  float q = floorf((x - lo) * inv_cell);
+  if (!(q == q)) q = 0.0f;
+  q = fminf(fmaxf(q, 0.0f), (float)(g - 1));
+  return (int)q;
 }
 
 SGNN_DEV float dist2_ordered(const float* a, const float* b, int dim) {
@@ -127,32 +219,31 @@ SGNN_DEV float dist2_ordered(const float* a, const float* b, int dim) {
 
 __global__ __launch_bounds__(256) void k_cell_assign(const float* pos, int64_t stride, int64_t n,
                                                      int dim, const int64_t* ex_ptr, int n_ex,
-                                                     float inv_cell, uint32_t mask,
-                                                     int32_t* bucket_of, int32_t* ex_of,
-                                                     int32_t* count) {
+                                                     const uint32_t* bbox, int32_t* cell_of_p,
+                                                     int32_t* ex_of, int32_t* count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const Grid G = *reinterpret_cast<const Grid*>(bbox + 8);
   int lo = 0, hi = n_ex - 1;  // largest b with ex_ptr[b] <= i
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (ex_ptr[mid] <= i) lo = mid; else hi = mid - 1;
   }
   const float* p = pos + i * stride;
-  const int cx = cell_coord(p[0], inv_cell);
-  const int cy = dim > 1 ? cell_coord(p[1], inv_cell) : 0;
-  const int cz = dim > 2 ? cell_coord(p[2], inv_cell) : 0;
-  const uint32_t b = cell_hash(cx, cy, cz, lo, mask);
-  bucket_of[i] = (int32_t)b;
+  int c[3] = {0, 0, 0};
+  for (int d = 0; d < dim; ++d) c[d] = cell_of(p[d], G.lo[d], G.inv_cell, G.g[d]);
+  const int32_t key = (int32_t)((((int64_t)lo * G.g[2] + c[2]) * G.g[1] + c[1]) * G.g[0] + c[0]);
+  cell_of_p[i] = key;
   ex_of[i] = lo;
-  atomicAdd(&count[b], 1);
+  atomicAdd(&count[key], 1);
 }
 
-__global__ __launch_bounds__(256) void k_cell_scatter(int64_t n, const int32_t* bucket_of,
+__global__ __launch_bounds__(256) void k_cell_scatter(int64_t n, const int32_t* cell_of_p,
                                                       const int32_t* start, int32_t* fill,
                                                       int32_t* order) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int32_t b = bucket_of[i];
+  const int32_t b = cell_of_p[i];
   order[start[b] + atomicAdd(&fill[b], 1)] = (int32_t)i;
 }
 
@@ -180,55 +271,71 @@ SGNN_DEV int bitonic_merge64(int key, int lane) {
 }
 
 __global__ __launch_bounds__(256) void k_radius_query(
-    const float* pos, int64_t stride, int64_t n, int dim, float r2, float inv_cell,
-    uint32_t mask, const int32_t* ex_of, const int32_t* start, const int32_t* order, int cap,
-    int loop, int32_t* nbr, int32_t* deg) {
+    const float* pos, int64_t stride, int64_t n, int dim, float r2,
+    const uint32_t* bbox, const int32_t* cell_of_p, const int32_t* ex_of,
+    const int32_t* start, const int32_t* order, int cap, int loop, int32_t* nbr, int32_t* deg) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (i == 0 && lane == 0) deg[n] = 0;  // scan sentinel -> rowptr[n] = E
   if (i >= n) return;
+  const Grid G = *reinterpret_cast<const Grid*>(bbox + 8);
   float pi[3] = {0.0f, 0.0f, 0.0f};
   for (int d = 0; d < dim; ++d) pi[d] = pos[i * stride + d];
-  const int ex = ex_of[i];
-  int ci[3] = {cell_coord(pi[0], inv_cell), dim > 1 ? cell_coord(pi[1], inv_cell) : 0,
-               dim > 2 ? cell_coord(pi[2], inv_cell) : 0};
+  const int key = cell_of_p[i];
+  int c[3];
+  {
+    int k = key;
+    c[0] = k % G.g[0]; k /= G.g[0];
+    c[1] = k % G.g[1]; k /= G.g[1];
+    c[2] = k % G.g[2];
+  }
+  const int rowbase = key - c[0];  // key of cell (0, cy, cz) of this example
+  // the 3^(dim-1) row spans of the neighbourhood, concatenated
+  int s0[9], pre[10];
+  int nsp = 0;
+  pre[0] = 0;
+  const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
+  for (int dz = -1; dz <= 1; ++dz) {
+    const int z = c[2] + dz;
+    if (z < 0 || z >= G.g[2]) continue;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int y = c[1] + dy;
+      if (y < 0 || y >= G.g[1]) continue;
+      const int rk = rowbase + (dz * G.g[1] + dy) * G.g[0];
+      const int a = start[rk + x0], b = start[rk + x1 + 1];
+      s0[nsp] = a;
+      pre[nsp + 1] = pre[nsp] + (b - a);
+      ++nsp;
+    }
+  }
+  const int total = pre[nsp];
   int top = INT32_MAX;  // lanes [0, cnt) hold the kept ids, ascending
   int cnt = 0;
-  const int zr = dim > 2 ? 1 : 0, yr = dim > 1 ? 1 : 0;
-  for (int dz = -zr; dz <= zr; ++dz)
-    for (int dy = -yr; dy <= yr; ++dy)
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int tc[3] = {ci[0] + dx, ci[1] + dy, ci[2] + dz};
-        const uint32_t b = cell_hash(tc[0], tc[1], tc[2], ex, mask);
-        const int s0 = start[b], s1 = start[b + 1];
-        for (int base = s0; base < s1; base += 64) {
-          const int t = base + lane;
-          int key = INT32_MAX;
-          if (t < s1) {
-            const int j = order[t];
-            if (ex_of[j] == ex) {
-              float pj[3] = {0.0f, 0.0f, 0.0f};
-              for (int d = 0; d < dim; ++d) pj[d] = pos[(int64_t)j * stride + d];
-              bool same_cell = true;
-              for (int d = 0; d < dim; ++d) same_cell &= cell_coord(pj[d], inv_cell) == tc[d];
-              if (same_cell && dist2_ordered(pj, pi, dim) < r2) key = j;
-            }
-          }
-          if (cnt >= cap) {
-            const int kth = __shfl(top, cap - 1, 64);
-            if (key >= kth) key = INT32_MAX;
-          }
-          const unsigned long long bal = __ballot(key != INT32_MAX);
-          if (bal) {
-            const int nnew = __popcll(bal);
-            key = bitonic_sort64(key, lane);
-            const int other = __shfl(key, 63 - lane, 64);
-            top = bitonic_merge64(min(top, other), lane);
-            if (lane >= cap) top = INT32_MAX;
-            cnt = min(cnt + nnew, cap);
-          }
-        }
-      }
+  for (int base = 0; base < total; base += 64) {
+    const int t = base + lane;
+    int key_j = INT32_MAX;
+    if (t < total) {
+      int k = 0;
+      while (k + 1 < nsp && t >= pre[k + 1]) ++k;
+      const int j = order[s0[k] + (t - pre[k])];
+      float pj[3] = {0.0f, 0.0f, 0.0f};
+      for (int d = 0; d < dim; ++d) pj[d] = pos[(int64_t)j * stride + d];
+      if (dist2_ordered(pj, pi, dim) < r2) key_j = j;
+    }
+    if (cnt >= cap) {
+      const int kth = __shfl(top, cap - 1, 64);
+      if (key_j >= kth) key_j = INT32_MAX;
+    }
+    const unsigned long long bal = __ballot(key_j != INT32_MAX);
+    if (bal) {
+      const int nnew = __popcll(bal);
+      key_j = bitonic_sort64(key_j, lane);
+      const int other = __shfl(key_j, 63 - lane, 64);
+      top = bitonic_merge64(min(top, other), lane);
+      if (lane >= cap) top = INT32_MAX;
+      cnt = min(cnt + nnew, cap);
+    }
+  }
   if (!loop) {  // torch_cluster: K+1 nearest-by-index, then drop the self loop
     const unsigned long long self = __ballot(lane < cnt && top == (int)i);
     if (self) {
@@ -240,6 +347,7 @@ __global__ __launch_bounds__(256) void k_radius_query(
   }
   if (lane < cnt) nbr[i * cap + lane] = top;
   if (lane == 0) deg[i] = cnt;
+  (void)ex_of;
 }
 
 __global__ __launch_bounds__(256) void k_compact(int64_t n, int cap, const int32_t* nbr,
@@ -255,8 +363,9 @@ __global__ __launch_bounds__(256) void k_compact(int64_t n, int cap, const int32
 }
 
 struct RadiusWs {
-  uint32_t nbuckets;
+  uint32_t nbuckets;  // cell capacity (cells of all examples)
   int32_t *count, *fill, *start, *bucket_of, *ex_of, *order, *nbr, *deg, *partials;
+  uint32_t* bbox;
   size_t bytes;
 };
 
@@ -277,8 +386,9 @@ RadiusWs radius_layout(int64_t n, int32_t K, int32_t loop, void* base) {
     off += align_up(sizeof(int32_t) * (size_t)count);
     return r;
   };
-  w.count = take(2 * (int64_t)m + 2);  // count[m+1] and fill[m+1]: one memset
+  w.count = take(2 * (int64_t)m + 2 + 16);  // count[m+1], fill[m+1], bbox[16]: one memset
   w.fill = w.count + m + 1;
+  w.bbox = reinterpret_cast<uint32_t*>(w.fill + m + 1);
   w.start = take(m + 1);
   w.bucket_of = take(n);
   w.ex_of = take(n);
@@ -334,20 +444,24 @@ extern "C" int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n
   if (!pos || !ex_ptr || !workspace || !rowptr || !send || !recv)
     return set_error(SGNN_ERR_INVALID, "radius_graph: null pointer");
   RadiusWs w = radius_layout(n, K, loop, workspace);
-  const float cell = radius * 1.01f;  // margin keeps |dp| < r inside +-1 cell under rounding
-  const float inv_cell = 1.0f / cell;
+  if ((int64_t)n_ex > (int64_t)w.nbuckets)
+    return set_error(SGNN_ERR_UNSUPPORTED, "radius_graph: more examples than cell capacity (2n)");
+  const float cell0 = radius * 1.01f;  // margin keeps |dp| < r inside +-1 cell under rounding
   const float r2 = radius * radius;
+  const int64_t max_cells = w.nbuckets;
   const unsigned nblk = (unsigned)((n + 255) / 256);
-  (void)hipMemsetAsync(w.count, 0, sizeof(int32_t) * (2 * (size_t)w.nbuckets + 2), stream);
+  (void)hipMemsetAsync(w.count, 0, sizeof(int32_t) * (2 * (size_t)w.nbuckets + 2 + 16), stream);
+  hipLaunchKernelGGL(k_bbox, dim3(std::min<unsigned>(nblk, 128)), dim3(256), 0, stream, pos,
+                     pos_stride, n, dim, n_ex, cell0, max_cells, w.bbox);
   hipLaunchKernelGGL(k_cell_assign, dim3(nblk), dim3(256), 0, stream, pos, pos_stride, n, dim,
-                     ex_ptr, n_ex, inv_cell, w.nbuckets - 1, w.bucket_of, w.ex_of, w.count);
+                     ex_ptr, n_ex, w.bbox, w.bucket_of, w.ex_of, w.count);
   int st = scan_exclusive(w.count, w.start, (int64_t)w.nbuckets + 1, w.partials, stream);
   if (st) return st;
   hipLaunchKernelGGL(k_cell_scatter, dim3(nblk), dim3(256), 0, stream, n, w.bucket_of, w.start,
                      w.fill, w.order);
   hipLaunchKernelGGL(k_radius_query, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, pos,
-                     pos_stride, n, dim, r2, inv_cell, w.nbuckets - 1, w.ex_of, w.start, w.order,
-                     cap, loop, w.nbr, w.deg);
+                     pos_stride, n, dim, r2, w.bbox, w.bucket_of, w.ex_of,
+                     w.start, w.order, cap, loop, w.nbr, w.deg);
   st = scan_exclusive(w.deg, rowptr, n + 1, w.partials, stream);
   if (st) return st;
   const int64_t tot = n * cap;
