@@ -40,6 +40,17 @@ typedef struct sgnn_mlp {
   int32_t in_dim, hidden, out_dim, nlin;
 } sgnn_mlp;
 
+/* Optional activation saves of the training forward (NULL pointer / NULL
+ * struct = inference).  Edge tensors use the 32-edge tiled layout of e0t;
+ * node tensors are row-major [N][H]; rstd is one float per item. */
+typedef struct sgnn_saves {
+  float* h;     /* post-ReLU hidden of the MLP's first Linear */
+  float* yhat;  /* LayerNorm-normalised (pre-affine) output */
+  float* rstd;  /* LayerNorm 1/std per item */
+  float* agg;   /* node layers: resolved aggregate [N][H] */
+  float* hd;    /* node_layer_decode: decoder hidden [N][H] */
+} sgnn_saves;
+
 const char* sgnn_version(void);
 const char* sgnn_last_error(void);
 
@@ -76,7 +87,7 @@ int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int32_t dim,
                       const int64_t* types, const float* emb_w, int32_t emb_dim,
                       int32_t use_emb, const float* vel_mean, const float* vel_std,
                       float radius, const sgnn_mlp* enc, const sgnn_mlp* edge0,
-                      float* x0, float* u, float* v, void* stream);
+                      float* x0, float* u, float* v, const sgnn_saves* saves, void* stream);
 
 /* Encoder, edge side: edge features (learned_simulator.py:299-312:
  * (p_s - p_r)/R and its norm) fused with Encoder.edge_fn (graph_network.py:
@@ -86,7 +97,7 @@ int64_t sgnn_edge_latent_floats(int64_t edge_cap, int32_t hidden);
 int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t dim, float radius,
                       const int32_t* rowptr, const int32_t* send, const int32_t* recv,
                       int64_t n, int64_t edge_cap, const sgnn_mlp* enc, float* e0t,
-                      void* stream);
+                      const sgnn_saves* saves, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Processor, edge half of one InteractionNetwork (graph_network.py:150-199):
@@ -100,14 +111,15 @@ int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t dim, float r
 int sgnn_edge_layer(const float* u, const float* v, const float* e0t, float e_scale,
                     const int32_t* rowptr, const int32_t* send, const int32_t* recv,
                     int64_t n, int64_t edge_cap, const sgnn_mlp* edge_fn, float* agg,
-                    float* cin, float* cout, void* stream);
+                    float* cin, float* cout, const sgnn_saves* saves, void* stream);
 
 /* Processor, node half (graph_network.py:201-222 and the residual :176):
  *   x_out = x_in + LN(W2 relu(W1 [agg, x_in] + b1) + b2)
  * fused with the next layer's projections (u, v as sgnn_encode_nodes). */
 int sgnn_node_layer(const float* x_in, const float* agg, const float* cin, const float* cout,
                     const int32_t* rowptr, int64_t n, const sgnn_mlp* node_fn,
-                    const sgnn_mlp* next_edge, float* x_out, float* u, float* v, void* stream);
+                    const sgnn_mlp* next_edge, float* x_out, float* u, float* v,
+                    const sgnn_saves* saves, void* stream);
 
 /* Last processor node half fused with the Decoder (graph_network.py:321-333,
  * no LayerNorm) and LearnedSimulator._decoder_postprocessor
@@ -122,7 +134,87 @@ int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin
                            const sgnn_mlp* node_fn, const sgnn_mlp* decoder,
                            const float* pos_seq, int32_t T, int32_t dim,
                            const float* acc_mean, const float* acc_std, float* x_out,
-                           float* pred, float* next_pos, float* window_out, void* stream);
+                           float* pred, float* next_pos, float* window_out,
+                           const sgnn_saves* saves, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Training backward: reverse of predict_accelerations (learned_simulator.py:
+ * 440-491) + the loss of train.py:257-268, i.e. what loss.backward() does
+ * through PyG/torch autograd.  Call order per step (L layers):
+ *   sgnn_transpose_csr (sender-sorted CSR for dV; once per graph)
+ *   sgnn_decoder_loss_bwd                 -> g = dL/dx_L
+ *   for k = L-1 .. 0:
+ *     sgnn_node_layer_bwd(k, g)           -> dagg, dx'
+ *     sgnn_edge_layer_bwd(k, dagg)        -> dU (+carries), dh rows, dE0
+ *     sgnn_uv_bwd(k, dx', dU, dh)         -> g = dL/dx_k
+ *   sgnn_encode_nodes_bwd(g), sgnn_encode_edges_bwd(dE0)
+ *   sgnn_reduce_slabs                     -> parameter gradients
+ * Each *_bwd launches `nslab` persistent workgroups and writes one partial
+ * slab of sgnn_bwd_slab_floats(kind, H, feat) floats per workgroup.  Slab
+ * layouts (row-major, W = 4 waves per workgroup, vectors as W partial rows):
+ *   EDGE    : dW2[H][H] | dW1e[H][H] (x 2^k in the reduce) | db2, dgamma, dbeta [W][H]
+ *   NODE    : dW2[H][H] | dW1[H][2H] | db1, db2, dgamma, dbeta [W][H]
+ *   UV      : dW1[:, 0:2H] as [H][2H] | db1 [W][H]
+ *   DECODER : dW2[32][H] (rows > dim zero) | dW1[H][H] | db2 [W][32] | db1 [W][H] |
+ *             loss [W][8] = (total, x, y, z, strain) sums of squared errors
+ *   ENC_NODE: dW2[H][H] | dW1[H][32*ceil(F/32)] | db1, db2, dgamma, dbeta [W][H]
+ *   ENC_EDGE: dW2[H][H] | dW1[H][32] | db1, db2, dgamma, dbeta [W][H]
+ * ------------------------------------------------------------------------- */
+enum { SGNN_SLAB_EDGE = 0, SGNN_SLAB_NODE = 1, SGNN_SLAB_UV = 2, SGNN_SLAB_DECODER = 3,
+       SGNN_SLAB_ENC_NODE = 4, SGNN_SLAB_ENC_EDGE = 5 };
+int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat);
+
+/* out[r*dst_ld + c] (+)= scale * sum_{g<nslab} sum_{q<nrep}
+ *                         src[g*slab_stride + offset + q*rep_stride + r*src_ld + c] */
+typedef struct sgnn_reduce_desc {
+  const float* src; float* dst;
+  int64_t slab_stride, offset, rep_stride;
+  int32_t nslab, nrep, src_ld, nrows, ncols, dst_ld, accumulate;
+  float scale;
+} sgnn_reduce_desc;
+int sgnn_reduce_slabs(const sgnn_reduce_desc* descs_dev, int32_t ndesc, int64_t max_elems,
+                      void* stream);
+
+size_t sgnn_transpose_workspace_bytes(int64_t n, int64_t edge_cap);
+int sgnn_transpose_csr(const int32_t* rowptr, const int32_t* send, int64_t n, int64_t edge_cap,
+                       void* workspace, int32_t* tptr, int32_t* tperm, void* stream);
+
+/* dpred != NULL: use it as dL/dpred [n][dim+1] (autograd path) instead of the
+ * fused loss gradient 2*w*(pred - target)*inv_count of train.py:257-268. */
+int sgnn_decoder_loss_bwd(const float* pred, const float* pos_seq, const float* next_pos,
+                          const float* noise, const float* next_strain, const float* acc_mean,
+                          const float* acc_std, int64_t n, int32_t T, int32_t dim, float w_pos,
+                          float w_strain, float inv_count, const float* dpred,
+                          const float* hd_save, const float* x_last, const sgnn_mlp* decoder,
+                          float* g, float* slab, int32_t nslab, void* stream);
+int sgnn_node_layer_bwd(const float* g, int64_t n, const float* yhat_save,
+                        const float* rstd_save, const float* h_save, const float* agg_save,
+                        const float* x_in, const sgnn_mlp* node_fn, float* dagg, float* dxp,
+                        float* slab, int32_t nslab, void* stream);
+int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t* send,
+                        const int32_t* recv, int64_t n, const float* h_save,
+                        const float* yhat_save, const float* rstd_save, const float* e0t,
+                        float e_scale, const sgnn_mlp* edge_fn, float* du, float* cin,
+                        float* cout, float* dh_rows, float* de0t, int32_t de0_accumulate,
+                        float* slab, int32_t nslab, void* stream);
+int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, const float* cout,
+                const int32_t* rowptr, const float* dh_rows, const int32_t* tptr,
+                const int32_t* tperm, const float* x_in, int64_t n, const sgnn_mlp* edge_fn,
+                float* g, float* slab, int32_t nslab, void* stream);
+int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
+                          int32_t dim, const float* vel_mean, const float* vel_std, float radius,
+                          const float* h_save, const float* yhat_save, const float* rstd_save,
+                          const sgnn_mlp* enc, float* slab, int32_t nslab, void* stream);
+int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_stride, int32_t dim,
+                          float radius, const int32_t* rowptr, const int32_t* send,
+                          const int32_t* recv, int64_t n, const float* yhat_save,
+                          const float* rstd_save, const sgnn_mlp* enc, float* slab,
+                          int32_t nslab, void* stream);
+
+/* Fused Adam over a flat fp32 buffer; same update as torch.optim.Adam
+ * (amsgrad=False, weight_decay=0) used by train.py:199,271-273. step >= 1. */
+int sgnn_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   float lr, float beta1, float beta2, float eps, int64_t step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,24 @@ class SgnnMlp(ctypes.Structure):
 
 P_MLP = ctypes.POINTER(SgnnMlp)
 
+
+class SgnnSaves(ctypes.Structure):
+    """struct sgnn_saves (include/sgnn.h)."""
+    _fields_ = [("h", c_void_p), ("yhat", c_void_p), ("rstd", c_void_p), ("agg", c_void_p),
+                ("hd", c_void_p)]
+
+
+class SgnnReduceDesc(ctypes.Structure):
+    """struct sgnn_reduce_desc (include/sgnn.h)."""
+    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("slab_stride", c_int64), ("offset", c_int64),
+                ("rep_stride", c_int64), ("nslab", c_int32), ("nrep", c_int32), ("src_ld", c_int32),
+                ("nrows", c_int32), ("ncols", c_int32), ("dst_ld", c_int32), ("accumulate", c_int32),
+                ("scale", c_float)]
+
+
+P_SAVES = ctypes.POINTER(SgnnSaves)
+SLAB_EDGE, SLAB_NODE, SLAB_UV, SLAB_DECODER, SLAB_ENC_NODE, SLAB_ENC_EDGE = range(6)
+
 # name -> (restype, argtypes); every symbol include/sgnn.h declares
 SIGNATURES = {
     "sgnn_version": (ctypes.c_char_p, []),
@@ -38,19 +56,48 @@ SIGNATURES = {
                                          c_void_p, c_int64, c_void_p]),
     "sgnn_encode_nodes": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
                                          c_int32, c_int32, c_void_p, c_void_p, c_float, P_MLP,
-                                         P_MLP, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                         P_MLP, c_void_p, c_void_p, c_void_p, P_SAVES, c_void_p]),
     "sgnn_edge_latent_floats": (c_int64, [c_int64, c_int32]),
     "sgnn_encode_edges": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
-                                         c_void_p, c_int64, c_int64, P_MLP, c_void_p, c_void_p]),
+                                         c_void_p, c_int64, c_int64, P_MLP, c_void_p, P_SAVES,
+                                         c_void_p]),
     "sgnn_edge_layer": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
                                        c_void_p, c_int64, c_int64, P_MLP, c_void_p, c_void_p,
-                                       c_void_p, c_void_p]),
+                                       c_void_p, P_SAVES, c_void_p]),
     "sgnn_node_layer": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                                       P_MLP, P_MLP, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                       P_MLP, P_MLP, c_void_p, c_void_p, c_void_p, P_SAVES,
+                                       c_void_p]),
     "sgnn_node_layer_decode": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_int64, P_MLP, P_MLP, c_void_p, c_int32, c_int32,
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                              c_void_p, c_void_p]),
+                                              c_void_p, P_SAVES, c_void_p]),
+    "sgnn_bwd_slab_floats": (c_int64, [c_int32, c_int32, c_int32]),
+    "sgnn_reduce_slabs": (ctypes.c_int, [c_void_p, c_int32, c_int64, c_void_p]),
+    "sgnn_transpose_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64]),
+    "sgnn_transpose_csr": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
+                                          c_void_p, c_void_p]),
+    "sgnn_decoder_loss_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_void_p, c_int64, c_int32, c_int32, c_float,
+                                             c_float, c_float, c_void_p, c_void_p, c_void_p, P_MLP,
+                                             c_void_p, c_void_p, c_int32, c_void_p]),
+    "sgnn_node_layer_bwd": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, P_MLP, c_void_p, c_void_p, c_void_p,
+                                           c_int32, c_void_p]),
+    "sgnn_edge_layer_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_float, P_MLP,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_int32, c_void_p, c_int32, c_void_p]),
+    "sgnn_uv_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_int64, P_MLP, c_void_p,
+                                   c_void_p, c_int32, c_void_p]),
+    "sgnn_encode_nodes_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                             c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                             c_void_p, P_MLP, c_void_p, c_int32, c_void_p]),
+    "sgnn_encode_edges_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_float,
+                                             c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                             c_void_p, P_MLP, c_void_p, c_int32, c_void_p]),
+    "sgnn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,
+                                      c_float, c_float, c_float, c_int64, c_void_p]),
 }
 
 _LIB: Optional[ctypes.CDLL] = None

@@ -196,3 +196,148 @@ SGNN_DEV void store_row_clayout(float* row, const f32x16 (&x)[TH]) {
       st4(row + 32 * t + 8 * g + 4 * h, v);
     }
 }
+
+// LayerNorm that also returns the normalised value yhat and 1/std per item
+// (saved by the training forward for the LayerNorm backward).
+template <int TH>
+SGNN_DEV void acc_layernorm_save(f32x16 (&acc)[TH], const float* gamma_lds, const float* beta_lds,
+                                 f32x16 (&yhat)[TH], float& rstd_out) {
+  const int h = lane_id() >> 5;
+  constexpr float inv_n = 1.0f / (32.0f * TH);
+  float s = 0.0f;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += acc[t][r];
+  s += wave_xor32(s);
+  const float mean = s * inv_n;
+  float v = 0.0f;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float d = acc[t][r] - mean;
+      v += d * d;
+    }
+  v += wave_xor32(v);
+  const float rstd = 1.0f / sqrtf(v * inv_n + 1e-5f);
+  rstd_out = rstd;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u = 32 * t + crow(r, h);
+      const float yh = (acc[t][r] - mean) * rstd;
+      yhat[t][r] = yh;
+      acc[t][r] = yh * gamma_lds[u] + beta_lds[u];
+    }
+}
+
+// LayerNorm backward for one item per lane pair (units in registers):
+//   g = dout * gamma;  dy = rstd * (g - mean(g) - yhat * mean(g * yhat)).
+template <int TH>
+SGNN_DEV void acc_layernorm_bwd(const f32x16 (&dout)[TH], const f32x16 (&yhat)[TH], float rstd,
+                                const float* gamma_lds, f32x16 (&dy)[TH]) {
+  const int h = lane_id() >> 5;
+  constexpr float inv_n = 1.0f / (32.0f * TH);
+  float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float g = dout[t][r] * gamma_lds[32 * t + crow(r, h)];
+      dy[t][r] = g;
+      s1 += g;
+      s2 += g * yhat[t][r];
+    }
+  s1 += wave_xor32(s1);
+  s2 += wave_xor32(s2);
+  const float m1 = s1 * inv_n, m2 = s2 * inv_n;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dy[t][r] = rstd * (dy[t][r] - m1 - yhat[t][r] * m2);
+}
+
+// Tiled per-32-item layout used for edge tensors: tile base + (t*4+g)*256 +
+// lane*4 holds units 32t+8g+4h+(0..3) of item (lane&31).
+template <int TH>
+SGNN_DEV void load_tiled(f32x16 (&x)[TH], const float* tile_base) {
+  const float* p = tile_base + lane_id() * 4;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = ld4(p + (t * 4 + g) * 256);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[t][4 * g + c] = v[c];
+    }
+}
+
+template <int TH>
+SGNN_DEV void store_tiled(float* tile_base, const f32x16 (&x)[TH]) {
+  float* p = tile_base + lane_id() * 4;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = x[t][4 * g + c];
+      st4(p + (t * 4 + g) * 256, v);
+    }
+}
+
+// Write an item-on-lane register tile into an LDS image [item][unit] (ld).
+template <int TH>
+SGNN_DEV void lds_store_items(float* img, int ld, int item, const f32x16 (&x)[TH]) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = x[t][4 * g + c];
+      st4(img + item * ld + 32 * t + 8 * g + 4 * h, v);
+    }
+}
+
+// Outer-product accumulation over items from two LDS images [item][unit]:
+//   acc[u][v] += sum_{item < nitems} A[item][ua + u] * B[item][vb + v]
+// for one 32x32 output tile (u, v in 0..31): MFMA with the items as k.
+SGNN_DEV void mfma_outer(f32x16& acc, const float* A, int lda, int ua, const float* B, int ldb,
+                         int vb, int nitems) {
+  const int l = lane_id() & 31, h = lane_id() >> 5;
+  for (int s = 0; s < nitems; s += 2) {
+    const int it = s + h;
+    acc = mfma32(A[it * lda + ua + l], B[it * ldb + vb + l], acc);
+  }
+}
+
+// Store a 32x32 C-layout accumulator tile (rows u, cols = lane) into a
+// row-major matrix region dst[u * ld + v] (v = lane&31).
+SGNN_DEV void store_tile_rowmajor(float* dst, int ld, const f32x16& acc) {
+  const int l = lane_id() & 31, h = lane_id() >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dst[crow(r, h) * ld + l] = acc[r];
+}
+
+SGNN_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Stage a [rows x cols] row-major global matrix TRANSPOSED into LDS:
+// lds[c * ld + r] = g[r * ldg + c] (r < rows_valid, c < cols_valid, zero pad).
+SGNN_DEV void stage_matrix_t(float* lds, int ld, const float* g, int ldg, int rows_valid,
+                             int cols_valid, int rows_pad, int cols_pad, float scale = 1.0f) {
+  const int total = rows_pad * cols_pad;
+  for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    const int r = idx / cols_pad, c = idx - r * cols_pad;
+    float v = 0.0f;
+    if (r < rows_valid && c < cols_valid) v = g[(int64_t)r * ldg + c] * scale;
+    lds[c * ld + r] = v;
+  }
+}

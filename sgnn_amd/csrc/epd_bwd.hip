@@ -1,0 +1,1150 @@
+// Backward of the Encode-Process-Decode training step for gfx950.
+//
+// Reverse-mode of sgnn/single_scale/learned_simulator.py:440-491
+// (predict_accelerations) + train.py:257-268 (loss), i.e. what
+// loss.backward() computes through PyG/torch autograd, as 3L + 4 fused
+// launches (L = message-passing layers):
+//   k_dec_bwd       loss -> d pred -> Decoder backward -> g_L = dL/dx_L
+//   k_node_bwd(k)   node MLP + LayerNorm + residual backward -> d agg_k, dx_k'
+//   k_edge_bwd(k)   edge MLP + LayerNorm backward from d agg_k[recv]:
+//                   dh (ReLU-masked) -> segment sums dU (receiver CSR),
+//                   dh rows for dV, dE0 += 2^k W1e^T dh
+//   k_uv_bwd(k)     g_k = dx_k' + W1i^T dU + W1j^T dV  (dV gathered through
+//                   the sender-sorted transpose CSR, deterministic)
+//   k_enc_node_bwd, k_enc_edge_bwd   Encoder MLPs
+//   k_reduce_slabs  weight gradients
+// Weight gradients are outer products summed over items (nodes / edges):
+// each 4-wave workgroup stages 128 items of both operands in LDS
+// ([item][unit] images) and every wave accumulates one 32x32 output tile
+// with v_mfma_f32_32x32x2_f32 using the items as the k dimension.  Per-WG
+// partials go to a slab; k_reduce_slabs sums the slabs in fixed order, so
+// gradients are bitwise reproducible run to run (no float atomics).
+#include "common.h"
+#include "../../include/sgnn.h"
+#include "sgnn_internal.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = 4;
+constexpr int kChunk = 32 * kWaves;  // items per workgroup iteration
+
+SGNN_DEV int clamp_items(int64_t remaining) {
+  return remaining <= 0 ? 0 : (remaining >= 32 ? 32 : (int)remaining);
+}
+
+template <int TH>
+SGNN_DEV void zero(f32x16 (&x)[TH]) {
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[t][r] = 0.0f;
+}
+
+template <int TH>
+SGNN_DEV void zero_if(f32x16 (&x)[TH], bool pred) {
+  if (pred) zero<TH>(x);
+}
+
+// lane = unit: sum over the first nvalid items of a wave's LDS slice
+SGNN_DEV float lane_sum(const float* slice, int ld, int nvalid, int unit) {
+  float s = 0.0f;
+  for (int it = 0; it < nvalid; ++it) s += slice[it * ld + unit];
+  return s;
+}
+
+template <int TH>
+SGNN_DEV void lane_sums(float (&acc)[TH / 2 > 0 ? TH / 2 : 1], const float* slice, int ld,
+                        int nvalid) {
+  constexpr int UPL = (32 * TH) / 64 > 0 ? (32 * TH) / 64 : 1;
+#pragma unroll
+  for (int q = 0; q < UPL; ++q) {
+    const int u = lane_id() + 64 * q;
+    if (u < 32 * TH) acc[q] += lane_sum(slice, ld, nvalid, u);
+  }
+}
+
+// Segment sum over the receiver-sorted CSR of a wave's 32-item LDS slice
+// (lane = unit) with tile carries (same contract as the forward edge layer).
+template <int TH>
+SGNN_DEV void segment_sum_store(const float* slice, int ld, int rv, int nvalid, int64_t base,
+                                int64_t tile, const int32_t* rowptr, float* dst_rows, float* cin,
+                                float* cout) {
+  constexpr int H = 32 * TH;
+  constexpr int UPL = H / 64 > 0 ? H / 64 : 1;
+  const int l = lane_id();
+  float acc[UPL];
+#pragma unroll
+  for (int q = 0; q < UPL; ++q) acc[q] = 0.0f;
+  int seg0 = 0;
+  for (int jj = 0; jj < nvalid; ++jj) {
+#pragma unroll
+    for (int q = 0; q < UPL; ++q)
+      if (l + 64 * q < H) acc[q] += slice[jj * ld + l + 64 * q];
+    const int rr = __builtin_amdgcn_readlane(rv, jj);
+    const int nx = (jj + 1 < nvalid) ? __builtin_amdgcn_readlane(rv, jj + 1) : -1;
+    if (nx != rr) {
+      const int64_t seg_s = base + seg0, seg_e = base + jj + 1;
+      const int64_t rp0 = rowptr[rr], rp1 = rowptr[rr + 1];
+      float* dst;
+      if (rp0 == seg_s && rp1 == seg_e) dst = dst_rows + (int64_t)rr * H;
+      else if (rp0 == seg_s) dst = cout + tile * H;
+      else dst = cin + tile * H;
+#pragma unroll
+      for (int q = 0; q < UPL; ++q) {
+        if (l + 64 * q < H) dst[l + 64 * q] = acc[q];
+        acc[q] = 0.0f;
+      }
+      seg0 = jj + 1;
+    }
+  }
+}
+
+// Resolve a receiver-CSR row sum (agg or dU) for node i from rows + carries.
+template <int TH>
+SGNN_DEV void load_resolved(f32x16 (&a)[TH], const float* rows, const float* cin,
+                            const float* cout, const int32_t* rowptr, int64_t i) {
+  constexpr int H = 32 * TH;
+  const int32_t r0 = rowptr[i], r1 = rowptr[i + 1];
+  if (r1 <= r0) {
+    zero<TH>(a);
+    return;
+  }
+  const int32_t t0 = r0 >> 5, t1 = (r1 - 1) >> 5;
+  if (t0 == t1) {
+    load_row_clayout<TH>(a, rows + i * H);
+  } else {
+    load_row_clayout<TH>(a, cout + (int64_t)t0 * H);
+    add_row_clayout<TH>(a, cin + (int64_t)t1 * H);
+  }
+}
+
+// Each wave owns output tiles w, w+4, ... of a [32*TU x 32*TV] gradient.
+template <int NT>
+SGNN_DEV void outer_tiles(f32x16 (&acc)[NT], int TU, int TV, const float* A, int lda, int abase,
+                          const float* B, int ldb, int bbase) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    const int tile = w + kWaves * q;
+    if (tile < TU * TV) {
+      const int tu = tile / TV, tv = tile - tu * TV;
+      mfma_outer(acc[q], A, lda, abase + 32 * tu, B, ldb, bbase + 32 * tv, kChunk);
+    }
+  }
+}
+
+template <int NT>
+SGNN_DEV void store_outer(float* dst, int ld, int TU, int TV, const f32x16 (&acc)[NT]) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    const int tile = w + kWaves * q;
+    if (tile < TU * TV) {
+      const int tu = tile / TV, tv = tile - tu * TV;
+      store_tile_rowmajor(dst + (32 * tu) * ld + 32 * tv, ld, acc[q]);
+    }
+  }
+}
+
+template <int NT>
+SGNN_DEV void zero_acc(f32x16 (&acc)[NT]) {
+#pragma unroll
+  for (int q = 0; q < NT; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
+}
+
+// per-wave lane-unit vector partial -> slab row (wave w)
+template <int TH>
+SGNN_DEV void store_lane_vec(float* dst, const float (&acc)[TH / 2 > 0 ? TH / 2 : 1]) {
+  constexpr int H = 32 * TH;
+  constexpr int UPL = H / 64 > 0 ? H / 64 : 1;
+  const int w = threadIdx.x >> 6, l = lane_id();
+#pragma unroll
+  for (int q = 0; q < UPL; ++q)
+    if (l + 64 * q < H) dst[w * H + l + 64 * q] = acc[q];
+}
+
+#define LANEVEC(name) float name[TH / 2 > 0 ? TH / 2 : 1] = {}
+
+// ===========================================================================
+// Edge layer backward
+struct EdgeBwdArgs {
+  const float* dagg;
+  const int32_t *rowptr, *send, *recv;
+  int64_t n;
+  const float *hs, *yh, *rstd, *e0t;
+  float e_scale;
+  const float *w2, *we, *gamma;  // we = edge W1 + 2H (ld 3H)
+  float *du, *cin, *cout, *dh_rows, *de0t;
+  int de0_accumulate;
+  float* slab;
+  int64_t slab_stride;
+};
+
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4;
+  extern __shared__ float lds[];
+  float* W2T = lds;
+  float* WeT = W2T + H * ldh;
+  float* gam = WeT + H * ldh;
+  float* bufA = gam + H;
+  float* bufB = bufA + kChunk * ldh;
+  stage_matrix_t(W2T, ldh, a.w2, H, H, H, H, H);
+  stage_matrix_t(WeT, ldh, a.we, 3 * H, H, H, H, H);
+  stage_vec(gam, a.gamma, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
+  float* sA = bufA + w * 32 * ldh;
+  float* sB = bufB + w * 32 * ldh;
+  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
+  f32x16 acc_w2[NT], acc_w1[NT];
+  zero_acc<NT>(acc_w2);
+  zero_acc<NT>(acc_w1);
+  LANEVEC(s_db2);
+  LANEVEC(s_dg);
+  LANEVEC(s_db);
+  const int64_t E = a.rowptr[a.n];
+  const int64_t nchunks = (E + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+    const int nvalid = clamp_items(E - base);
+    const bool valid = e < E;
+    const int64_t ec = valid ? e : E - 1;
+    f32x16 dy[TH], hh[TH];
+    int rv = 0;
+    if (nvalid > 0) {
+      rv = a.recv[ec];
+      f32x16 dm[TH], yh[TH];
+      load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
+      load_tiled<TH>(yh, a.yh + tile * (32 * H));
+      load_tiled<TH>(hh, a.hs + tile * (32 * H));
+      const float rs = a.rstd[ec];
+      zero_if<TH>(dm, !valid);
+      acc_layernorm_bwd<TH>(dm, yh, rs, gam, dy);
+      zero_if<TH>(dy, !valid);
+      zero_if<TH>(hh, !valid);
+      // d beta = sum dm, d gamma = sum dm * yhat  (graph_network.py:148 LayerNorm)
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];
+      lds_store_items<TH>(sA, ldh, j, dm);
+      lds_store_items<TH>(sB, ldh, j, yh);
+      wave_lds_sync();
+      lane_sums<TH>(s_db, sA, ldh, nvalid);
+      lane_sums<TH>(s_dg, sB, ldh, nvalid);
+      wave_lds_sync();
+      lds_store_items<TH>(sA, ldh, j, dy);
+      lds_store_items<TH>(sB, ldh, j, hh);
+      wave_lds_sync();
+      lane_sums<TH>(s_db2, sA, ldh, nvalid);
+    } else {
+      zero<TH>(dy);
+      zero<TH>(hh);
+      lds_store_items<TH>(sA, ldh, j, dy);
+      lds_store_items<TH>(sB, ldh, j, hh);
+    }
+    __syncthreads();
+    outer_tiles<NT>(acc_w2, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW2 = sum dy (x) h
+    __syncthreads();
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    if (nvalid > 0) {
+      mfma_from_acc<TH, TH>(dh, W2T, ldh, 0, dy);  // W2^T dy
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dh[t][r] = hh[t][r] > 0.0f ? dh[t][r] : 0.0f;
+      zero_if<TH>(dh, !valid);
+      // dE0 += 2^k W1e^T dh (the edge latent feeding layer k is 2^k e0)
+      f32x16 de[TH];
+      zero<TH>(de);
+      mfma_from_acc<TH, TH>(de, WeT, ldh, 0, dh);
+      float* dtile = a.de0t + tile * (32 * H);
+      if (a.de0_accumulate) {
+        f32x16 old[TH];
+        load_tiled<TH>(old, dtile);
+#pragma unroll
+        for (int t = 0; t < TH; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) de[t][r] = old[t][r] + de[t][r] * a.e_scale;
+      } else {
+#pragma unroll
+        for (int t = 0; t < TH; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) de[t][r] *= a.e_scale;
+      }
+      store_tiled<TH>(dtile, de);
+      if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
+      f32x16 e0[TH];
+      load_tiled<TH>(e0, a.e0t + tile * (32 * H));
+      zero_if<TH>(e0, !valid);
+      lds_store_items<TH>(sA, ldh, j, dh);
+      lds_store_items<TH>(sB, ldh, j, e0);
+      wave_lds_sync();
+      segment_sum_store<TH>(sA, ldh, rv, nvalid, base, tile, a.rowptr, a.du, a.cin, a.cout);
+    } else {
+      f32x16 z[TH];
+      zero<TH>(z);
+      lds_store_items<TH>(sA, ldh, j, z);
+      lds_store_items<TH>(sB, ldh, j, z);
+    }
+    __syncthreads();
+    outer_tiles<NT>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1e = sum dh (x) e0
+    __syncthreads();
+  }
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  store_outer<NT>(slab, H, TH, TH, acc_w2);
+  store_outer<NT>(slab + H * H, H, TH, TH, acc_w1);
+  store_lane_vec<TH>(slab + 2 * H * H, s_db2);
+  store_lane_vec<TH>(slab + 2 * H * H + kWaves * H, s_dg);
+  store_lane_vec<TH>(slab + 2 * H * H + 2 * kWaves * H, s_db);
+}
+
+// ===========================================================================
+// Node layer backward (graph_network.py:201-222 + residual :176)
+struct NodeBwdArgs {
+  const float* g;  // dL/dx_out
+  int64_t n;
+  const float *yh, *rstd, *hn, *agg, *x;
+  const float *w1, *w2, *gamma;
+  float *dagg, *dxp;
+  float* slab;
+  int64_t slab_stride;
+};
+
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_node_bwd(NodeBwdArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4;
+  extern __shared__ float lds[];
+  float* W2T = lds;                 // [H][ldh]
+  float* W1T = W2T + H * ldh;       // [2H][ldh]: W1T[i][k] = W1[k][i]
+  float* gam = W1T + 2 * H * ldh;
+  float* bufA = gam + H;
+  float* bufB = bufA + kChunk * ldh;
+  stage_matrix_t(W2T, ldh, a.w2, H, H, H, H, H);
+  stage_matrix_t(W1T, ldh, a.w1, 2 * H, H, 2 * H, H, 2 * H);
+  stage_vec(gam, a.gamma, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  float* sA = bufA + w * 32 * ldh;
+  float* sB = bufB + w * 32 * ldh;
+  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
+  f32x16 acc_w2[NT], acc_w1a[NT], acc_w1x[NT];
+  zero_acc<NT>(acc_w2);
+  zero_acc<NT>(acc_w1a);
+  zero_acc<NT>(acc_w1x);
+  LANEVEC(s_db2);
+  LANEVEC(s_dg);
+  LANEVEC(s_db);
+  LANEVEC(s_db1);
+  const int64_t nchunks = (a.n + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t i = c * kChunk + w * 32 + j;
+    const int nvalid = clamp_items(a.n - (c * kChunk + w * 32));
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    f32x16 gi[TH], dy[TH], hn[TH];
+    load_row_clayout<TH>(gi, a.g + ic * H);
+    zero_if<TH>(gi, !valid);
+    {
+      f32x16 yh[TH];
+      load_row_clayout<TH>(yh, a.yh + ic * H);
+      const float rs = a.rstd[ic];
+      acc_layernorm_bwd<TH>(gi, yh, rs, gam, dy);
+      zero_if<TH>(dy, !valid);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yh[t][r] *= gi[t][r];
+      lds_store_items<TH>(sA, ldh, j, gi);
+      lds_store_items<TH>(sB, ldh, j, yh);
+      wave_lds_sync();
+      lane_sums<TH>(s_db, sA, ldh, nvalid);
+      lane_sums<TH>(s_dg, sB, ldh, nvalid);
+      wave_lds_sync();
+    }
+    load_row_clayout<TH>(hn, a.hn + ic * H);
+    zero_if<TH>(hn, !valid);
+    lds_store_items<TH>(sA, ldh, j, dy);
+    lds_store_items<TH>(sB, ldh, j, hn);
+    wave_lds_sync();
+    lane_sums<TH>(s_db2, sA, ldh, nvalid);
+    __syncthreads();
+    outer_tiles<NT>(acc_w2, TH, TH, bufA, ldh, 0, bufB, ldh, 0);
+    __syncthreads();
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    mfma_from_acc<TH, TH>(dh, W2T, ldh, 0, dy);
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dh[t][r] = hn[t][r] > 0.0f ? dh[t][r] : 0.0f;
+    f32x16 ag[TH];
+    load_row_clayout<TH>(ag, a.agg + ic * H);
+    zero_if<TH>(ag, !valid);
+    lds_store_items<TH>(sA, ldh, j, dh);
+    lds_store_items<TH>(sB, ldh, j, ag);
+    wave_lds_sync();
+    lane_sums<TH>(s_db1, sA, ldh, nvalid);
+    __syncthreads();
+    outer_tiles<NT>(acc_w1a, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, :H] = dh (x) agg
+    __syncthreads();
+    f32x16 xx[TH];
+    load_row_clayout<TH>(xx, a.x + ic * H);
+    zero_if<TH>(xx, !valid);
+    lds_store_items<TH>(sB, ldh, j, xx);
+    __syncthreads();
+    outer_tiles<NT>(acc_w1x, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, H:] = dh (x) x
+    __syncthreads();
+    // d agg = W1[:, :H]^T dh ; dx' = g + W1[:, H:]^T dh
+    f32x16 o[TH];
+    zero<TH>(o);
+    mfma_from_acc<TH, TH>(o, W1T, ldh, 0, dh);
+    if (valid) store_row_clayout<TH>(a.dagg + i * H, o);
+    mfma_from_acc<TH, TH>(gi, W1T + H * ldh, ldh, 0, dh);
+    if (valid) store_row_clayout<TH>(a.dxp + i * H, gi);
+    (void)h;
+  }
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  store_outer<NT>(slab, H, TH, TH, acc_w2);
+  store_outer<NT>(slab + H * H, 2 * H, TH, TH, acc_w1a);
+  store_outer<NT>(slab + H * H + H, 2 * H, TH, TH, acc_w1x);
+  float* v = slab + 3 * H * H;
+  store_lane_vec<TH>(v, s_db1);
+  store_lane_vec<TH>(v + kWaves * H, s_db2);
+  store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
+  store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
+}
+
+// ===========================================================================
+// u/v projections backward: g = dx' + W1i^T dU + W1j^T dV
+struct UvBwdArgs {
+  const float* dxp;
+  const float *du, *cin, *cout;
+  const int32_t* rowptr;
+  const float* dh_rows;
+  const int32_t *tptr, *tperm;
+  const float* x;
+  int64_t n;
+  const float* w1;  // edge W1 [H][3H]
+  float* g;
+  float* slab;
+  int64_t slab_stride;
+};
+
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_uv_bwd(UvBwdArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4;
+  extern __shared__ float lds[];
+  float* WiT = lds;
+  float* WjT = WiT + H * ldh;
+  float* bufA = WjT + H * ldh;
+  float* bufB = bufA + kChunk * ldh;
+  stage_matrix_t(WiT, ldh, a.w1, 3 * H, H, H, H, H);
+  stage_matrix_t(WjT, ldh, a.w1 + H, 3 * H, H, H, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
+  float* sA = bufA + w * 32 * ldh;
+  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
+  f32x16 acc_i[NT], acc_j[NT];
+  zero_acc<NT>(acc_i);
+  zero_acc<NT>(acc_j);
+  LANEVEC(s_db1);
+  const int64_t nchunks = (a.n + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t i = c * kChunk + w * 32 + j;
+    const int nvalid = clamp_items(a.n - (c * kChunk + w * 32));
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    f32x16 du[TH], dv[TH], xx[TH], gg[TH];
+    load_resolved<TH>(du, a.du, a.cin, a.cout, a.rowptr, ic);
+    zero<TH>(dv);
+    for (int32_t t = a.tptr[ic], t1 = a.tptr[ic + 1]; t < t1; ++t)
+      add_row_clayout<TH>(dv, a.dh_rows + (int64_t)a.tperm[t] * H);
+    zero_if<TH>(du, !valid);
+    zero_if<TH>(dv, !valid);
+    load_row_clayout<TH>(xx, a.x + ic * H);
+    zero_if<TH>(xx, !valid);
+    load_row_clayout<TH>(gg, a.dxp + ic * H);
+    mfma_from_acc<TH, TH>(gg, WiT, ldh, 0, du);
+    mfma_from_acc<TH, TH>(gg, WjT, ldh, 0, dv);
+    if (valid) store_row_clayout<TH>(a.g + i * H, gg);
+    lds_store_items<TH>(sA, ldh, j, du);
+    lds_store_items<TH>(bufB + w * 32 * ldh, ldh, j, xx);
+    wave_lds_sync();
+    lane_sums<TH>(s_db1, sA, ldh, nvalid);
+    __syncthreads();
+    outer_tiles<NT>(acc_i, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, 0:H] = dU (x) x
+    __syncthreads();
+    lds_store_items<TH>(sA, ldh, j, dv);
+    __syncthreads();
+    outer_tiles<NT>(acc_j, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, H:2H] = dV (x) x
+    __syncthreads();
+  }
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  store_outer<NT>(slab, 2 * H, TH, TH, acc_i);
+  store_outer<NT>(slab + H, 2 * H, TH, TH, acc_j);
+  store_lane_vec<TH>(slab + 2 * H * H, s_db1);
+}
+
+// ===========================================================================
+// Loss (train.py:257-268) + Decoder backward (graph_network.py:321-333)
+struct DecBwdArgs {
+  const float* pred;      // [n][D+1]
+  const float* pos_seq;   // noisy input window [n][T][D]
+  const float* next_pos;  // [n][D]
+  const float* noise;     // [n][T][D] or null
+  const float* next_strain;  // [n]
+  const float *acc_mean, *acc_std;
+  int64_t n;
+  int T, D;
+  float w_pos, w_strain, inv_count;
+  const float* dpred;
+  const float *hd, *x;
+  const float *wd1, *wd2;
+  float* g;
+  float* slab;
+  int64_t slab_stride;
+};
+
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_dec_bwd(DecBwdArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4, ldo = 32 + 4;
+  extern __shared__ float lds[];
+  float* W1T = lds;                 // [H][ldh]
+  float* W2T = W1T + H * ldh;       // [H][ldo]: W2T[i][k] = Wd2[k][i], k < 32 (D+1 valid)
+  float* bufA = W2T + H * ldo;
+  float* bufB = bufA + kChunk * ldh;
+  stage_matrix_t(W1T, ldh, a.wd1, H, H, H, H, H);
+  stage_matrix_t(W2T, ldo, a.wd2, H, a.D + 1, H, 32, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  float* sA = bufA + w * 32 * ldh;
+  float* sB = bufB + w * 32 * ldh;
+  constexpr int NT2 = (TH + kWaves - 1) / kWaves;     // [32 x H] decoder W2
+  constexpr int NT1 = (TH * TH + kWaves - 1) / kWaves;
+  f32x16 acc_w2[NT2], acc_w1[NT1];
+  zero_acc<NT2>(acc_w2);
+  zero_acc<NT1>(acc_w1);
+  float s_db2 = 0.0f;  // lane = output unit (< 32)
+  LANEVEC(s_db1);
+  float loss_acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // total, x, y, z, strain
+  const int64_t nchunks = (a.n + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t i = c * kChunk + w * 32 + j;
+    const int nvalid = clamp_items(a.n - (c * kChunk + w * 32));
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    f32x16 dp[1];
+    zero<1>(dp);
+    if (valid && h == 0 && a.dpred) {
+      for (int cc = 0; cc <= a.D; ++cc) dp[0][cc] = a.dpred[ic * (a.D + 1) + cc];
+    } else if (valid && h == 0) {
+      const int D = a.D, T = a.T;
+      const float* p = a.pos_seq + ic * T * D;
+      float tot = 0.0f;
+      for (int cc = 0; cc < D; ++cc) {  // learned_simulator.py:479-481, :509-517
+        const float nz = a.noise ? a.noise[(ic * T + T - 1) * D + cc] : 0.0f;
+        const float nxt = __fadd_rn(a.next_pos[ic * D + cc], nz);
+        const float prev = p[(T - 1) * D + cc];
+        const float pvel = __fsub_rn(prev, p[(T - 2) * D + cc]);
+        const float acc = __fsub_rn(__fsub_rn(nxt, prev), pvel);
+        const float tgt = __fdiv_rn(__fsub_rn(acc, a.acc_mean[cc]), a.acc_std[cc]);
+        const float d = a.pred[ic * (D + 1) + cc] - tgt;
+        dp[0][cc] = 2.0f * a.w_pos * d * a.inv_count;
+        tot += d * d;
+        loss_acc[1 + cc] += d * d;
+      }
+      const float ds = a.pred[ic * (D + 1) + D] - a.next_strain[ic];
+      dp[0][D] = 2.0f * a.w_strain * ds * a.inv_count;
+      loss_acc[0] += a.w_pos * tot + a.w_strain * ds * ds;
+      loss_acc[4] += ds * ds;
+    }
+    constexpr int ldp = 32 + 4;
+    float* sP = sA;  // reuse: [32][ldp] image of dpred
+    {
+      f32x16 hd[TH];
+      load_row_clayout<TH>(hd, a.hd + ic * H);
+      zero_if<TH>(hd, !valid);
+      // d pred image (32 units) and hd image for dW2 = dpred (x) hd
+      f32x4 v;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) v[cc] = dp[0][4 * gq + cc];
+        st4(bufA + (w * 32 + j) * ldp + 8 * gq + 4 * h, v);
+      }
+      lds_store_items<TH>(sB, ldh, j, hd);
+      wave_lds_sync();
+      if (l < 32) s_db2 += lane_sum(bufA + w * 32 * ldp, ldp, nvalid, l);
+      __syncthreads();
+      outer_tiles<NT2>(acc_w2, 1, TH, bufA, ldp, 0, bufB, ldh, 0);
+      __syncthreads();
+      f32x16 dh[TH];
+      zero<TH>(dh);
+      mfma_from_acc<TH, 1>(dh, W2T, ldo, 0, dp);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dh[t][r] = hd[t][r] > 0.0f ? dh[t][r] : 0.0f;
+      f32x16 xx[TH];
+      load_row_clayout<TH>(xx, a.x + ic * H);
+      zero_if<TH>(xx, !valid);
+      lds_store_items<TH>(sA, ldh, j, dh);
+      lds_store_items<TH>(sB, ldh, j, xx);
+      wave_lds_sync();
+      lane_sums<TH>(s_db1, sA, ldh, nvalid);
+      __syncthreads();
+      outer_tiles<NT1>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);
+      __syncthreads();
+      f32x16 gg[TH];
+      zero<TH>(gg);
+      mfma_from_acc<TH, TH>(gg, W1T, ldh, 0, dh);
+      if (valid) store_row_clayout<TH>(a.g + i * H, gg);
+    }
+    (void)sP;
+  }
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  store_outer<NT2>(slab, H, 1, TH, acc_w2);           // [32][H] (rows >= D+1 are zero)
+  store_outer<NT1>(slab + 32 * H, H, TH, TH, acc_w1);  // [H][H]
+  float* v = slab + 32 * H + H * H;
+  if (l < 32) v[w * 32 + l] = s_db2;
+  store_lane_vec<TH>(v + kWaves * 32, s_db1);
+  // loss partials: reduce over lanes, one row of 4 per wave
+  float* lp = v + kWaves * 32 + kWaves * H;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    float s = loss_acc[q];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (l == 0) lp[w * 8 + q] = s;
+  }
+}
+
+// ===========================================================================
+// Encoder node MLP backward (graph_network.py:86-90)
+struct EncNodeBwdArgs {
+  const float* g;
+  const float* pos_seq;
+  int64_t n;
+  int T, dim, feat;
+  const float *vel_mean, *vel_std;
+  float radius;
+  const float *h1, *yh, *rstd;
+  const float *w2, *gamma;
+  float* slab;
+  int64_t slab_stride;
+};
+
+template <int TH, int TKF>
+__global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4, ldf = 32 * TKF + 4;
+  extern __shared__ float lds[];
+  float* W2T = lds;
+  float* gam = W2T + H * ldh;
+  float* bufA = gam + H;
+  float* bufB = bufA + kChunk * ldh;  // sized max(ldh, ldf) per row
+  constexpr int ldb = ldh > ldf ? ldh : ldf;
+  stage_matrix_t(W2T, ldh, a.w2, H, H, H, H, H);
+  stage_vec(gam, a.gamma, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  float* sA = bufA + w * 32 * ldh;
+  float* sB = bufB + w * 32 * ldb;
+  constexpr int NT2 = (TH * TH + kWaves - 1) / kWaves;
+  constexpr int NT1 = (TH * TKF + kWaves - 1) / kWaves;
+  f32x16 acc_w2[NT2], acc_w1[NT1];
+  zero_acc<NT2>(acc_w2);
+  zero_acc<NT1>(acc_w1);
+  LANEVEC(s_db1);
+  LANEVEC(s_db2);
+  LANEVEC(s_dg);
+  LANEVEC(s_db);
+  const int nvel = (a.T - 1) * a.dim;
+  const int64_t nchunks = (a.n + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t i = c * kChunk + w * 32 + j;
+    const int nvalid = clamp_items(a.n - (c * kChunk + w * 32));
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    f32x16 gi[TH], dy[TH];
+    load_row_clayout<TH>(gi, a.g + ic * H);
+    zero_if<TH>(gi, !valid);
+    {
+      f32x16 yh[TH];
+      load_row_clayout<TH>(yh, a.yh + ic * H);
+      acc_layernorm_bwd<TH>(gi, yh, a.rstd[ic], gam, dy);
+      zero_if<TH>(dy, !valid);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yh[t][r] *= gi[t][r];
+      lds_store_items<TH>(sA, ldh, j, gi);
+      lds_store_items<TH>(sB, ldb, j, yh);
+      wave_lds_sync();
+      lane_sums<TH>(s_db, sA, ldh, nvalid);
+      lane_sums<TH>(s_dg, sB, ldb, nvalid);
+      wave_lds_sync();
+    }
+    f32x16 h1[TH];
+    load_row_clayout<TH>(h1, a.h1 + ic * H);
+    zero_if<TH>(h1, !valid);
+    lds_store_items<TH>(sA, ldh, j, dy);
+    lds_store_items<TH>(sB, ldb, j, h1);
+    wave_lds_sync();
+    lane_sums<TH>(s_db2, sA, ldh, nvalid);
+    __syncthreads();
+    outer_tiles<NT2>(acc_w2, TH, TH, bufA, ldh, 0, bufB, ldb, 0);
+    __syncthreads();
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    mfma_from_acc<TH, TH>(dh, W2T, ldh, 0, dy);
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dh[t][r] = (h1[t][r] > 0.0f && valid) ? dh[t][r] : 0.0f;
+    // node features recomputed exactly as the forward (learned_simulator.py:272-284)
+    f32x16 xf[TKF];
+    const float* p = a.pos_seq + ic * a.T * a.dim;
+#pragma unroll
+    for (int tk = 0; tk < TKF; ++tk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = 32 * tk + crow(r, h);
+        float val = 0.0f;
+        if (valid && f < nvel) {
+          const int t = f / a.dim, cc = f - t * a.dim;
+          const float vel = __fsub_rn(p[(t + 1) * a.dim + cc], p[t * a.dim + cc]);
+          val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[cc]), a.vel_std[cc]);
+        } else if (valid && f == nvel) {
+          val = fminf(fmaxf(__fadd_rn(p[(a.T - 1) * a.dim], 2.0f), 0.0f), a.radius);
+        }
+        xf[tk][r] = val;
+      }
+    lds_store_items<TH>(sA, ldh, j, dh);
+    lds_store_items<TKF>(sB, ldb, j, xf);
+    wave_lds_sync();
+    lane_sums<TH>(s_db1, sA, ldh, nvalid);
+    __syncthreads();
+    outer_tiles<NT1>(acc_w1, TH, TKF, bufA, ldh, 0, bufB, ldb, 0);
+    __syncthreads();
+  }
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  store_outer<NT2>(slab, H, TH, TH, acc_w2);
+  store_outer<NT1>(slab + H * H, 32 * TKF, TH, TKF, acc_w1);
+  float* v = slab + H * H + H * 32 * TKF;
+  store_lane_vec<TH>(v, s_db1);
+  store_lane_vec<TH>(v + kWaves * H, s_db2);
+  store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
+  store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
+}
+
+// ===========================================================================
+// Encoder edge MLP backward (graph_network.py:92-96) from dE0
+struct EncEdgeBwdArgs {
+  const float* de0t;
+  const float* pos;
+  int64_t stride;
+  int dim;
+  float radius;
+  const int32_t *rowptr, *send, *recv;
+  int64_t n;
+  const float *yh, *rstd;
+  const float *w1, *b1, *w2, *gamma;
+  float* slab;
+  int64_t slab_stride;
+};
+
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4, ld1 = 5, ldf = 32 + 4;
+  extern __shared__ float lds[];
+  float* W1 = lds;
+  float* W2T = W1 + H * ld1;
+  float* b1 = W2T + H * ldh;
+  float* gam = b1 + H;
+  float* bufA = gam + H;
+  float* bufB = bufA + kChunk * ldh;
+  stage_matrix(W1, ld1, a.w1, a.dim + 1, H, a.dim + 1, H, 4);
+  stage_matrix_t(W2T, ldh, a.w2, H, H, H, H, H);
+  stage_vec(b1, a.b1, H, H);
+  stage_vec(gam, a.gamma, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  float* sA = bufA + w * 32 * ldh;
+  float* sB = bufB + w * 32 * ldh;
+  constexpr int NT2 = (TH * TH + kWaves - 1) / kWaves;
+  constexpr int NT1 = (TH + kWaves - 1) / kWaves;
+  f32x16 acc_w2[NT2], acc_w1[NT1];
+  zero_acc<NT2>(acc_w2);
+  zero_acc<NT1>(acc_w1);
+  LANEVEC(s_db1);
+  LANEVEC(s_db2);
+  LANEVEC(s_dg);
+  LANEVEC(s_db);
+  const int64_t E = a.rowptr[a.n];
+  const int64_t nchunks = (E + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+    const int nvalid = clamp_items(E - base);
+    const bool valid = e < E;
+    const int64_t ec = valid ? e : (E > 0 ? E - 1 : 0);
+    f32x16 dy[TH], h1[TH], fx[1];
+    zero<TH>(dy);
+    zero<TH>(h1);
+    zero<1>(fx);
+    if (nvalid > 0) {
+      f32x16 dm[TH], yh[TH];
+      load_tiled<TH>(dm, a.de0t + tile * (32 * H));
+      load_tiled<TH>(yh, a.yh + tile * (32 * H));
+      zero_if<TH>(dm, !valid);
+      acc_layernorm_bwd<TH>(dm, yh, a.rstd[ec], gam, dy);
+      zero_if<TH>(dy, !valid);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];
+      lds_store_items<TH>(sA, ldh, j, dm);
+      lds_store_items<TH>(sB, ldh, j, yh);
+      wave_lds_sync();
+      lane_sums<TH>(s_db, sA, ldh, nvalid);
+      lane_sums<TH>(s_dg, sB, ldh, nvalid);
+      wave_lds_sync();
+      // recompute edge features and the first hidden layer (cheap: K = dim+1)
+      const int64_t s = a.send[ec], r = a.recv[ec];
+      float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      float ss = 0.0f;
+      for (int cc = 0; cc < a.dim; ++cc) {
+        const float d = __fdiv_rn(__fsub_rn(a.pos[s * a.stride + cc], a.pos[r * a.stride + cc]), a.radius);
+        f[cc] = d;
+        ss = __fadd_rn(ss, __fmul_rn(d, d));
+      }
+      f[a.dim] = sqrtf(ss);
+      acc_bias<TH>(h1, b1);
+      mfma_step<TH>(h1, W1, ld1, h, h ? f[1] : f[0]);
+      mfma_step<TH>(h1, W1, ld1, 2 + h, h ? f[3] : f[2]);
+      acc_relu<TH>(h1);
+      zero_if<TH>(h1, !valid);
+      if (valid && h == 0) {
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) fx[0][cc] = f[cc];
+      }
+    }
+    lds_store_items<TH>(sA, ldh, j, dy);
+    lds_store_items<TH>(sB, ldh, j, h1);
+    wave_lds_sync();
+    lane_sums<TH>(s_db2, sA, ldh, nvalid);
+    __syncthreads();
+    outer_tiles<NT2>(acc_w2, TH, TH, bufA, ldh, 0, bufB, ldh, 0);
+    __syncthreads();
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    mfma_from_acc<TH, TH>(dh, W2T, ldh, 0, dy);
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dh[t][r] = h1[t][r] > 0.0f ? dh[t][r] : 0.0f;
+    lds_store_items<TH>(sA, ldh, j, dh);
+    lds_store_items<1>(bufB + w * 32 * ldf, ldf, j, fx);
+    wave_lds_sync();
+    lane_sums<TH>(s_db1, sA, ldh, nvalid);
+    __syncthreads();
+    outer_tiles<NT1>(acc_w1, TH, 1, bufA, ldh, 0, bufB, ldf, 0);
+    __syncthreads();
+  }
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  store_outer<NT2>(slab, H, TH, TH, acc_w2);
+  store_outer<NT1>(slab + H * H, 32, TH, 1, acc_w1);
+  float* v = slab + H * H + H * 32;
+  store_lane_vec<TH>(v, s_db1);
+  store_lane_vec<TH>(v + kWaves * H, s_db2);
+  store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
+  store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
+}
+
+// ===========================================================================
+// Slab reduction: out[r][c] = scale * sum_g sum_q slab_g[off + q*rep + r*ld + c]
+__global__ __launch_bounds__(256) void k_reduce_slabs(const sgnn_reduce_desc* descs) {
+  const sgnn_reduce_desc d = descs[blockIdx.y];
+  const int64_t total = (int64_t)d.nrows * d.ncols;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
+    float s = 0.0f;
+    for (int g = 0; g < d.nslab; ++g) {
+      const float* p = d.src + (int64_t)g * d.slab_stride + d.offset + (int64_t)r * d.src_ld + cc;
+      for (int q = 0; q < d.nrep; ++q) s += p[(int64_t)q * d.rep_stride];
+    }
+    s *= d.scale;
+    float* o = d.dst + (int64_t)r * d.dst_ld + cc;
+    *o = d.accumulate ? *o + s : s;
+  }
+}
+
+// ===========================================================================
+// Sender-sorted transpose of the receiver CSR (for dV): tptr[s] .. tptr[s+1]
+// lists the edge ids with sender s in ascending order (deterministic).
+__global__ __launch_bounds__(256) void k_tcsr_count(const int32_t* rowptr, int64_t n,
+                                                    const int32_t* send, int32_t* cnt) {
+  const int64_t E = rowptr[n];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[send[e]], 1);
+}
+
+__global__ __launch_bounds__(256) void k_tcsr_fill(const int32_t* rowptr, int64_t n,
+                                                   const int32_t* send, const int32_t* tptr,
+                                                   int32_t* fill, int32_t* raw) {
+  const int64_t E = rowptr[n];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t s = send[e];
+    raw[tptr[s] + atomicAdd(&fill[s], 1)] = (int32_t)e;
+  }
+}
+
+// one wave per sender segment: rank = number of smaller edge ids in the segment
+__global__ __launch_bounds__(256) void k_tcsr_sort(const int32_t* tptr, int64_t n,
+                                                   const int32_t* raw, int32_t* perm) {
+  const int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (s >= n) return;
+  const int lane = lane_id();
+  const int32_t b = tptr[s], len = tptr[s + 1] - b;
+  for (int q = lane; q < len; q += 64) {
+    const int32_t key = raw[b + q];
+    int rank = 0;
+    for (int t = 0; t < len; ++t) rank += raw[b + t] < key;
+    perm[b + rank] = key;
+  }
+}
+
+template <typename K>
+void set_lds(K kernel, size_t bytes) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+extern "C" int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat) {
+  const int64_t H = hidden, W = kWaves;
+  const int64_t fpad = 32 * ((feat + 31) / 32);
+  switch (kind) {
+    case SGNN_SLAB_EDGE: return 2 * H * H + 3 * W * H;
+    case SGNN_SLAB_NODE: return 3 * H * H + 4 * W * H;
+    case SGNN_SLAB_UV: return 2 * H * H + W * H;
+    case SGNN_SLAB_DECODER: return 32 * H + H * H + W * 32 + W * H + W * 8;
+    case SGNN_SLAB_ENC_NODE: return H * H + H * fpad + 4 * W * H;
+    case SGNN_SLAB_ENC_EDGE: return H * H + H * 32 + 4 * W * H;
+    default: return -1;
+  }
+}
+
+static size_t bwd_lds(int kind, int H, int tkf) {
+  const size_t ldh = H + 4, chunk = kChunk;
+  switch (kind) {
+    case SGNN_SLAB_EDGE: return 4 * (2 * H * ldh + H + 2 * chunk * ldh);
+    case SGNN_SLAB_NODE: return 4 * (3 * H * ldh + H + 2 * chunk * ldh);
+    case SGNN_SLAB_UV: return 4 * (2 * H * ldh + 2 * chunk * ldh);
+    case SGNN_SLAB_DECODER: return 4 * (H * ldh + H * 36 + 2 * chunk * ldh);
+    case SGNN_SLAB_ENC_NODE: {
+      const size_t ldb = std::max<size_t>(ldh, 32 * tkf + 4);
+      return 4 * (H * ldh + H + chunk * ldh + chunk * ldb);
+    }
+    case SGNN_SLAB_ENC_EDGE: return 4 * (H * 5 + H * ldh + 2 * H + 2 * chunk * ldh);
+    default: return 0;
+  }
+}
+
+#define CHECK_H(H, what) \
+  if ((H) != 64) return sgnn::set_error(SGNN_ERR_UNSUPPORTED, what ": hidden must be 64 in this build")
+
+extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t* send,
+                                   const int32_t* recv, int64_t n, const float* h_save,
+                                   const float* yhat_save, const float* rstd_save,
+                                   const float* e0t, float e_scale, const sgnn_mlp* edge_fn,
+                                   float* du, float* cin, float* cout, float* dh_rows, float* de0t,
+                                   int32_t de0_accumulate, float* slab, int32_t nslab,
+                                   void* stream) {
+  using namespace sgnn;
+  if (!edge_fn || !dagg || !rowptr || !send || !recv || !h_save || !yhat_save || !rstd_save ||
+      !e0t || !du || !cin || !cout || !dh_rows || !de0t || !slab || nslab < 1 || n <= 0)
+    return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: bad arguments");
+  const int H = edge_fn->hidden;
+  CHECK_H(H, "edge_layer_bwd");
+  EdgeBwdArgs a{dagg, rowptr, send, recv, n, h_save, yhat_save, rstd_save, e0t, e_scale,
+                edge_fn->w2, edge_fn->w1 + 2 * H, edge_fn->ln_g, du, cin, cout, dh_rows, de0t,
+                de0_accumulate, slab, sgnn_bwd_slab_floats(SGNN_SLAB_EDGE, H, 0)};
+  const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0);
+  set_lds(k_edge_bwd<2>, lds);
+  hipLaunchKernelGGL((k_edge_bwd<2>), dim3(nslab), dim3(kBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
+  return check_launch("edge_layer_bwd");
+}
+
+extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const float* yhat_save,
+                                   const float* rstd_save, const float* h_save,
+                                   const float* agg_save, const float* x_in,
+                                   const sgnn_mlp* node_fn, float* dagg, float* dxp, float* slab,
+                                   int32_t nslab, void* stream) {
+  using namespace sgnn;
+  if (!node_fn || !g || !yhat_save || !rstd_save || !h_save || !agg_save || !x_in || !dagg ||
+      !dxp || !slab || nslab < 1 || n <= 0)
+    return set_error(SGNN_ERR_INVALID, "node_layer_bwd: bad arguments");
+  const int H = node_fn->hidden;
+  CHECK_H(H, "node_layer_bwd");
+  NodeBwdArgs a{g, n, yhat_save, rstd_save, h_save, agg_save, x_in, node_fn->w1, node_fn->w2,
+                node_fn->ln_g, dagg, dxp, slab, sgnn_bwd_slab_floats(SGNN_SLAB_NODE, H, 0)};
+  const size_t lds = bwd_lds(SGNN_SLAB_NODE, H, 0);
+  set_lds(k_node_bwd<2>, lds);
+  hipLaunchKernelGGL((k_node_bwd<2>), dim3(nslab), dim3(kBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
+  return check_launch("node_layer_bwd");
+}
+
+extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, const float* cout,
+                           const int32_t* rowptr, const float* dh_rows, const int32_t* tptr,
+                           const int32_t* tperm, const float* x_in, int64_t n,
+                           const sgnn_mlp* edge_fn, float* g, float* slab, int32_t nslab,
+                           void* stream) {
+  using namespace sgnn;
+  if (!edge_fn || !dxp || !du || !cin || !cout || !rowptr || !dh_rows || !tptr || !tperm ||
+      !x_in || !g || !slab || nslab < 1 || n <= 0)
+    return set_error(SGNN_ERR_INVALID, "uv_bwd: bad arguments");
+  const int H = edge_fn->hidden;
+  CHECK_H(H, "uv_bwd");
+  UvBwdArgs a{dxp, du, cin, cout, rowptr, dh_rows, tptr, tperm, x_in, n, edge_fn->w1, g, slab,
+              sgnn_bwd_slab_floats(SGNN_SLAB_UV, H, 0)};
+  const size_t lds = bwd_lds(SGNN_SLAB_UV, H, 0);
+  set_lds(k_uv_bwd<2>, lds);
+  hipLaunchKernelGGL((k_uv_bwd<2>), dim3(nslab), dim3(kBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
+  return check_launch("uv_bwd");
+}
+
+extern "C" int sgnn_decoder_loss_bwd(const float* pred, const float* pos_seq,
+                                     const float* next_pos, const float* noise,
+                                     const float* next_strain, const float* acc_mean,
+                                     const float* acc_std, int64_t n, int32_t T, int32_t dim,
+                                     float w_pos, float w_strain, float inv_count,
+                                     const float* dpred, const float* hd_save, const float* x_last,
+                                     const sgnn_mlp* decoder, float* g, float* slab,
+                                     int32_t nslab, void* stream) {
+  using namespace sgnn;
+  if (!decoder || !pred || !hd_save || !x_last || !g || !slab || nslab < 1 || n <= 0 || T < 2 ||
+      dim < 1 || dim > 3 ||
+      (!dpred && (!pos_seq || !next_pos || !next_strain || !acc_mean || !acc_std)))
+    return set_error(SGNN_ERR_INVALID, "decoder_loss_bwd: bad arguments");
+  const int H = decoder->hidden;
+  CHECK_H(H, "decoder_loss_bwd");
+  if (decoder->out_dim != dim + 1) return set_error(SGNN_ERR_INVALID, "decoder_loss_bwd: out dim");
+  DecBwdArgs a{pred, pos_seq, next_pos, noise, next_strain, acc_mean, acc_std, n, T, dim,
+               w_pos, w_strain, inv_count, dpred, hd_save, x_last, decoder->w1, decoder->w2, g, slab,
+               sgnn_bwd_slab_floats(SGNN_SLAB_DECODER, H, 0)};
+  const size_t lds = bwd_lds(SGNN_SLAB_DECODER, H, 0);
+  set_lds(k_dec_bwd<2>, lds);
+  hipLaunchKernelGGL((k_dec_bwd<2>), dim3(nslab), dim3(kBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
+  return check_launch("decoder_loss_bwd");
+}
+
+extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
+                                     int32_t dim, const float* vel_mean, const float* vel_std,
+                                     float radius, const float* h_save, const float* yhat_save,
+                                     const float* rstd_save, const sgnn_mlp* enc, float* slab,
+                                     int32_t nslab, void* stream) {
+  using namespace sgnn;
+  if (!enc || !g || !pos_seq || !vel_mean || !vel_std || !h_save || !yhat_save || !rstd_save ||
+      !slab || nslab < 1 || n <= 0)
+    return set_error(SGNN_ERR_INVALID, "encode_nodes_bwd: bad arguments");
+  const int H = enc->hidden;
+  CHECK_H(H, "encode_nodes_bwd");
+  const int feat = (T - 1) * dim + 1;
+  if (enc->in_dim != feat)
+    return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd: particle-type embeddings not supported");
+  const int tkf = (feat + 31) / 32;
+  EncNodeBwdArgs a{g, pos_seq, n, T, dim, feat, vel_mean, vel_std, radius, h_save, yhat_save,
+                   rstd_save, enc->w2, enc->ln_g, slab,
+                   sgnn_bwd_slab_floats(SGNN_SLAB_ENC_NODE, H, feat)};
+  const size_t lds = bwd_lds(SGNN_SLAB_ENC_NODE, H, tkf);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (tkf == 1) {
+    set_lds(k_enc_node_bwd<2, 1>, lds);
+    hipLaunchKernelGGL((k_enc_node_bwd<2, 1>), dim3(nslab), dim3(kBlock), lds, s, a);
+  } else if (tkf == 2) {
+    set_lds(k_enc_node_bwd<2, 2>, lds);
+    hipLaunchKernelGGL((k_enc_node_bwd<2, 2>), dim3(nslab), dim3(kBlock), lds, s, a);
+  } else {
+    return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd: > 64 node features");
+  }
+  return check_launch("encode_nodes_bwd");
+}
+
+extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_stride,
+                                     int32_t dim, float radius, const int32_t* rowptr,
+                                     const int32_t* send, const int32_t* recv, int64_t n,
+                                     const float* yhat_save, const float* rstd_save,
+                                     const sgnn_mlp* enc, float* slab, int32_t nslab,
+                                     void* stream) {
+  using namespace sgnn;
+  if (!enc || !de0t || !pos || !rowptr || !send || !recv || !yhat_save || !rstd_save || !slab ||
+      nslab < 1 || n <= 0)
+    return set_error(SGNN_ERR_INVALID, "encode_edges_bwd: bad arguments");
+  const int H = enc->hidden;
+  CHECK_H(H, "encode_edges_bwd");
+  EncEdgeBwdArgs a{de0t, pos, pos_stride, dim, radius, rowptr, send, recv, n, yhat_save,
+                   rstd_save, enc->w1, enc->b1, enc->w2, enc->ln_g, slab,
+                   sgnn_bwd_slab_floats(SGNN_SLAB_ENC_EDGE, H, 0)};
+  const size_t lds = bwd_lds(SGNN_SLAB_ENC_EDGE, H, 0);
+  set_lds(k_enc_edge_bwd<2>, lds);
+  hipLaunchKernelGGL((k_enc_edge_bwd<2>), dim3(nslab), dim3(kBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
+  return check_launch("encode_edges_bwd");
+}
+
+extern "C" int sgnn_reduce_slabs(const sgnn_reduce_desc* descs_dev, int32_t ndesc,
+                                 int64_t max_elems, void* stream) {
+  using namespace sgnn;
+  if (!descs_dev || ndesc < 1 || ndesc > 65535 || max_elems < 1)
+    return set_error(SGNN_ERR_INVALID, "reduce_slabs: bad arguments");
+  const unsigned gx = (unsigned)std::min<int64_t>((max_elems + 255) / 256, 64);
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(gx, (unsigned)ndesc), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), descs_dev);
+  return check_launch("reduce_slabs");
+}
+
+extern "C" size_t sgnn_transpose_workspace_bytes(int64_t n, int64_t edge_cap) {
+  return sizeof(int32_t) * (size_t)(2 * (n + 1) + edge_cap) + 3 * 256 + 65536;
+}
+
+extern "C" int sgnn_transpose_csr(const int32_t* rowptr, const int32_t* send, int64_t n,
+                                  int64_t edge_cap, void* workspace, int32_t* tptr,
+                                  int32_t* tperm, void* stream) {
+  using namespace sgnn;
+  if (!rowptr || !send || !workspace || !tptr || !tperm || n <= 0 || edge_cap < 1)
+    return set_error(SGNN_ERR_INVALID, "transpose_csr: bad arguments");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  char* p = static_cast<char*>(workspace);
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += (bytes + 255) & ~size_t(255);
+    return r;
+  };
+  int32_t* cnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 2 * (n + 1)));
+  int32_t* fill = cnt + (n + 1);
+  int32_t* raw = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * edge_cap));
+  int32_t* partials = reinterpret_cast<int32_t*>(take(65536 - 512));
+  (void)hipMemsetAsync(cnt, 0, sizeof(int32_t) * 2 * (n + 1), s);
+  const unsigned g = (unsigned)std::min<int64_t>((edge_cap + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_tcsr_count, dim3(g), dim3(256), 0, s, rowptr, n, send, cnt);
+  int st = scan_exclusive(cnt, tptr, n + 1, partials, s);
+  if (st) return st;
+  hipLaunchKernelGGL(k_tcsr_fill, dim3(g), dim3(256), 0, s, rowptr, n, send, tptr, fill, raw);
+  hipLaunchKernelGGL(k_tcsr_sort, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, tptr, n, raw,
+                     tperm);
+  return check_launch("transpose_csr");
+}

@@ -41,6 +41,7 @@ struct EncNodeArgs {
   const float *w1, *b1, *w2, *b2, *g, *bb;  // encoder node MLP
   const float *we, *be;                     // edge0 W1 [H][3H], b1
   float *x0, *u, *v;
+  sgnn_saves sv;
 };
 
 template <int TH>
@@ -55,7 +56,7 @@ SGNN_DEV void store_uv(const float* Wi, const float* Wj, const float* b1e, int l
   if (valid) store_row_clayout<TH>(v_row, acc);
 }
 
-template <int TH, int TKF>
+template <int TH, int TKF, bool TRAIN>
 __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
   constexpr int H = 32 * TH, ldh = H + 4, ldf = 32 * TKF + 4;
   extern __shared__ float lds[];
@@ -109,10 +110,21 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
     acc_bias<TH>(hacc, b1);
     mfma_from_acc<TH, TKF>(hacc, W1, ldf, 0, xf);
     acc_relu<TH>(hacc);
+    if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
     f32x16 y[TH];
     acc_bias<TH>(y, b2);
     mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
-    acc_layernorm<TH>(y, g, bb);
+    if (TRAIN) {
+      f32x16 yh[TH];
+      float rs;
+      acc_layernorm_save<TH>(y, g, bb, yh, rs);
+      if (valid) {
+        store_row_clayout<TH>(a.sv.yhat + i * H, yh);
+        if (h == 0) a.sv.rstd[i] = rs;
+      }
+    } else {
+      acc_layernorm<TH>(y, g, bb);
+    }
     if (valid) store_row_clayout<TH>(a.x0 + i * H, y);
     store_uv<TH>(Wi, Wj, b1e, ldh, y, a.u + i * H, a.v + i * H, valid);
   }
@@ -127,9 +139,10 @@ struct EncEdgeArgs {
   int64_t n;
   const float *w1, *b1, *w2, *b2, *g, *bb;
   float* e0t;
+  sgnn_saves sv;
 };
 
-template <int TH>
+template <int TH, bool TRAIN>
 __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
   constexpr int H = 32 * TH, ldh = H + 4, ld1 = 5;
   extern __shared__ float lds[];
@@ -171,7 +184,15 @@ __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
     f32x16 y[TH];
     acc_bias<TH>(y, b2);
     mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
-    acc_layernorm<TH>(y, g, bb);
+    if (TRAIN) {
+      f32x16 yh[TH];
+      float rs;
+      acc_layernorm_save<TH>(y, g, bb, yh, rs);
+      store_tiled<TH>(a.sv.yhat + tile * (32 * H), yh);
+      if (h == 0 && e < E) a.sv.rstd[e] = rs;
+    } else {
+      acc_layernorm<TH>(y, g, bb);
+    }
     float* dst = a.e0t + tile * (32 * H) + l * 4;
 #pragma unroll
     for (int t = 0; t < TH; ++t)
@@ -192,15 +213,10 @@ struct EdgeLayerArgs {
   int64_t n;
   const float *we, *w2, *b2, *g, *bb;  // we = edge W1 + 2H (ld 3H)
   float *agg, *cin, *cout;
+  sgnn_saves sv;
 };
 
-SGNN_DEV void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <int TH>
+template <int TH, bool TRAIN>
 __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
   constexpr int H = 32 * TH, ldh = H + 4;
   extern __shared__ float lds[];
@@ -240,10 +256,19 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     for (int q = 0; q < TH * 4; ++q) xg[q] = ld4(src + q * 256);
     mfma_from_groups<TH, TH>(hacc, We, ldh, 0, xg, a.e_scale);
     acc_relu<TH>(hacc);
+    if (TRAIN) store_tiled<TH>(a.sv.h + tile * (32 * H), hacc);
     f32x16 y[TH];
     acc_bias<TH>(y, b2);
     mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
-    acc_layernorm<TH>(y, g, bb);
+    if (TRAIN) {
+      f32x16 yh[TH];
+      float rs;
+      acc_layernorm_save<TH>(y, g, bb, yh, rs);
+      store_tiled<TH>(a.sv.yhat + tile * (32 * H), yh);
+      if (h == 0 && valid) a.sv.rstd[e] = rs;
+    } else {
+      acc_layernorm<TH>(y, g, bb);
+    }
 #pragma unroll
     for (int t = 0; t < TH; ++t)
 #pragma unroll
@@ -300,6 +325,7 @@ struct NodeLayerArgs {
   const float *acc_mean, *acc_std;
   float *pred, *next_pos, *window_out;
   float* x_out;
+  sgnn_saves sv;
 };
 
 template <int TH>
@@ -322,7 +348,7 @@ SGNN_DEV void load_agg(f32x16 (&a)[TH], const NodeLayerArgs& p, int64_t i) {
   }
 }
 
-template <int TH, int MODE>
+template <int TH, int MODE, bool TRAIN>
 __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
   constexpr int H = 32 * TH, ldh = H + 4, ld2 = 2 * H + 4;
   extern __shared__ float lds[];
@@ -362,16 +388,28 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
     const int64_t ic = valid ? i : a.n - 1;
     f32x16 ag[TH], x[TH];
     load_agg<TH>(ag, a, ic);
+    if (TRAIN && valid) store_row_clayout<TH>(a.sv.agg + i * H, ag);
     load_row_clayout<TH>(x, a.x_in + ic * H);
     f32x16 hacc[TH];
     acc_bias<TH>(hacc, b1);
     mfma_from_acc<TH, TH>(hacc, W1, ld2, 0, ag);   // graph_network.py:220 cat([aggr, x])
     mfma_from_acc<TH, TH>(hacc, W1, ld2, H, x);
     acc_relu<TH>(hacc);
+    if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
     f32x16 y[TH];
     acc_bias<TH>(y, b2);
     mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
-    acc_layernorm<TH>(y, g, bb);
+    if (TRAIN) {
+      f32x16 yh[TH];
+      float rs;
+      acc_layernorm_save<TH>(y, g, bb, yh, rs);
+      if (valid) {
+        store_row_clayout<TH>(a.sv.yhat + i * H, yh);
+        if (h == 0) a.sv.rstd[i] = rs;
+      }
+    } else {
+      acc_layernorm<TH>(y, g, bb);
+    }
 #pragma unroll
     for (int t = 0; t < TH; ++t)
 #pragma unroll
@@ -384,6 +422,7 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
       acc_bias<TH>(hd, ba);
       mfma_from_acc<TH, TH>(hd, Wa, ldh, 0, x);
       acc_relu<TH>(hd);
+      if (TRAIN && valid) store_row_clayout<TH>(a.sv.hd + i * H, hd);
       f32x16 o[1];
       acc_bias<1>(o, bd2);
       mfma_from_acc<1, TH>(o, Wb, ldh, 0, hd);
@@ -428,6 +467,19 @@ void set_lds(K kernel, size_t bytes) {
 
 constexpr size_t kLdsMax = 160 * 1024;
 
+template <typename KI, typename KT, typename A>
+void launch2(KI ki, KT kt, bool train, unsigned grid, size_t lds, hipStream_t s, const A& a) {
+  if (train) {
+    set_lds(kt, lds);
+    hipLaunchKernelGGL(kt, dim3(grid), dim3(kBlock), lds, s, a);
+  } else {
+    set_lds(ki, lds);
+    hipLaunchKernelGGL(ki, dim3(grid), dim3(kBlock), lds, s, a);
+  }
+}
+
+bool want_saves(const sgnn_saves* sv) { return sv != nullptr && sv->yhat != nullptr; }
+
 }  // namespace
 
 extern "C" int64_t sgnn_edge_latent_floats(int64_t edge_cap, int32_t hidden) {
@@ -438,7 +490,8 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
                                  const int64_t* types, const float* emb_w, int32_t emb_dim,
                                  int32_t use_emb, const float* vel_mean, const float* vel_std,
                                  float radius, const sgnn_mlp* enc, const sgnn_mlp* edge0,
-                                 float* x0, float* u, float* v, void* stream) {
+                                 float* x0, float* u, float* v, const sgnn_saves* saves,
+                                 void* stream) {
   using namespace sgnn;
   if (n <= 0) return SGNN_OK;
   if (!pos_seq || !vel_mean || !vel_std || !x0 || !u || !v || T < 2 || dim < 1 || dim > 3)
@@ -453,19 +506,21 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
   if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: hidden must be 64 in this build");
   EncNodeArgs a{pos_seq, n, T, dim, types, emb_w, emb_dim, use_emb, vel_mean, vel_std, radius,
                 feat, enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, edge0->w1,
-                edge0->b1, x0, u, v};
+                edge0->b1, x0, u, v, {}};
+  const bool train = want_saves(saves);
+  if (train) {
+    if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "encode_nodes: saves");
+    a.sv = *saves;
+  }
   const unsigned grid = persistent_grid(n, 32 * kWaves, 2);
   const int tkf = (feat + 31) / 32;
   const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + 3 * H * (H + 4) + 5 * H);
   if (lds > kLdsMax) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: too many features");
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (tkf) {
-    case 1: set_lds(k_encode_nodes<2, 1>, lds);
-      hipLaunchKernelGGL((k_encode_nodes<2, 1>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 2: set_lds(k_encode_nodes<2, 2>, lds);
-      hipLaunchKernelGGL((k_encode_nodes<2, 2>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 3: set_lds(k_encode_nodes<2, 3>, lds);
-      hipLaunchKernelGGL((k_encode_nodes<2, 3>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 1: launch2(k_encode_nodes<2, 1, false>, k_encode_nodes<2, 1, true>, train, grid, lds, s, a); break;
+    case 2: launch2(k_encode_nodes<2, 2, false>, k_encode_nodes<2, 2, true>, train, grid, lds, s, a); break;
+    case 3: launch2(k_encode_nodes<2, 3, false>, k_encode_nodes<2, 3, true>, train, grid, lds, s, a); break;
     default: return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: > 96 node features");
   }
   return check_launch("encode_nodes");
@@ -474,7 +529,7 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
 extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t dim, float radius,
                                  const int32_t* rowptr, const int32_t* send, const int32_t* recv,
                                  int64_t n, int64_t edge_cap, const sgnn_mlp* enc, float* e0t,
-                                 void* stream) {
+                                 const sgnn_saves* saves, void* stream) {
   using namespace sgnn;
   if (n <= 0 || edge_cap <= 0) return SGNN_OK;
   if (!pos || !rowptr || !send || !recv || !e0t || dim < 1 || dim > 3)
@@ -485,18 +540,23 @@ extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t d
   if (st) return st;
   if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_edges: hidden must be 64 in this build");
   EncEdgeArgs a{pos, pos_stride, dim, radius, rowptr, send, recv, n,
-                enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, e0t};
+                enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, e0t, {}};
+  const bool train = want_saves(saves);
+  if (train) {
+    if (!saves->rstd) return set_error(SGNN_ERR_INVALID, "encode_edges: saves");
+    a.sv = *saves;
+  }
   const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 4);
   const size_t lds = sizeof(float) * (size_t)(H * 5 + H * (H + 4) + 4 * H);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL((k_encode_edges<2>), dim3(grid), dim3(kBlock), lds, s, a);
+  launch2(k_encode_edges<2, false>, k_encode_edges<2, true>, train, grid, lds, s, a);
   return check_launch("encode_edges");
 }
 
 extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t, float e_scale,
                                const int32_t* rowptr, const int32_t* send, const int32_t* recv,
                                int64_t n, int64_t edge_cap, const sgnn_mlp* edge_fn, float* agg,
-                               float* cin, float* cout, void* stream) {
+                               float* cin, float* cout, const sgnn_saves* saves, void* stream) {
   using namespace sgnn;
   if (n <= 0 || edge_cap <= 0) return SGNN_OK;
   if (!u || !v || !e0t || !rowptr || !send || !recv || !agg || !cin || !cout || !edge_fn)
@@ -506,16 +566,21 @@ extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t,
   if (st) return st;
   if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer: hidden must be 64 in this build");
   EdgeLayerArgs a{u, v, e0t, e_scale, rowptr, send, recv, n, edge_fn->w1 + 2 * H, edge_fn->w2,
-                  edge_fn->b2, edge_fn->ln_g, edge_fn->ln_b, agg, cin, cout};
+                  edge_fn->b2, edge_fn->ln_g, edge_fn->ln_b, agg, cin, cout, {}};
+  const bool train = want_saves(saves);
+  if (train) {
+    if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "edge_layer: saves");
+    a.sv = *saves;
+  }
   const size_t lds = sizeof(float) * (size_t)(2 * H * (H + 4) + 3 * H + kWaves * 32 * (H + 4));
   const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 2);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  set_lds(k_edge_layer<2>, lds);
-  hipLaunchKernelGGL((k_edge_layer<2>), dim3(grid), dim3(kBlock), lds, s, a);
+  launch2(k_edge_layer<2, false>, k_edge_layer<2, true>, train, grid, lds, s, a);
   return check_launch("edge_layer");
 }
 
-static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode, void* stream) {
+static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode,
+                             const sgnn_saves* saves, void* stream) {
   using namespace sgnn;
   const int H = node_fn ? node_fn->hidden : 0;
   int st = check_mlp(node_fn, 2 * H, H, H, true, "node_layer: node MLP shape");
@@ -523,23 +588,24 @@ static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode
   if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "node_layer: hidden must be 64 in this build");
   a.w1 = node_fn->w1; a.b1 = node_fn->b1; a.w2 = node_fn->w2; a.b2 = node_fn->b2;
   a.g = node_fn->ln_g; a.bb = node_fn->ln_b;
+  const bool train = want_saves(saves);
+  if (train) {
+    if (!saves->h || !saves->rstd || !saves->agg || (mode == 1 && (!saves->hd || !a.x_out)))
+      return set_error(SGNN_ERR_INVALID, "node_layer: saves");
+    a.sv = *saves;
+  }
   const size_t lds = sizeof(float) * (size_t)(H * (2 * H + 4) + 3 * H * (H + 4) + 5 * H + 32);
   const unsigned grid = persistent_grid(a.n, 32 * kWaves, 1);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (mode == 0) {
-    set_lds(k_node_layer<2, 0>, lds);
-    hipLaunchKernelGGL((k_node_layer<2, 0>), dim3(grid), dim3(kBlock), lds, s, a);
-  } else {
-    set_lds(k_node_layer<2, 1>, lds);
-    hipLaunchKernelGGL((k_node_layer<2, 1>), dim3(grid), dim3(kBlock), lds, s, a);
-  }
+  if (mode == 0) launch2(k_node_layer<2, 0, false>, k_node_layer<2, 0, true>, train, grid, lds, s, a);
+  else launch2(k_node_layer<2, 1, false>, k_node_layer<2, 1, true>, train, grid, lds, s, a);
   return check_launch("node_layer");
 }
 
 extern "C" int sgnn_node_layer(const float* x_in, const float* agg, const float* cin,
                                const float* cout, const int32_t* rowptr, int64_t n,
                                const sgnn_mlp* node_fn, const sgnn_mlp* next_edge, float* x_out,
-                               float* u, float* v, void* stream) {
+                               float* u, float* v, const sgnn_saves* saves, void* stream) {
   using namespace sgnn;
   if (n <= 0) return SGNN_OK;
   if (!x_in || !agg || !cin || !cout || !rowptr || !x_out || !u || !v || !next_edge)
@@ -550,7 +616,7 @@ extern "C" int sgnn_node_layer(const float* x_in, const float* agg, const float*
   NodeLayerArgs a{};
   a.x_in = x_in; a.agg = agg; a.cin = cin; a.cout = cout; a.rowptr = rowptr; a.n = n;
   a.we = next_edge->w1; a.be = next_edge->b1; a.u = u; a.v = v; a.x_out = x_out;
-  return node_layer_common(a, node_fn, 0, stream);
+  return node_layer_common(a, node_fn, 0, saves, stream);
 }
 
 extern "C" int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin,
@@ -559,7 +625,7 @@ extern "C" int sgnn_node_layer_decode(const float* x_in, const float* agg, const
                                       const float* pos_seq, int32_t T, int32_t dim,
                                       const float* acc_mean, const float* acc_std, float* x_out,
                                       float* pred, float* next_pos, float* window_out,
-                                      void* stream) {
+                                      const sgnn_saves* saves, void* stream) {
   using namespace sgnn;
   if (n <= 0) return SGNN_OK;
   if (!x_in || !agg || !cin || !cout || !rowptr || !pos_seq || !acc_mean || !acc_std || !pred ||
@@ -574,5 +640,5 @@ extern "C" int sgnn_node_layer_decode(const float* x_in, const float* agg, const
   a.pos_seq = pos_seq; a.T = T; a.dim = dim; a.acc_mean = acc_mean; a.acc_std = acc_std;
   a.pred = pred; a.next_pos = next_pos; a.window_out = window_out; a.x_out = x_out;
   if (window_out == pos_seq) return set_error(SGNN_ERR_INVALID, "node_layer_decode: window_out aliases pos_seq");
-  return node_layer_common(a, node_fn, 1, stream);
+  return node_layer_common(a, node_fn, 1, saves, stream);
 }

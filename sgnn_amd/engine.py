@@ -169,11 +169,11 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
                               _ptr(emb_weight) if use_emb else 0, emb_dim, int(use_emb),
                               inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius),
                               ctypes.byref(pk.enc_node), ctypes.byref(pk.edge[0]),
-                              ws.x_a.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), s),
+                              ws.x_a.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), None, s),
           "sgnn_encode_nodes")
     check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius),
                               ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
-                              ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(), s),
+                              ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(), None, s),
           "sgnn_encode_edges")
     x_in, x_out = ws.x_a, ws.x_b
     nl = len(pk.edge)
@@ -184,7 +184,7 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
         check(L.sgnn_edge_layer(ws.u.data_ptr(), ws.v.data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
                                 ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
                                 ws.edge_cap, ctypes.byref(pk.edge[k]), ws.agg.data_ptr(),
-                                ws.cin.data_ptr(), ws.cout.data_ptr(), s), "sgnn_edge_layer")
+                                ws.cin.data_ptr(), ws.cout.data_ptr(), None, s), "sgnn_edge_layer")
         if timers is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
@@ -193,7 +193,7 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
             check(L.sgnn_node_layer(x_in.data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
                                     ws.cout.data_ptr(), ws.rowptr.data_ptr(), n,
                                     ctypes.byref(pk.node[k]), ctypes.byref(pk.edge[k + 1]),
-                                    x_out.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), s),
+                                    x_out.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), None, s),
                   "sgnn_node_layer")
             x_in, x_out = x_out, x_in
         else:
@@ -202,7 +202,7 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
                                            ctypes.byref(pk.node[k]), ctypes.byref(pk.dec),
                                            pos.data_ptr(), T, d, inp.acc_mean.data_ptr(),
                                            inp.acc_std.data_ptr(), 0, pred.data_ptr(),
-                                           next_pos.data_ptr(), _ptr(window_out), s),
+                                           next_pos.data_ptr(), _ptr(window_out), None, s),
                   "sgnn_node_layer_decode")
 
 

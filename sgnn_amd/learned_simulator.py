@@ -11,8 +11,36 @@ from typing import Dict, Tuple
 import torch
 import torch.nn as nn
 
-from . import engine, graph_network
+from . import engine, graph_network, training
 from ._hip import require_gpu_tensor
+
+
+class _TrainedEPD(torch.autograd.Function):
+    """pred = EncodeProcessDecode(features(noisy window)) with a HIP backward
+    (graph_network.py:388-406 under autograd).  One forward may be in flight
+    per workspace: a second forward before backward invalidates the first."""
+
+    @staticmethod
+    def forward(ctx, sim, inp, tw, *params):
+        training.train_forward(sim._encode_process_decode, sim._connectivity_radius, inp, tw)
+        tw.generation = getattr(tw, "generation", 0) + 1
+        ctx.sim, ctx.inp, ctx.tw, ctx.gen = sim, inp, tw, tw.generation
+        return tw.pred.clone()
+
+    @staticmethod
+    def backward(ctx, dpred):
+        sim, tw = ctx.sim, ctx.tw
+        if tw.generation != ctx.gen:
+            raise RuntimeError("sgnn_amd: a newer predict_accelerations overwrote the saved "
+                               "activations of this graph before backward")
+        epd = sim._encode_process_decode
+        scratch = getattr(tw, "grad_scratch", None)
+        if scratch is None:
+            scratch = {k: torch.zeros_like(p) for k, p in epd.named_parameters(prefix="_encode_process_decode")}
+            tw.grad_scratch = scratch
+        training.train_backward(epd, sim._connectivity_radius, ctx.inp, tw, scratch,
+                                dpred=dpred.to(torch.float32).contiguous())
+        return (None, None, None, *[g.clone() for g in scratch.values()])
 
 
 class LearnedSimulator(nn.Module):
@@ -156,13 +184,53 @@ class LearnedSimulator(nn.Module):
                             self._connectivity_radius, inp, ws, pred, next_pos)
         return next_pos, pred[:, -1]
 
+    def predict_accelerations(self, next_positions: torch.Tensor, position_sequence_noise: torch.Tensor,
+                              position_sequence: torch.Tensor, nparticles_per_example,
+                              particle_types: torch.Tensor):
+        """learned_simulator.py:440-491 -> (predicted_normalized_acceleration,
+        target_normalized_acceleration, predicted_strain); differentiable with
+        respect to the EncodeProcessDecode parameters (HIP backward)."""
+        noisy = position_sequence + position_sequence_noise
+        epd = self._encode_process_decode
+        params = list(epd.parameters())
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        inp, use_emb = self._step_inputs(noisy, nparticles_per_example, particle_types)
+        n, T, d = inp.pos_seq.shape
+        if need_grad:
+            training.check_trainable(epd, self._nparticle_types)
+            tw = self._train_workspace(n, T, inp.pos_seq.device)
+            pred = _TrainedEPD.apply(self, inp, tw, *params)
+        else:
+            ws = self._workspace(n, T, inp.pos_seq.device)
+            pred = torch.empty(n, d + 1, dtype=torch.float32, device=inp.pos_seq.device)
+            nxt = torch.empty(n, d, dtype=torch.float32, device=inp.pos_seq.device)
+            engine.forward_step(epd, self._particle_type_embedding.weight, use_emb,
+                                self._connectivity_radius, inp, ws, pred, nxt)
+        next_position_adjusted = next_positions + position_sequence_noise[:, -1]
+        target = self._inverse_decoder_postprocessor(next_position_adjusted, inp.pos_seq)
+        return pred[:, :d], target, pred[:, -1]
+
+    def _train_workspace(self, n: int, T: int, device) -> training.TrainWorkspace:
+        cache = self.__dict__.setdefault("_tw_cache", {})
+        key = (n, T, str(device))
+        tw = cache.get(key)
+        if tw is None:
+            if len(cache) > 4:
+                cache.clear()
+            tw = training.TrainWorkspace(self._encode_process_decode, n, T, self._particle_dimensions,
+                                         self._max_num_neighbors, True, device)
+            cache[key] = tw
+        return tw
+
     def _inverse_decoder_postprocessor(self, next_position, position_sequence):
         """learned_simulator.py:493-517"""
         prev = position_sequence[:, -1]
         prev_vel = prev - position_sequence[:, -2]
         acc = (next_position - prev) - prev_vel
         st = self._normalization_stats["acceleration"]
-        return (acc - st["mean"]) / st["std"]
+        mean = torch.as_tensor(st["mean"]).to(acc.device)
+        std = torch.as_tensor(st["std"]).to(acc.device)
+        return (acc - mean) / std
 
     def save(self, path: str = "model.pt"):
         """learned_simulator.py:519-527"""

@@ -1,0 +1,326 @@
+"""Training step on the HIP kernels: saved-activation forward, fused backward,
+slab reduction into a flat gradient buffer, RCCL all-reduce, fused Adam.
+
+Mirrors the reference training step (sgnn/single_scale/train.py:231-280):
+noise -> LearnedSimulator.predict_accelerations (learned_simulator.py:440-491)
+-> loss (train.py:257-268) -> backward -> Adam -> exponential LR decay.
+Whole-graph data parallelism: each rank owns whole
+graphs; the reference's mean over all particles of the concatenated batch is
+reproduced by scaling every rank's loss gradient by 1/N_global, so the SUM
+all-reduce of the flat gradient equals the single-process gradient.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _hip, engine
+from ._hip import SgnnReduceDesc, SgnnSaves, check, lib, stream_ptr
+
+DEFAULT_NSLAB = 256  # persistent workgroups (one per CU) for the backward kernels
+
+
+class FlatParams:
+    """Point every parameter of `module` into one flat fp32 buffer, and its
+    `.grad` into one flat gradient buffer: one RCCL all-reduce, one Adam launch."""
+
+    def __init__(self, module: nn.Module):
+        params = list(module.parameters())
+        dev = params[0].device
+        total = sum(p.numel() for p in params)
+        self.param = torch.empty(total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.offsets: Dict[int, Tuple[int, int]] = {}
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                self.param[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.param[off:off + n].view_as(p)
+                p.grad = self.grad[off:off + n].view_as(p)
+                self.offsets[id(p)] = (off, n)
+                off += n
+        self.numel = total
+
+
+class TrainWorkspace:
+    """Forward saves + backward buffers + weight-gradient slabs for one shape."""
+
+    def __init__(self, epd: nn.Module, n: int, T: int, dim: int, K: int, loop: bool,
+                 device: torch.device, nslab: int = DEFAULT_NSLAB):
+        L = lib()
+        H, nl = epd.latent_dim, epd.nlayers
+        self.H, self.L, self.n, self.T, self.dim, self.nslab = H, nl, n, T, dim, nslab
+        self.feat = epd.nnode_in
+        self.f = engine.StepWorkspace(n, T, dim, H, K, loop, device)
+        cap = self.f.edge_cap
+        tl = int(L.sgnn_edge_latent_floats(cap, H))
+        f32 = dict(dtype=torch.float32, device=device)
+        e = lambda *s: torch.empty(*s, **f32)
+        self.enc_h, self.enc_yh, self.enc_rstd = e(n, H), e(n, H), e(n)
+        self.ee_yh, self.ee_rstd = e(tl), e(cap)
+        self.e_h = [e(tl) for _ in range(nl)]
+        self.e_yh = [e(tl) for _ in range(nl)]
+        self.e_rstd = [e(cap) for _ in range(nl)]
+        self.n_agg = [e(n, H) for _ in range(nl)]
+        self.n_h = [e(n, H) for _ in range(nl)]
+        self.n_yh = [e(n, H) for _ in range(nl)]
+        self.n_rstd = [e(n) for _ in range(nl)]
+        self.xs = [e(n, H) for _ in range(nl + 1)]
+        self.hd = e(n, H)
+        self.pred = e(n, dim + 1)
+        self.next_scratch = e(n, dim)
+        self.g, self.dxp, self.dagg, self.du = e(n, H), e(n, H), e(n, H), e(n, H)
+        self.dh_rows = e(cap, H)
+        self.de0t = e(tl)
+        i32 = dict(dtype=torch.int32, device=device)
+        self.tptr = torch.empty(n + 1, **i32)
+        self.tperm = torch.empty(cap, **i32)
+        self.tws = torch.empty(int(L.sgnn_transpose_workspace_bytes(n, cap)) + 256, dtype=torch.uint8,
+                               device=device)
+        # slab arena
+        self.slab_floats = {k: int(L.sgnn_bwd_slab_floats(k, H, self.feat)) for k in range(6)}
+        self.slab_off: Dict[Tuple[int, int], int] = {}
+        off = 0
+        keys = [(_hip.SLAB_DECODER, 0)] + [(_hip.SLAB_NODE, k) for k in range(nl)] + \
+               [(_hip.SLAB_EDGE, k) for k in range(nl)] + [(_hip.SLAB_UV, k) for k in range(nl)] + \
+               [(_hip.SLAB_ENC_NODE, 0), (_hip.SLAB_ENC_EDGE, 0)]
+        for key in keys:
+            self.slab_off[key] = off
+            off += nslab * self.slab_floats[key[0]]
+        self.arena = torch.empty(off, **f32)
+        self.loss_out = torch.zeros(8, **f32)
+        self._descs_key = None
+        self._descs_dev = None
+        self._ndesc = 0
+        self._max_elems = 1
+
+    def slab(self, kind: int, k: int = 0) -> int:
+        return self.arena.data_ptr() + 4 * self.slab_off[(kind, k)]
+
+    def tws_ptr(self) -> int:
+        return (self.tws.data_ptr() + 255) & ~255
+
+    # ---------------------------------------------------------------- reduce
+    def descriptors(self, epd: nn.Module, grads: Dict[str, torch.Tensor]) -> None:
+        """Build the slab -> parameter-gradient reduction table (device copy)."""
+        key = tuple(g.data_ptr() for g in grads.values())
+        if key == self._descs_key:
+            return
+        H, nl, ns = self.H, self.L, self.nslab
+        W = 4
+        descs: List[SgnnReduceDesc] = []
+
+        def add(kind, k, offset, dst, nrows, ncols, src_ld, dst_ld=None, nrep=1, rep_stride=0,
+                scale=1.0, dst_off=0):
+            d = SgnnReduceDesc()
+            d.src = self.arena.data_ptr() + 4 * self.slab_off[(kind, k)]
+            d.dst = dst.data_ptr() + 4 * dst_off
+            d.slab_stride = self.slab_floats[kind]
+            d.offset = offset
+            d.rep_stride = rep_stride
+            d.nslab, d.nrep, d.src_ld = ns, nrep, src_ld
+            d.nrows, d.ncols = nrows, ncols
+            d.dst_ld = dst_ld if dst_ld is not None else ncols
+            d.accumulate = 0
+            d.scale = scale
+            descs.append(d)
+
+        pre = "_encode_process_decode."
+        g = lambda name: grads[pre + name]
+        # encoder node MLP  (slab ENC_NODE: dW2 | dW1[H][fpad] | db1 db2 dg db)
+        fpad = 32 * ((self.feat + 31) // 32)
+        vb = H * H + H * fpad
+        e = "_encoder.node_fn."
+        add(_hip.SLAB_ENC_NODE, 0, H * H, g(e + "0.NN-0.weight"), H, self.feat, fpad)
+        add(_hip.SLAB_ENC_NODE, 0, vb, g(e + "0.NN-0.bias"), 1, H, H, nrep=W, rep_stride=H)
+        add(_hip.SLAB_ENC_NODE, 0, 0, g(e + "0.NN-1.weight"), H, H, H)
+        add(_hip.SLAB_ENC_NODE, 0, vb + W * H, g(e + "0.NN-1.bias"), 1, H, H, nrep=W, rep_stride=H)
+        add(_hip.SLAB_ENC_NODE, 0, vb + 2 * W * H, g(e + "1.weight"), 1, H, H, nrep=W, rep_stride=H)
+        add(_hip.SLAB_ENC_NODE, 0, vb + 3 * W * H, g(e + "1.bias"), 1, H, H, nrep=W, rep_stride=H)
+        # encoder edge MLP
+        vb = H * H + H * 32
+        e = "_encoder.edge_fn."
+        add(_hip.SLAB_ENC_EDGE, 0, H * H, g(e + "0.NN-0.weight"), H, self.dim + 1, 32)
+        add(_hip.SLAB_ENC_EDGE, 0, vb, g(e + "0.NN-0.bias"), 1, H, H, nrep=W, rep_stride=H)
+        add(_hip.SLAB_ENC_EDGE, 0, 0, g(e + "0.NN-1.weight"), H, H, H)
+        add(_hip.SLAB_ENC_EDGE, 0, vb + W * H, g(e + "0.NN-1.bias"), 1, H, H, nrep=W, rep_stride=H)
+        add(_hip.SLAB_ENC_EDGE, 0, vb + 2 * W * H, g(e + "1.weight"), 1, H, H, nrep=W, rep_stride=H)
+        add(_hip.SLAB_ENC_EDGE, 0, vb + 3 * W * H, g(e + "1.bias"), 1, H, H, nrep=W, rep_stride=H)
+        for k in range(nl):
+            p = f"_processor.gnn_stacks.{k}."
+            # edge MLP first Linear: [x_i | x_j] from UV slab, [e] from EDGE slab (x 2^k)
+            add(_hip.SLAB_UV, k, 0, g(p + "edge_fn.0.NN-0.weight"), H, 2 * H, 2 * H, dst_ld=3 * H)
+            add(_hip.SLAB_EDGE, k, H * H, g(p + "edge_fn.0.NN-0.weight"), H, H, H, dst_ld=3 * H,
+                scale=float(2.0 ** k), dst_off=2 * H)
+            add(_hip.SLAB_UV, k, 2 * H * H, g(p + "edge_fn.0.NN-0.bias"), 1, H, H, nrep=W, rep_stride=H)
+            add(_hip.SLAB_EDGE, k, 0, g(p + "edge_fn.0.NN-1.weight"), H, H, H)
+            vb = 2 * H * H
+            add(_hip.SLAB_EDGE, k, vb, g(p + "edge_fn.0.NN-1.bias"), 1, H, H, nrep=W, rep_stride=H)
+            add(_hip.SLAB_EDGE, k, vb + W * H, g(p + "edge_fn.1.weight"), 1, H, H, nrep=W, rep_stride=H)
+            add(_hip.SLAB_EDGE, k, vb + 2 * W * H, g(p + "edge_fn.1.bias"), 1, H, H, nrep=W,
+                rep_stride=H)
+            vb = 3 * H * H
+            add(_hip.SLAB_NODE, k, H * H, g(p + "node_fn.0.NN-0.weight"), H, 2 * H, 2 * H)
+            add(_hip.SLAB_NODE, k, vb, g(p + "node_fn.0.NN-0.bias"), 1, H, H, nrep=W, rep_stride=H)
+            add(_hip.SLAB_NODE, k, 0, g(p + "node_fn.0.NN-1.weight"), H, H, H)
+            add(_hip.SLAB_NODE, k, vb + W * H, g(p + "node_fn.0.NN-1.bias"), 1, H, H, nrep=W,
+                rep_stride=H)
+            add(_hip.SLAB_NODE, k, vb + 2 * W * H, g(p + "node_fn.1.weight"), 1, H, H, nrep=W,
+                rep_stride=H)
+            add(_hip.SLAB_NODE, k, vb + 3 * W * H, g(p + "node_fn.1.bias"), 1, H, H, nrep=W,
+                rep_stride=H)
+        # decoder (slab DECODER: dW2[32][H] | dW1[H][H] | db2[W][32] | db1[W][H] | loss[W][8])
+        d1 = self.dim + 1
+        vb = 32 * H + H * H
+        add(_hip.SLAB_DECODER, 0, 32 * H, g("_decoder.node_fn.NN-0.weight"), H, H, H)
+        add(_hip.SLAB_DECODER, 0, vb + W * 32, g("_decoder.node_fn.NN-0.bias"), 1, H, H, nrep=W,
+            rep_stride=H)
+        add(_hip.SLAB_DECODER, 0, 0, g("_decoder.node_fn.NN-1.weight"), d1, H, H)
+        add(_hip.SLAB_DECODER, 0, vb, g("_decoder.node_fn.NN-1.bias"), 1, d1, 32, nrep=W,
+            rep_stride=32)
+        add(_hip.SLAB_DECODER, 0, vb + W * 32 + W * H, self.loss_out, 1, 5, 8, nrep=W, rep_stride=8)
+        arr = (SgnnReduceDesc * len(descs))(*descs)
+        raw = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
+                               dtype=torch.uint8)
+        self._descs_dev = raw.to(self.arena.device)
+        self._ndesc = len(descs)
+        self._max_elems = max(d.nrows * d.ncols for d in descs)
+        self._descs_key = key
+
+
+def _saves(h=None, yhat=None, rstd=None, agg=None, hd=None) -> SgnnSaves:
+    p = engine._ptr
+    return SgnnSaves(h=p(h), yhat=p(yhat), rstd=p(rstd), agg=p(agg), hd=p(hd))
+
+
+def check_trainable(epd: nn.Module, nparticle_types: int) -> None:
+    if epd.latent_dim != 64:
+        raise NotImplementedError("HIP training path: latent_dim must be 64 in this build")
+    if epd.nmlp_layers != 1:
+        raise NotImplementedError("HIP training path: nmlp_layers must be 1")
+    if nparticle_types > 1:
+        raise NotImplementedError("HIP training path: particle-type embeddings (nparticle_types > 1)")
+
+
+def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: TrainWorkspace) -> None:
+    """predict_accelerations' forward with every activation the backward needs saved."""
+    L = lib()
+    pk = engine.ParamPack.get(epd)
+    ws = tw.f
+    n, T, d = ws.n, ws.T, ws.dim
+    s = stream_ptr(inp.pos_seq.device)
+    pos = inp.pos_seq
+    engine.radius_graph(ws, pos, (T - 1) * d, T * d, inp.ex_ptr, inp.n_ex, radius)
+    sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd)
+    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, 0, 0, 0, 0, inp.vel_mean.data_ptr(),
+                              inp.vel_std.data_ptr(), float(radius), ctypes.byref(pk.enc_node),
+                              ctypes.byref(pk.edge[0]), tw.xs[0].data_ptr(), ws.u.data_ptr(),
+                              ws.v.data_ptr(), ctypes.byref(sv), s), "sgnn_encode_nodes")
+    sv = _saves(yhat=tw.ee_yh, rstd=tw.ee_rstd)
+    check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius),
+                              ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
+                              ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(),
+                              ctypes.byref(sv), s), "sgnn_encode_edges")
+    nl = len(pk.edge)
+    for k in range(nl):
+        sv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k])
+        check(L.sgnn_edge_layer(ws.u.data_ptr(), ws.v.data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
+                                ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
+                                ws.edge_cap, ctypes.byref(pk.edge[k]), ws.agg.data_ptr(),
+                                ws.cin.data_ptr(), ws.cout.data_ptr(), ctypes.byref(sv), s),
+              "sgnn_edge_layer")
+        if k < nl - 1:
+            sv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k])
+            check(L.sgnn_node_layer(tw.xs[k].data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
+                                    ws.cout.data_ptr(), ws.rowptr.data_ptr(), n,
+                                    ctypes.byref(pk.node[k]), ctypes.byref(pk.edge[k + 1]),
+                                    tw.xs[k + 1].data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(),
+                                    ctypes.byref(sv), s), "sgnn_node_layer")
+        else:
+            sv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], hd=tw.hd)
+            check(L.sgnn_node_layer_decode(tw.xs[k].data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
+                                           ws.cout.data_ptr(), ws.rowptr.data_ptr(), n,
+                                           ctypes.byref(pk.node[k]), ctypes.byref(pk.dec),
+                                           pos.data_ptr(), T, d, inp.acc_mean.data_ptr(),
+                                           inp.acc_std.data_ptr(), tw.xs[k + 1].data_ptr(),
+                                           tw.pred.data_ptr(), tw.next_scratch.data_ptr(), 0,
+                                           ctypes.byref(sv), s), "sgnn_node_layer_decode")
+    check(L.sgnn_transpose_csr(ws.rowptr.data_ptr(), ws.send.data_ptr(), n, ws.edge_cap,
+                               tw.tws_ptr(), tw.tptr.data_ptr(), tw.tperm.data_ptr(), s),
+          "sgnn_transpose_csr")
+
+
+def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: TrainWorkspace,
+                   grads: Dict[str, torch.Tensor], dpred: Optional[torch.Tensor] = None,
+                   next_pos: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
+                   next_strain: Optional[torch.Tensor] = None, w_pos: float = 1.0,
+                   w_strain: float = 1.0, inv_count: float = 1.0) -> None:
+    """Gradients of every parameter into `grads` (name -> tensor views).
+    With dpred: dL/dpred is given (autograd path); otherwise the loss of
+    train.py:257-268 is differentiated in-kernel (its sums land in tw.loss_out)."""
+    L = lib()
+    pk = engine.ParamPack.get(epd)
+    tw.descriptors(epd, grads)
+    ws = tw.f
+    n, T, d = ws.n, ws.T, ws.dim
+    s = stream_ptr(inp.pos_seq.device)
+    ns = tw.nslab
+    p = engine._ptr
+    check(L.sgnn_decoder_loss_bwd(tw.pred.data_ptr(), inp.pos_seq.data_ptr(), p(next_pos), p(noise),
+                                  p(next_strain), inp.acc_mean.data_ptr(), inp.acc_std.data_ptr(), n, T,
+                                  d, float(w_pos), float(w_strain), float(inv_count), p(dpred),
+                                  tw.hd.data_ptr(), tw.xs[tw.L].data_ptr(), ctypes.byref(pk.dec),
+                                  tw.g.data_ptr(), tw.slab(_hip.SLAB_DECODER), ns, s),
+          "sgnn_decoder_loss_bwd")
+    for k in range(tw.L - 1, -1, -1):
+        check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, tw.n_yh[k].data_ptr(), tw.n_rstd[k].data_ptr(),
+                                    tw.n_h[k].data_ptr(), tw.n_agg[k].data_ptr(), tw.xs[k].data_ptr(),
+                                    ctypes.byref(pk.node[k]), tw.dagg.data_ptr(), tw.dxp.data_ptr(),
+                                    tw.slab(_hip.SLAB_NODE, k), ns, s), "sgnn_node_layer_bwd")
+        check(L.sgnn_edge_layer_bwd(tw.dagg.data_ptr(), ws.rowptr.data_ptr(), ws.send.data_ptr(),
+                                    ws.recv.data_ptr(), n, tw.e_h[k].data_ptr(), tw.e_yh[k].data_ptr(),
+                                    tw.e_rstd[k].data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
+                                    ctypes.byref(pk.edge[k]), tw.du.data_ptr(), ws.cin.data_ptr(),
+                                    ws.cout.data_ptr(), tw.dh_rows.data_ptr(), tw.de0t.data_ptr(),
+                                    int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), ns, s),
+              "sgnn_edge_layer_bwd")
+        check(L.sgnn_uv_bwd(tw.dxp.data_ptr(), tw.du.data_ptr(), ws.cin.data_ptr(), ws.cout.data_ptr(),
+                            ws.rowptr.data_ptr(), tw.dh_rows.data_ptr(), tw.tptr.data_ptr(),
+                            tw.tperm.data_ptr(), tw.xs[k].data_ptr(), n, ctypes.byref(pk.edge[k]),
+                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), ns, s), "sgnn_uv_bwd")
+    check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d,
+                                  inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius),
+                                  tw.enc_h.data_ptr(), tw.enc_yh.data_ptr(), tw.enc_rstd.data_ptr(),
+                                  ctypes.byref(pk.enc_node), tw.slab(_hip.SLAB_ENC_NODE), ns, s),
+          "sgnn_encode_nodes_bwd")
+    check(L.sgnn_encode_edges_bwd(tw.de0t.data_ptr(), inp.pos_seq.data_ptr() + 4 * (T - 1) * d, T * d,
+                                  d, float(radius), ws.rowptr.data_ptr(), ws.send.data_ptr(),
+                                  ws.recv.data_ptr(), n, tw.ee_yh.data_ptr(), tw.ee_rstd.data_ptr(),
+                                  ctypes.byref(pk.enc_edge), tw.slab(_hip.SLAB_ENC_EDGE), ns, s),
+          "sgnn_encode_edges_bwd")
+    check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._ndesc, tw._max_elems, s),
+          "sgnn_reduce_slabs")
+
+
+class Adam:
+    """torch.optim.Adam(lr) semantics (train.py:199) on a FlatParams buffer, one
+    fused kernel per step; `lr` may be changed between steps (train.py:276-278)."""
+
+    def __init__(self, flat: FlatParams, lr: float, betas=(0.9, 0.999), eps: float = 1e-8):
+        self.flat = flat
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.exp_avg = torch.zeros_like(flat.param)
+        self.exp_avg_sq = torch.zeros_like(flat.param)
+        self.step_count = 0
+
+    def step(self) -> None:
+        self.step_count += 1
+        f = self.flat
+        check(lib().sgnn_adam_step(f.param.data_ptr(), f.grad.data_ptr(), self.exp_avg.data_ptr(),
+                                   self.exp_avg_sq.data_ptr(), f.numel, float(self.lr),
+                                   float(self.betas[0]), float(self.betas[1]), float(self.eps),
+                                   self.step_count, stream_ptr(f.param.device)), "sgnn_adam_step")

@@ -1,0 +1,121 @@
+"""GPU parity of the training step (HIP forward-with-saves + fused backward +
+slab reduction + fused Adam) against the reference's own training step
+(golden train2d_r06: loss, every parameter gradient, Adam-updated weights) and
+against oracle autograd at larger sizes.
+
+Tolerances (fp32, different summation order than CPU autograd):
+  loss:     rel 1e-5
+  grads:    |g - g_ref| <= 2e-4 * max|g_ref| + 1e-6 per tensor
+  params:   |p - p_ref| <= 2e-5 + 1e-5 |p_ref| after one Adam step (lr 1e-3)
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import golden, hparams, product_sim, state_of, stats_of
+
+pytestmark = pytest.mark.gpu
+
+
+def _grad_close(got, ref, name, rel=2e-4):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    scale = np.abs(ref).max()
+    err = np.abs(got - ref).max()
+    assert err <= rel * scale + 1e-6, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+    return err / max(scale, 1e-30)
+
+
+def _golden_inputs(z):
+    t = lambda k: torch.from_numpy(z[k]).cuda()
+    return t("positions"), t("next_position"), t("next_strain"), t("noise"), z["nparticles_per_example"]
+
+
+def test_trainer_step_matches_reference():
+    from sgnn_amd.train import Trainer
+    z = golden("train2d_r06")
+    sim = product_sim(z, prefix="w0/")
+    tr = Trainer(sim, lr_init=float(z["lr"]))
+    pos, nxt, strain, noise, npe = _golden_inputs(z)
+    out = tr.train_step(pos, nxt, strain, npe, noise=noise)
+    torch.cuda.synchronize()
+    loss = float(out["loss"])
+    print(f"loss {loss:.7f} ref {float(z['loss']):.7f}")
+    assert abs(loss - float(z["loss"])) <= 1e-5 * abs(float(z["loss"]))
+    worst = 0.0
+    grads = {k: p.grad for k, p in sim.named_parameters()}
+    # the Trainer stepped Adam already: compare the gradients it used
+    for k in z.files:
+        if k.startswith("g/"):
+            worst = max(worst, _grad_close(grads[k[2:]].cpu().numpy(), z[k], k))
+    print(f"worst relative grad error {worst:.3e}")
+    sd = sim.state_dict()
+    for k in z.files:
+        if k.startswith("w1/") and ("g/" + k[3:]) in z.files:
+            ref = z[k]
+            got = sd[k[3:]].cpu().numpy()
+            # Adam's first step is ~lr*sign(g): near-zero gradients (|g| ~ eps) amplify
+            # fp32 gradient differences, so the bound is 2% of lr absolute
+            np.testing.assert_allclose(got, ref, rtol=1e-5, atol=2e-5, err_msg=k)
+
+
+def test_predict_accelerations_autograd_matches_reference():
+    """The drop-in path: reference-style loss in torch + loss.backward()."""
+    z = golden("train2d_r06")
+    sim = product_sim(z, prefix="w0/")
+    pos, nxt, strain, noise, npe = _golden_inputs(z)
+    pa, ta, ps = sim.predict_accelerations(nxt, noise, pos, npe, torch.zeros(pos.shape[0], dtype=torch.long,
+                                                                               device="cuda"))
+    np.testing.assert_allclose(ta.detach().cpu().numpy(), z["target_acc"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(pa.detach().cpu().numpy(), z["pred_acc"], rtol=1e-4, atol=2e-5)
+    loss = ((((pa - ta) ** 2).sum(-1)) + (ps - strain) ** 2).mean()   # train.py:257-268
+    loss.backward()
+    for k, p in sim.named_parameters():
+        if ("g/" + k) in z.files:
+            _grad_close(p.grad.cpu().numpy(), z["g/" + k], k)
+
+
+def test_backward_is_bitwise_deterministic():
+    from sgnn_amd.train import Trainer
+    z = golden("train2d_r06")
+    pos, nxt, strain, noise, npe = _golden_inputs(z)
+    outs = []
+    for _ in range(2):
+        sim = product_sim(z, prefix="w0/")
+        tr = Trainer(sim, lr_init=1e-3)
+        tr.train_step(pos, nxt, strain, npe, noise=noise)
+        torch.cuda.synchronize()
+        outs.append(tr.flat.grad.cpu().clone())
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("nx,ny,radius,n_ex", [(60, 40, 0.6, 2), (50, 40, 15.0, 1)])
+def test_gradients_against_oracle_autograd(nx, ny, radius, n_ex):
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import synthetic
+    from sgnn_amd.train import Trainer
+    z = golden("train2d_r06")
+    seqs = [synthetic.trajectory(synthetic.lattice_2d(nx, ny, x0=0.25 + 0.05 * k), 12, seed=40 + k)
+            for k in range(n_ex)]
+    seq = np.concatenate(seqs, 0)
+    counts = [s.shape[0] for s in seqs]
+    pos, nxt = torch.from_numpy(seq[:, :11]), torch.from_numpy(seq[:, 11])
+    strain = torch.from_numpy(np.random.default_rng(1).normal(0, 1, seq.shape[0]).astype(np.float32))
+    g = torch.Generator().manual_seed(7)
+    noise = O.random_walk_noise(pos, 0.02, generator=g)
+    state = {k: v.clone().requires_grad_(True) for k, v in state_of(z, "w0/").items()}
+    osim = O.OracleSimulator(state, 2, 5, radius, stats_of(z))
+    osim.p = state
+    pa, ta, ps = osim.predict_accelerations(nxt, noise, pos, counts, torch.zeros(seq.shape[0], dtype=torch.long))
+    ref_loss = O.training_loss(pa, ta, ps, strain)
+    ref_loss.backward()
+    sim = product_sim(z, prefix="w0/")
+    sim._connectivity_radius = radius
+    tr = Trainer(sim, lr_init=1e-3)
+    out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), counts, noise=noise.cuda())
+    torch.cuda.synchronize()
+    assert abs(float(out["loss"]) - ref_loss.item()) <= 2e-5 * abs(ref_loss.item())
+    worst = 0.0
+    for k, p in sim.named_parameters():
+        if state[k].grad is not None:
+            worst = max(worst, _grad_close(p.grad.cpu().numpy(), state[k].grad.numpy(), k, rel=5e-4))
+    print(f"{nx}x{ny} r={radius}: worst relative grad error {worst:.3e}")
