@@ -2,24 +2,30 @@
 """Benchmark: particle-steps/s (+ M edge-messages/s) of the 2D Taylor-impact
 learned simulator on MI355X (BASELINE.json `metric`).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode rollout|train]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode train|rollout]
                   [--workload c2|c1_r15|c1_r06]
 
-One "step" of --mode rollout is one autoregressive LearnedSimulator
-.predict_positions (radius graph + features + encoder + L interaction layers
-+ decoder + Euler + window shift) on inputs already resident in HBM.
-Multi-GPU: rollout is "replicas only" (one independent trajectory per rank,
-no collective on the data path); value = particles x steps summed over ranks
-/ max-over-ranks wall time.  Synthetic lattice data, random-init weights.
+--mode train (default; BASELINE configs[1] "~50k particles, 5 layers,
+hidden=64, fp32, forward+backward"): one step = the reference training step
+(train.py:231-280): random-walk noise, predict_accelerations forward, loss,
+backward, [N>1: RCCL all-reduce of the flat gradient], Adam, LR decay.  Each
+rank owns one whole graph (weak scaling, whole-graph DDP over xGMI).
+--mode rollout: one step = one autoregressive predict_positions (radius
+graph + features + encoder + L layers + decoder + Euler + window shift);
+multi-GPU rollout is replicas only (no collective).
+Inputs are resident in HBM before the timed region.  Synthetic lattice data
+and random-init weights (no dataset/checkpoint offline).
 
-Extra keys: "roofline" (dominant kernel = the fused edge layer, timed live
-with HIP events on the launch stream) and "cpu_baseline" (the oracle — the
-plain-torch CPU restatement of the reference path — on this box's host cores,
-rank 0 at N=1 only, bounded sample).
+Extra keys: "roofline" (dominant kernel, timed live with HIP events on the
+launch stream, traffic from the committed rocprofv3 PMC summary),
+"cpu_baseline" (the oracle = plain-torch CPU restatement of the reference on
+this box's host cores, rank 0 at N=1 only, bounded sample) and "rollout"
+(C2 and C1 forward-rollout rates with their own CPU baselines).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import platform
@@ -41,24 +47,24 @@ WORKLOADS = {
     "c1_r15": (50, 40, 15.0, 64, 5),     # configs[0] shape at the BASELINE radius (cap binds)
     "c1_r06": (50, 40, 0.6, 64, 5),      # configs[0] shape at the reference default radius
 }
-T_SEQ = 11          # config.yaml:20 input_sequence_length
+T_SEQ = 11                # config.yaml:20 input_sequence_length
 MFMA_F32_PEAK = 157.3e12  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
-HBM_PEAK = 8.0e12
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["rollout"], default="rollout")
+    ap.add_argument("--mode", choices=["train", "rollout"], default="train")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
-    ap.add_argument("--cpu-steps", type=int, default=8, help="oracle steps for cpu_baseline (0: skip)")
+    ap.add_argument("--cpu-steps", type=int, default=6, help="oracle steps for cpu_baseline (0: skip)")
+    ap.add_argument("--no-rollout-extras", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
 
 
-def init_dist(args):
+def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -74,64 +80,51 @@ def make_sim(H, L, radius, dim, device, seed):
     st = {k: {kk: torch.tensor(vv) for kk, vv in v.items()} for k, v in stats.items()}
     sim = LearnedSimulator(dim, (T_SEQ - 1) * dim + 1, dim + 1, H, L, 1, H, radius, st, 1, 9,
                            device=device)
-    return sim.to(device), st
+    return sim.to(device)
 
 
-def cpu_baseline(sim, window, radius, L, steps):
-    """The oracle (test infrastructure, CPU restatement of the reference) on a
-    bounded sample: `steps` autoregressive rollout steps of the same workload."""
-    from oracle import sgnn_oracle as O
-    state = {k: v.detach().cpu() for k, v in sim.state_dict().items()}
-    osim = O.OracleSimulator(state, window.shape[2], L, radius, sim._normalization_stats)
-    cur = window.cpu()
-    n = cur.shape[0]
-    types_ = torch.zeros(n, dtype=torch.long)
-    with torch.no_grad():
-        nxt, _ = osim.predict_positions(cur, [n], types_)  # warm-up
-        cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            nxt, _ = osim.predict_positions(cur, [n], types_)
-            cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
-        dt = time.perf_counter() - t0
-    cpu_model = platform.processor() or platform.machine()
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": torch.get_num_threads(),
-            "kind": "port", "cpu_model": cpu_model,
-            "sample": f"{steps} autoregressive oracle rollout steps (torch CPU fp32 restatement + C "
-                      f"cell-list radius search) on the same {n}-particle workload, after 1 warm-up step",
-            "seconds": dt}
+    return platform.processor() or platform.machine()
 
 
-def profiled_traffic(workload, kernel="k_edge_layer"):
+def profiled_traffic(workload, mode, kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/*_summary.json, FETCH_SIZE x2 + WRITE_SIZE), newest matching tag."""
-    import glob
+    (profiles/r*_summary.json: FETCH_SIZE x2 + WRITE_SIZE), newest matching tag."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
         d = json.load(open(path))
-        if d.get("workload") != workload:
+        if d.get("workload") != workload or d.get("mode", "rollout") != mode:
             continue
         for k, v in d["kernels"].items():
-            if k.startswith(kernel) and "hbm_bytes" in v:
+            if k.split("<")[0] == kernel and "hbm_bytes" in v:
                 best = (v["hbm_bytes"], os.path.relpath(path, ROOT))
     return best
 
 
-def main():
-    args = parse()
-    world, rank, local = init_dist(args)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-    nx, ny, radius, H, L = WORKLOADS[args.workload]
-    dim = 2
-    sim, stats = make_sim(H, L, radius, dim, device, args.seed)
+def sync_barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, device):
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ----------------------------------------------------------------------------- rollout
+def rollout_setup(workload, device, seed, rank):
+    nx, ny, radius, H, L = WORKLOADS[workload]
+    sim = make_sim(H, L, radius, 2, device, seed)
     seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny), T_SEQ, seed=1000 + rank)
     n = seq.shape[0]
     window0 = torch.from_numpy(seq)
@@ -139,81 +132,201 @@ def main():
     inp, use_emb = sim._step_inputs(window0.to(device), [n], types_)
     ws = sim._workspace(n, T_SEQ, device)
     win = [inp.pos_seq, torch.empty_like(inp.pos_seq)]
-    pred = torch.empty(n, dim + 1, device=device)
-    next_pos = torch.empty(n, dim, device=device)
-    epd = sim._encode_process_decode
-    emb_w = sim._particle_type_embedding.weight
+    pred = torch.empty(n, 3, device=device)
+    nxt = torch.empty(n, 2, device=device)
 
     def run(k0, nsteps, timers=None):
         for k in range(k0, k0 + nsteps):
             inp.pos_seq = win[k % 2]
-            engine.forward_step(epd, emb_w, use_emb, radius, inp, ws, pred, next_pos,
-                                window_out=win[(k + 1) % 2], timers=timers)
+            engine.forward_step(sim._encode_process_decode, sim._particle_type_embedding.weight, use_emb,
+                                radius, inp, ws, pred, nxt, window_out=win[(k + 1) % 2], timers=timers)
+    return sim, window0, ws, run, n, radius, H, L
 
+
+def cpu_rollout_baseline(sim, window, radius, L, steps):
+    """Oracle (test infrastructure: CPU restatement of the reference) rollout."""
+    from oracle import sgnn_oracle as O
+    state = {k: v.detach().cpu() for k, v in sim.state_dict().items()}
+    osim = O.OracleSimulator(state, window.shape[2], L, radius, sim._normalization_stats)
+    cur, n = window.cpu(), window.shape[0]
+    types_ = torch.zeros(n, dtype=torch.long)
     with torch.no_grad():
-        run(0, args.warmup)
-        torch.cuda.synchronize()
-        # pass 1: wall clock of exactly K steps (no instrumentation)
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
+        nxt, _ = osim.predict_positions(cur, [n], types_)
+        cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
         t0 = time.perf_counter()
-        run(args.warmup, args.steps)
-        torch.cuda.synchronize()
-        if world > 1:
-            torch.distributed.barrier()
+        for _ in range(steps):
+            nxt, _ = osim.predict_positions(cur, [n], types_)
+            cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
         dt = time.perf_counter() - t0
-        # pass 2: same K steps with HIP events around every edge-layer launch
+    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": torch.get_num_threads(),
+            "kind": "port", "cpu_model": cpu_model(), "seconds": dt,
+            "sample": f"{steps} autoregressive oracle rollout steps (torch CPU fp32 restatement of the "
+                      f"reference ops + C cell-list radius search), {n} particles, after 1 warm-up step"}
+
+
+def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps):
+    sim, window0, ws, run, n, radius, H, L = rollout_setup(workload, device, seed, rank)
+    with torch.no_grad():
+        run(0, warmup)
+        sync_barrier(world)
+        t0 = time.perf_counter()
+        run(warmup, steps)
+        sync_barrier(world)
+        dt = time.perf_counter() - t0
         timers = []
-        t2 = time.perf_counter()
-        run(args.warmup + args.steps, args.steps, timers=timers)
+        run(warmup + steps, steps, timers=timers)
         torch.cuda.synchronize()
-        dt_events = time.perf_counter() - t2
-    edge_ms = [a.elapsed_time(b) for a, b in timers]
+    dt = max_over_ranks(dt, world, device)
     E = ws.num_edges()
-    t = torch.tensor([dt], device=device)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
-    value = n * args.steps * world / dt
-    # dominant kernel: fused edge layer; algorithmic work per launch = E edges x
-    # (H x H of the e-block of W1 + H x H of W2) multiply-adds + LayerNorm.
-    edge_avg_s = float(np.mean(edge_ms)) * 1e-3
-    flops_edge = E * (2 * H * H * 2)
-    achieved = flops_edge / edge_avg_s
-    prof = profiled_traffic(args.workload)
-    out = {
-        "metric": "particle-steps/sec (2D Taylor-impact rollout)",
-        "value": value,
+    edge_avg_s = float(np.mean([a.elapsed_time(b) for a, b in timers])) * 1e-3
+    flops = E * 4 * H * H
+    out = {"workload": f"{workload}: {n} particles/GPU, r={radius}, L={L}, H={H}", "particles": n,
+           "edges": E, "value": n * steps * world / dt, "unit": "particle-steps/s",
+           "ms_per_step": dt / steps * 1e3,
+           "M_edge_messages_per_s": E * L * steps * world / dt / 1e6,
+           "edge_kernel_us": edge_avg_s * 1e6, "edge_kernel_mfma_frac": flops / edge_avg_s / MFMA_F32_PEAK}
+    if cpu_steps > 0 and rank == 0 and world == 1:
+        out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps)
+        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+    return out, timers, flops, edge_avg_s, E, n, radius, H, L
+
+
+# ----------------------------------------------------------------------------- train
+def cpu_train_baseline(state, seq, strain, radius, L, steps, stats):
+    """Oracle training step (noise + forward + torch autograd + torch Adam) on the CPU."""
+    from oracle import sgnn_oracle as O
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in state.items()}
+    osim = O.OracleSimulator(params, 2, L, radius, stats)
+    osim.p = params
+    opt = torch.optim.Adam([p for k, p in params.items() if "embedding" not in k], lr=1e-3)
+    pos, nxt = torch.from_numpy(seq[:, :T_SEQ]), torch.from_numpy(seq[:, T_SEQ])
+    n = pos.shape[0]
+    types_ = torch.zeros(n, dtype=torch.long)
+
+    def step():
+        noise = O.random_walk_noise(pos, 0.02)
+        pa, ta, ps = osim.predict_accelerations(nxt, noise, pos, [n], types_)
+        loss = O.training_loss(pa, ta, ps, strain)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": torch.get_num_threads(),
+            "kind": "port", "cpu_model": cpu_model(), "seconds": dt,
+            "sample": f"{steps} oracle training steps (noise + forward + torch autograd backward + Adam, "
+                      f"torch CPU fp32 restatement of the reference ops), {n} particles, after 1 warm-up"}
+
+
+def bench_train(args, world, rank, device):
+    from sgnn_amd.train import Trainer
+    nx, ny, radius, H, L = WORKLOADS[args.workload]
+    sim = make_sim(H, L, radius, 2, device, args.seed)
+    state0 = {k: v.detach().cpu().clone() for k, v in sim.state_dict().items()}
+    seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny), T_SEQ + 1, seed=2000 + rank)
+    n = seq.shape[0]
+    pos = torch.from_numpy(seq[:, :T_SEQ]).to(device)
+    nxt = torch.from_numpy(seq[:, T_SEQ]).to(device)
+    strain_np = np.random.default_rng(rank).normal(0, 1, n).astype(np.float32)
+    strain = torch.from_numpy(strain_np).to(device)
+    tr = Trainer(sim, lr_init=1e-3)
+    for _ in range(args.warmup):
+        tr.train_step(pos, nxt, strain, [n])
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = tr.train_step(pos, nxt, strain, [n])
+    sync_barrier(world)
+    dt = time.perf_counter() - t0
+    timers = {}
+    t2 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_step(pos, nxt, strain, [n], timers=timers)
+    torch.cuda.synchronize()
+    dt_ev = time.perf_counter() - t2
+    dt = max_over_ranks(dt, world, device)
+    tw = tr.workspace(n, T_SEQ, device)
+    E = tw.f.num_edges()
+    loss = float(out["loss"])
+    kstats = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in timers.items()}
+    # dominant kernel by total time: the edge-layer backward (4 MFMA products / edge)
+    dom = "k_edge_bwd"
+    flops_bwd = E * 8 * H * H   # W2^T dy, W1e^T dh, dW2 += dy h^T, dW1e += dh e0^T
+    achieved = flops_bwd / kstats[dom]
+    prof = profiled_traffic(args.workload, "train", dom)
+    res = {
+        "metric": "particle-steps/sec (2D Taylor-impact, training fwd+bwd+Adam)",
+        "value": n * args.steps * world / dt,
         "unit": "particle-steps/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (0.5 mm Taylor-bar lattice + random-walk frames; random-init weights)",
-        "config": {"workload": f"{args.workload}: 2D lattice {nx}x{ny} = {n} particles/GPU, r={radius}, "
-                               f"L={L}, H={H}, T={T_SEQ}, K=20, rollout", "particles": n, "edges": E,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (0.5 mm Taylor-bar lattice + random-walk frames, random-walk training "
+                "noise; random-init weights)",
+        "config": {"workload": f"{args.workload}: 2D lattice {nx}x{ny} = {n} particles per GPU, r={radius}, "
+                               f"L={L}, H={H}, T={T_SEQ}, K=20, training step (noise+fwd+bwd+Adam)",
+                   "particles_per_gpu": n, "edges_per_gpu": E, "global_batch_graphs": world,
                    "layers": L, "hidden": H, "radius": radius,
-                   "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
-        "edge_messages_per_s": E * L * args.steps * world / dt,
+                   "parallelism": f"dp{world} (whole-graph, RCCL all-reduce)" if world > 1 else "single GPU"},
         "M_edge_messages_per_s": E * L * args.steps * world / dt / 1e6,
-        "roofline": {"bound": "mfma", "kernel": "k_edge_layer", "achieved": achieved / 1e12,
+        "final_loss": loss,
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved / 1e12,
                      "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK,
                      "traffic": prof[0] if prof else None,
-                     "traffic_unit": "bytes/launch (rocprofv3 PMC)",
-                     "traffic_source": prof[1] if prof else None, "avg_launch_us": edge_avg_s * 1e6,
-                     "flops_per_launch": flops_edge,
-                     "edge_share_of_step": float(np.sum(edge_ms)) / (dt_events * 1e3)},
+                     "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_source": prof[1] if prof else None,
+                     "avg_launch_us": kstats[dom] * 1e6, "flops_per_launch": flops_bwd,
+                     "share_of_step": float(np.sum([a.elapsed_time(b) for a, b in timers[dom]])) / (dt_ev * 1e3)},
+        "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and args.cpu_steps > 0:
-        out["cpu_baseline"] = cpu_baseline(sim, window0, radius, L, args.cpu_steps)
-        out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+        res["cpu_baseline"] = cpu_train_baseline(state0, seq, torch.from_numpy(strain_np), radius, L,
+                                                 args.cpu_steps, sim._normalization_stats)
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    return res
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist()
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if args.mode == "train":
+        res = bench_train(args, world, rank, device)
+        if not args.no_rollout_extras:
+            res["rollout"] = {}
+            for wl, cs in (("c2", 2), ("c1_r15", 3)):
+                r = bench_rollout(wl, 20, 3, world, rank, device, args.seed,
+                                  cs if args.cpu_steps > 0 else 0)[0]
+                res["rollout"][wl] = r
+    else:
+        r, timers, flops, edge_avg_s, E, n, radius, H, L = bench_rollout(
+            args.workload, args.steps, args.warmup, world, rank, device, args.seed, args.cpu_steps)
+        prof = profiled_traffic(args.workload, "rollout", "k_edge_layer")
+        res = {"metric": "particle-steps/sec (2D Taylor-impact rollout)", "value": r["value"],
+               "unit": "particle-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic (0.5 mm Taylor-bar lattice + random-walk frames; random-init weights)",
+               "config": {"workload": r["workload"] + ", rollout", "particles": n, "edges": E,
+                          "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+               "M_edge_messages_per_s": r["M_edge_messages_per_s"],
+               "roofline": {"bound": "mfma", "kernel": "k_edge_layer", "achieved": flops / edge_avg_s / 1e12,
+                            "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s",
+                            "frac": flops / edge_avg_s / MFMA_F32_PEAK,
+                            "traffic": prof[0] if prof else None,
+                            "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                            "traffic_source": prof[1] if prof else None,
+                            "avg_launch_us": edge_avg_s * 1e6, "flops_per_launch": flops}}
+        if "cpu_baseline" in r:
+            res["cpu_baseline"] = r["cpu_baseline"]
+            res["speedup_vs_cpu"] = r["speedup_vs_cpu"]
     if rank == 0:
-        print(json.dumps(out))
+        print(json.dumps(res))
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -172,8 +172,10 @@ typedef struct sgnn_reduce_desc {
   int32_t nslab, nrep, src_ld, nrows, ncols, dst_ld, accumulate;
   float scale;
 } sgnn_reduce_desc;
-int sgnn_reduce_slabs(const sgnn_reduce_desc* descs_dev, int32_t ndesc, int64_t max_elems,
-                      void* stream);
+/* block_start[d] = sum_{d' < d} ceil(nrows*ncols / 64) (device int32 [ndesc]);
+ * nblocks = the total.  Deterministic (fixed summation order). */
+int sgnn_reduce_slabs(const sgnn_reduce_desc* descs_dev, const int32_t* block_start,
+                      int32_t ndesc, int32_t nblocks, void* stream);
 
 size_t sgnn_transpose_workspace_bytes(int64_t n, int64_t edge_cap);
 int sgnn_transpose_csr(const int32_t* rowptr, const int32_t* send, int64_t n, int64_t edge_cap,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 outputs into profiles/<tag>_summary.json.
 
-  python profiles/summarize.py TAG WORKLOAD KSTATS_DIR FETCH_DIR WRITE_DIR
+  python profiles/summarize.py TAG WORKLOAD KSTATS_DIR FETCH_DIR WRITE_DIR [MODE]
 
 Per kernel: calls, average duration (kernel-trace --stats), and HBM bytes per
 launch from the separate FETCH_SIZE / WRITE_SIZE passes (both reported in KB;
@@ -23,7 +23,8 @@ def short(name):
 
 def main():
     tag, workload, kdir, fdir, wdir = sys.argv[1:6]
-    out = {"tag": tag, "workload": workload, "kernels": {}}
+    mode = sys.argv[6] if len(sys.argv) > 6 else "rollout"
+    out = {"tag": tag, "workload": workload, "mode": mode, "kernels": {}}
     for r in csv.DictReader(open(os.path.join(kdir, "run_kernel_stats.csv"))):
         out["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]),
                                            "avg_us": float(r["AverageNs"]) / 1e3,

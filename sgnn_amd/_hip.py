@@ -72,7 +72,7 @@ SIGNATURES = {
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p, P_SAVES, c_void_p]),
     "sgnn_bwd_slab_floats": (c_int64, [c_int32, c_int32, c_int32]),
-    "sgnn_reduce_slabs": (ctypes.c_int, [c_void_p, c_int32, c_int64, c_void_p]),
+    "sgnn_reduce_slabs": (ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "sgnn_transpose_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64]),
     "sgnn_transpose_csr": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                           c_void_p, c_void_p]),

@@ -866,21 +866,41 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
 }
 
 // ===========================================================================
-// Slab reduction: out[r][c] = scale * sum_g sum_q slab_g[off + q*rep + r*ld + c]
-__global__ __launch_bounds__(256) void k_reduce_slabs(const sgnn_reduce_desc* descs) {
-  const sgnn_reduce_desc d = descs[blockIdx.y];
+// Slab reduction: out[r][c] = scale * sum_g sum_q slab_g[off + q*rep + r*ld + c].
+// Block = 64 consecutive output elements x 4 slab groups (thread q sums slabs
+// g = q, q+4, ...; coalesced 256-B rows per slab), then the 4 partials are
+// added in fixed order through LDS: deterministic.
+__global__ __launch_bounds__(256) void k_reduce_slabs(const sgnn_reduce_desc* descs,
+                                                      const int32_t* block_start, int ndesc) {
+  __shared__ float part[4][64];
+  // descriptor of this block (block_start is an exclusive prefix of blocks per desc)
+  int lo = 0, hi = ndesc - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (block_start[mid] <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const sgnn_reduce_desc d = descs[lo];
   const int64_t total = (int64_t)d.nrows * d.ncols;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t idx = (int64_t)(blockIdx.x - block_start[lo]) * 64 + (threadIdx.x & 63);
+  const int q = threadIdx.x >> 6;
+  float s = 0.0f;
+  int64_t src_off = 0;
+  if (idx < total) {
     const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
-    float s = 0.0f;
-    for (int g = 0; g < d.nslab; ++g) {
-      const float* p = d.src + (int64_t)g * d.slab_stride + d.offset + (int64_t)r * d.src_ld + cc;
-      for (int q = 0; q < d.nrep; ++q) s += p[(int64_t)q * d.rep_stride];
+    src_off = d.offset + (int64_t)r * d.src_ld + cc;
+    for (int g = q; g < d.nslab; g += 4) {
+      const float* p = d.src + (int64_t)g * d.slab_stride + src_off;
+      for (int k = 0; k < d.nrep; ++k) s += p[(int64_t)k * d.rep_stride];
     }
-    s *= d.scale;
+  }
+  part[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && idx < total) {
+    const float t = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) +
+                    part[3][threadIdx.x];
+    const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
     float* o = d.dst + (int64_t)r * d.dst_ld + cc;
-    *o = d.accumulate ? *o + s : s;
+    *o = d.accumulate ? *o + t * d.scale : t * d.scale;
   }
 }
 
@@ -1106,14 +1126,13 @@ extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_
   return check_launch("encode_edges_bwd");
 }
 
-extern "C" int sgnn_reduce_slabs(const sgnn_reduce_desc* descs_dev, int32_t ndesc,
-                                 int64_t max_elems, void* stream) {
+extern "C" int sgnn_reduce_slabs(const sgnn_reduce_desc* descs_dev, const int32_t* block_start,
+                                 int32_t ndesc, int32_t nblocks, void* stream) {
   using namespace sgnn;
-  if (!descs_dev || ndesc < 1 || ndesc > 65535 || max_elems < 1)
+  if (!descs_dev || !block_start || ndesc < 1 || nblocks < 1)
     return set_error(SGNN_ERR_INVALID, "reduce_slabs: bad arguments");
-  const unsigned gx = (unsigned)std::min<int64_t>((max_elems + 255) / 256, 64);
-  hipLaunchKernelGGL(k_reduce_slabs, dim3(gx, (unsigned)ndesc), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), descs_dev);
+  hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)nblocks), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), descs_dev, block_start, ndesc);
   return check_launch("reduce_slabs");
 }
 

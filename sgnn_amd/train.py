@@ -94,7 +94,8 @@ class Trainer:
 
     def train_step(self, position: torch.Tensor, next_position: torch.Tensor,
                    next_strain: torch.Tensor, nparticles_per_example, particle_types=None,
-                   noise: Optional[torch.Tensor] = None, n_global: Optional[int] = None) -> dict:
+                   noise: Optional[torch.Tensor] = None, n_global: Optional[int] = None,
+                   timers: Optional[dict] = None) -> dict:
         """One optimisation step on this rank's graphs; returns device-side loss
         terms (no host sync).  `noise` defaults to fresh random-walk noise."""
         pos = position.to(torch.float32).contiguous()
@@ -111,8 +112,8 @@ class Trainer:
                 n_global = self.dp.global_count(n, pos.device)
                 self._count_cache[n] = n_global
         radius = self.sim._connectivity_radius
-        training.train_forward(self.epd, radius, inp, tw)
-        training.train_backward(self.epd, radius, inp, tw, self.grads,
+        training.train_forward(self.epd, radius, inp, tw, timers=timers)
+        training.train_backward(self.epd, radius, inp, tw, self.grads, timers=timers,
                                 next_pos=next_position.to(torch.float32).contiguous(), noise=noise,
                                 next_strain=next_strain.to(torch.float32).contiguous(),
                                 w_pos=self.w_pos, w_strain=self.w_strain, inv_count=1.0 / n_global)

@@ -188,7 +188,12 @@ class TrainWorkspace:
                                dtype=torch.uint8)
         self._descs_dev = raw.to(self.arena.device)
         self._ndesc = len(descs)
-        self._max_elems = max(d.nrows * d.ncols for d in descs)
+        starts, nb = [], 0
+        for d in descs:
+            starts.append(nb)
+            nb += (d.nrows * d.ncols + 63) // 64
+        self._block_start = torch.tensor(starts, dtype=torch.int32).to(self.arena.device)
+        self._nblocks = nb
         self._descs_key = key
 
 
@@ -206,7 +211,26 @@ def check_trainable(epd: nn.Module, nparticle_types: int) -> None:
         raise NotImplementedError("HIP training path: particle-type embeddings (nparticle_types > 1)")
 
 
-def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: TrainWorkspace) -> None:
+class _Timer:
+    """Optional HIP-event timing of named launches on the current stream."""
+
+    def __init__(self, timers: Optional[dict], name: str):
+        self.timers, self.name = timers, name
+
+    def __enter__(self):
+        if self.timers is not None:
+            self.ev0 = torch.cuda.Event(enable_timing=True)
+            self.ev0.record()
+
+    def __exit__(self, *exc):
+        if self.timers is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self.timers.setdefault(self.name, []).append((self.ev0, ev1))
+
+
+def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: TrainWorkspace,
+                  timers: Optional[dict] = None) -> None:
     """predict_accelerations' forward with every activation the backward needs saved."""
     L = lib()
     pk = engine.ParamPack.get(epd)
@@ -228,7 +252,8 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
     nl = len(pk.edge)
     for k in range(nl):
         sv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k])
-        check(L.sgnn_edge_layer(ws.u.data_ptr(), ws.v.data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
+        with _Timer(timers, "k_edge_layer(train)"):
+          check(L.sgnn_edge_layer(ws.u.data_ptr(), ws.v.data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
                                 ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
                                 ws.edge_cap, ctypes.byref(pk.edge[k]), ws.agg.data_ptr(),
                                 ws.cin.data_ptr(), ws.cout.data_ptr(), ctypes.byref(sv), s),
@@ -258,7 +283,7 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                    grads: Dict[str, torch.Tensor], dpred: Optional[torch.Tensor] = None,
                    next_pos: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
                    next_strain: Optional[torch.Tensor] = None, w_pos: float = 1.0,
-                   w_strain: float = 1.0, inv_count: float = 1.0) -> None:
+                   w_strain: float = 1.0, inv_count: float = 1.0, timers: Optional[dict] = None) -> None:
     """Gradients of every parameter into `grads` (name -> tensor views).
     With dpred: dL/dpred is given (autograd path); otherwise the loss of
     train.py:257-268 is differentiated in-kernel (its sums land in tw.loss_out)."""
@@ -281,7 +306,8 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                     tw.n_h[k].data_ptr(), tw.n_agg[k].data_ptr(), tw.xs[k].data_ptr(),
                                     ctypes.byref(pk.node[k]), tw.dagg.data_ptr(), tw.dxp.data_ptr(),
                                     tw.slab(_hip.SLAB_NODE, k), ns, s), "sgnn_node_layer_bwd")
-        check(L.sgnn_edge_layer_bwd(tw.dagg.data_ptr(), ws.rowptr.data_ptr(), ws.send.data_ptr(),
+        with _Timer(timers, "k_edge_bwd"):
+          check(L.sgnn_edge_layer_bwd(tw.dagg.data_ptr(), ws.rowptr.data_ptr(), ws.send.data_ptr(),
                                     ws.recv.data_ptr(), n, tw.e_h[k].data_ptr(), tw.e_yh[k].data_ptr(),
                                     tw.e_rstd[k].data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
                                     ctypes.byref(pk.edge[k]), tw.du.data_ptr(), ws.cin.data_ptr(),
@@ -302,8 +328,8 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                   ws.recv.data_ptr(), n, tw.ee_yh.data_ptr(), tw.ee_rstd.data_ptr(),
                                   ctypes.byref(pk.enc_edge), tw.slab(_hip.SLAB_ENC_EDGE), ns, s),
           "sgnn_encode_edges_bwd")
-    check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._ndesc, tw._max_elems, s),
-          "sgnn_reduce_slabs")
+    check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
+                              tw._nblocks, s), "sgnn_reduce_slabs")
 
 
 class Adam:

@@ -1,0 +1,94 @@
+"""Whole-graph data parallelism on CPU (gloo, world_size 2): the Trainer's DP
+bookkeeping (sgnn_amd.train.DataParallel: N_global count, 1/N_global loss
+scaling, SUM all-reduce of one flat gradient buffer) must reproduce the
+single-process gradient of the concatenated batch (train.py:268 takes the
+mean over all particles of the batch).  Gradients come from the oracle here
+(no GPU); on MI355X the same DataParallel object all-reduces over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.helpers import golden, state_of, stats_of
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _graphs():
+    from sgnn_amd import synthetic
+    from oracle import sgnn_oracle as O
+    out = []
+    for k, (nx, ny) in enumerate([(10, 8), (12, 7)]):   # unequal graph sizes
+        seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny), 12, seed=50 + k)
+        pos, nxt = torch.from_numpy(seq[:, :11]), torch.from_numpy(seq[:, 11])
+        strain = torch.from_numpy(np.random.default_rng(k).normal(0, 1, seq.shape[0]).astype(np.float32))
+        noise = O.random_walk_noise(pos, 0.02, generator=torch.Generator().manual_seed(9 + k))
+        out.append((pos, nxt, strain, noise))
+    return out
+
+
+def _oracle_grads(graphs, inv_count):
+    """sum over graphs of d/dtheta [ inv_count * sum_particles loss_i ]"""
+    from oracle import sgnn_oracle as O
+    z = golden("train2d_r06")
+    state = {k: v.clone().requires_grad_(True) for k, v in state_of(z, "w0/").items()}
+    sim = O.OracleSimulator(state, 2, 5, 0.6, stats_of(z))
+    sim.p = state
+    total = 0.0
+    for pos, nxt, strain, noise in graphs:
+        n = pos.shape[0]
+        pa, ta, ps = sim.predict_accelerations(nxt, noise, pos, [n], torch.zeros(n, dtype=torch.long))
+        loss_sum = O.training_loss(pa, ta, ps, strain) * n       # sum over this graph's particles
+        (loss_sum * inv_count).backward()
+        total += float(loss_sum)
+    names = [k for k in state if state[k].grad is not None]
+    flat = torch.cat([state[k].grad.reshape(-1) for k in names])
+    return flat, total * inv_count
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sgnn_amd.train import DataParallel
+    dp = DataParallel()
+    mine = [_graphs()[rank]]
+    n_local = mine[0][0].shape[0]
+    n_global = dp.global_count(n_local, "cpu")
+    flat, loss = _oracle_grads(mine, 1.0 / n_global)
+    loss_t = torch.tensor([loss])
+    dp.allreduce_(flat, loss_t)
+    q.put((rank, n_global, flat.numpy(), float(loss_t)))
+    dist.destroy_process_group()
+
+
+def test_whole_graph_dp_matches_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    graphs = _graphs()
+    n_total = sum(g[0].shape[0] for g in graphs)
+    ref_flat, ref_loss = _oracle_grads(graphs, 1.0 / n_total)
+    for rank, n_global, flat, loss in res:
+        assert n_global == n_total
+        np.testing.assert_allclose(flat, ref_flat.numpy(), rtol=1e-4, atol=1e-7)
+        assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss)
+    # every rank ends with the identical gradient -> identical Adam update
+    np.testing.assert_array_equal(res[0][2], res[1][2])
