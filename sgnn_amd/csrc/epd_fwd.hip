@@ -56,23 +56,40 @@ SGNN_DEV void store_uv(const float* Wi, const float* Wj, const float* b1e, int l
   if (valid) store_row_clayout<TH>(v_row, acc);
 }
 
+template <int TH>
+SGNN_DEV void store_uv2(const float* Wi, int ldi, const float* Wj, int ldj, const float* b1e,
+                        const f32x16 (&x)[TH], float* u_row, float* v_row, bool valid) {
+  f32x16 acc[TH];
+  acc_bias<TH>(acc, b1e);
+  mfma_from_acc<TH, TH>(acc, Wi, ldi, 0, x);
+  if (valid) store_row_clayout<TH>(u_row, acc);
+  acc_bias<TH>(acc, nullptr);
+  mfma_from_acc<TH, TH>(acc, Wj, ldj, 0, x);
+  if (valid) store_row_clayout<TH>(v_row, acc);
+}
+
 template <int TH, int TKF, bool TRAIN>
 __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
-  constexpr int H = 32 * TH, ldh = H + 4, ldf = 32 * TKF + 4;
+  constexpr bool GW = TH > 2;  // H = 128: weights read from L2 (460 KB/layer > LDS)
+  constexpr int H = 32 * TH, ldf = 32 * TKF + 4;
+  constexpr int ldh = GW ? H : H + 4, ldwe = GW ? 3 * H : H + 4;
   extern __shared__ float lds[];
   float* W1 = lds;
-  float* W2 = W1 + H * ldf;
-  float* Wi = W2 + H * ldh;
-  float* Wj = Wi + H * ldh;
-  float* b1 = Wj + H * ldh;
+  float* sW = W1 + H * ldf;
+  const float* W2 = GW ? a.w2 : sW;
+  const float* Wi = GW ? a.we : sW + H * ldh;
+  const float* Wj = GW ? a.we + H : sW + 2 * H * ldh;
+  float* b1 = GW ? sW : sW + 3 * H * ldh;
   float* b2 = b1 + H;
   float* g = b2 + H;
   float* bb = g + H;
   float* b1e = bb + H;
   stage_matrix(W1, ldf, a.w1, a.feat, H, a.feat, H, 32 * TKF);
-  stage_matrix(W2, ldh, a.w2, H, H, H, H, H);
-  stage_matrix(Wi, ldh, a.we, 3 * H, H, H, H, H);
-  stage_matrix(Wj, ldh, a.we + H, 3 * H, H, H, H, H);
+  if (!GW) {
+    stage_matrix(sW, ldh, a.w2, H, H, H, H, H);
+    stage_matrix(sW + H * ldh, ldh, a.we, 3 * H, H, H, H, H);
+    stage_matrix(sW + 2 * H * ldh, ldh, a.we + H, 3 * H, H, H, H, H);
+  }
   stage_vec(b1, a.b1, H, H);
   stage_vec(b2, a.b2, H, H);
   stage_vec(g, a.g, H, H);
@@ -126,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
       acc_layernorm<TH>(y, g, bb);
     }
     if (valid) store_row_clayout<TH>(a.x0 + i * H, y);
-    store_uv<TH>(Wi, Wj, b1e, ldh, y, a.u + i * H, a.v + i * H, valid);
+    store_uv<TH>(Wi, Wj, b1e, ldwe, y, a.u + i * H, a.v + i * H, valid);
   }
 }
 
@@ -144,16 +161,18 @@ struct EncEdgeArgs {
 
 template <int TH, bool TRAIN>
 __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
-  constexpr int H = 32 * TH, ldh = H + 4, ld1 = 5;
+  constexpr bool GW = TH > 2;
+  constexpr int H = 32 * TH, ldh = GW ? H : H + 4, ld1 = 5;
   extern __shared__ float lds[];
   float* W1 = lds;
-  float* W2 = W1 + H * ld1;
-  float* b1 = W2 + H * ldh;
+  float* sW = W1 + H * ld1;
+  const float* W2 = GW ? a.w2 : sW;
+  float* b1 = GW ? sW : sW + H * ldh;
   float* b2 = b1 + H;
   float* g = b2 + H;
   float* bb = g + H;
   stage_matrix(W1, ld1, a.w1, a.dim + 1, H, a.dim + 1, H, 4);
-  stage_matrix(W2, ldh, a.w2, H, H, H, H, H);
+  if (!GW) stage_matrix(sW, ldh, a.w2, H, H, H, H, H);
   stage_vec(b1, a.b1, H, H);
   stage_vec(b2, a.b2, H, H);
   stage_vec(g, a.g, H, H);
@@ -218,16 +237,21 @@ struct EdgeLayerArgs {
 
 template <int TH, bool TRAIN>
 __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
-  constexpr int H = 32 * TH, ldh = H + 4;
+  constexpr bool GW = TH > 2;
+  constexpr int H = 32 * TH, ldh = H + 4;            // ldh: LDS image leading dim
+  constexpr int lde = GW ? 3 * H : ldh, ldw2 = GW ? H : ldh;
   extern __shared__ float lds[];
-  float* We = lds;
-  float* W2 = We + H * ldh;
-  float* b2 = W2 + H * ldh;
+  float* sW = lds;
+  const float* We = GW ? a.we : sW;
+  const float* W2 = GW ? a.w2 : sW + H * ldh;
+  float* b2 = GW ? sW : sW + 2 * H * ldh;
   float* g = b2 + H;
   float* bb = g + H;
   float* mbuf = bb + H;  // per wave [32][ldh]
-  stage_matrix(We, ldh, a.we, 3 * H, H, H, H, H);
-  stage_matrix(W2, ldh, a.w2, H, H, H, H, H);
+  if (!GW) {
+    stage_matrix(sW, ldh, a.we, 3 * H, H, H, H, H);
+    stage_matrix(sW + H * ldh, ldh, a.w2, H, H, H, H, H);
+  }
   stage_vec(b2, a.b2, H, H);
   stage_vec(g, a.g, H, H);
   stage_vec(bb, a.bb, H, H);
@@ -254,12 +278,12 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     const float* src = a.e0t + tile * (32 * H) + l * 4;
 #pragma unroll
     for (int q = 0; q < TH * 4; ++q) xg[q] = ld4(src + q * 256);
-    mfma_from_groups<TH, TH>(hacc, We, ldh, 0, xg, a.e_scale);
+    mfma_from_groups<TH, TH>(hacc, We, lde, 0, xg, a.e_scale);
     acc_relu<TH>(hacc);
     if (TRAIN) store_tiled<TH>(a.sv.h + tile * (32 * H), hacc);
     f32x16 y[TH];
     acc_bias<TH>(y, b2);
-    mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
+    mfma_from_acc<TH, TH>(y, W2, ldw2, 0, hacc);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -350,27 +374,38 @@ SGNN_DEV void load_agg(f32x16 (&a)[TH], const NodeLayerArgs& p, int64_t i) {
 
 template <int TH, int MODE, bool TRAIN>
 __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
-  constexpr int H = 32 * TH, ldh = H + 4, ld2 = 2 * H + 4;
+  constexpr bool GW = TH > 2;
+  constexpr int H = 32 * TH, ldh = H + 4;
+  constexpr int ld2 = GW ? 2 * H : 2 * H + 4, ldw2 = GW ? H : ldh;
+  constexpr int lda = GW ? (MODE == 0 ? 3 * H : H) : ldh;
   extern __shared__ float lds[];
-  float* W1 = lds;
-  float* W2 = W1 + H * ld2;
-  float* Wa = W2 + H * ldh;   // mode 0: W1e_i   mode 1: decoder W1
-  float* Wb = Wa + H * ldh;   // mode 0: W1e_j   mode 1: decoder W2 (32 rows)
-  float* b1 = Wb + H * ldh;
+  float* sW = lds;
+  // LDS: [W1 | W2 | Wa | Wb] for H = 64; only the padded decoder W2 for H = 128
+  const float* W1 = GW ? a.w1 : sW;
+  const float* W2 = GW ? a.w2 : sW + H * ld2;
+  const float* Wa = GW ? (MODE == 0 ? a.we : a.wd1) : sW + H * ld2 + H * ldh;
+  float* sWb = GW ? sW : sW + H * ld2 + 2 * H * ldh;  // mode 0: W1e_j  mode 1: decoder W2 (32 rows)
+  const float* Wb = (GW && MODE == 0) ? a.we + H : sWb;
+  const int ldb = (GW && MODE == 0) ? 3 * H : ldh;
+  float* b1 = (GW && MODE == 0) ? sW : sWb + H * ldh;
   float* b2 = b1 + H;
   float* g = b2 + H;
   float* bb = g + H;
   float* ba = bb + H;  // mode 0: b1e   mode 1: decoder b1
   float* bd2 = ba + H;  // mode 1: decoder b2 (32)
-  stage_matrix(W1, ld2, a.w1, 2 * H, H, 2 * H, H, 2 * H);
-  stage_matrix(W2, ldh, a.w2, H, H, H, H, H);
+  if (!GW) {
+    stage_matrix(sW, ld2, a.w1, 2 * H, H, 2 * H, H, 2 * H);
+    stage_matrix(sW + H * ld2, ldh, a.w2, H, H, H, H, H);
+  }
   if (MODE == 0) {
-    stage_matrix(Wa, ldh, a.we, 3 * H, H, H, H, H);
-    stage_matrix(Wb, ldh, a.we + H, 3 * H, H, H, H, H);
+    if (!GW) {
+      stage_matrix(sW + H * ld2 + H * ldh, ldh, a.we, 3 * H, H, H, H, H);
+      stage_matrix(sWb, ldh, a.we + H, 3 * H, H, H, H, H);
+    }
     stage_vec(ba, a.be, H, H);
   } else {
-    stage_matrix(Wa, ldh, a.wd1, H, H, H, H, H);
-    stage_matrix(Wb, ldh, a.wd2, H, a.dim + 1, H, 32, H);
+    if (!GW) stage_matrix(sW + H * ld2 + H * ldh, ldh, a.wd1, H, H, H, H, H);
+    stage_matrix(sWb, ldh, a.wd2, H, a.dim + 1, H, 32, H);
     stage_vec(ba, a.bd1, H, H);
     stage_vec(bd2, a.bd2, a.dim + 1, 32);
   }
@@ -398,7 +433,7 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
     if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
     f32x16 y[TH];
     acc_bias<TH>(y, b2);
-    mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
+    mfma_from_acc<TH, TH>(y, W2, ldw2, 0, hacc);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -416,11 +451,11 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
       for (int r = 0; r < 16; ++r) x[t][r] = y[t][r] + x[t][r];  // :176 residual
     if (valid && a.x_out) store_row_clayout<TH>(a.x_out + i * H, x);
     if (MODE == 0) {
-      store_uv<TH>(Wa, Wb, ba, ldh, x, a.u + i * H, a.v + i * H, valid);
+      store_uv2<TH>(Wa, lda, Wb, ldb, ba, x, a.u + i * H, a.v + i * H, valid);
     } else {
       f32x16 hd[TH];
       acc_bias<TH>(hd, ba);
-      mfma_from_acc<TH, TH>(hd, Wa, ldh, 0, x);
+      mfma_from_acc<TH, TH>(hd, Wa, lda, 0, x);
       acc_relu<TH>(hd);
       if (TRAIN && valid) store_row_clayout<TH>(a.sv.hd + i * H, hd);
       f32x16 o[1];
@@ -503,7 +538,7 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
   if (!st) st = check_mlp(edge0, 3 * H, H, H, true, "encode_nodes: edge0 MLP shape");
   if (st) return st;
   if (use_emb && (!types || !emb_w)) return set_error(SGNN_ERR_INVALID, "encode_nodes: embedding");
-  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: hidden must be 64 in this build");
+  if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: hidden must be 64 or 128");
   EncNodeArgs a{pos_seq, n, T, dim, types, emb_w, emb_dim, use_emb, vel_mean, vel_std, radius,
                 feat, enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, edge0->w1,
                 edge0->b1, x0, u, v, {}};
@@ -514,13 +549,22 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
   }
   const unsigned grid = persistent_grid(n, 32 * kWaves, 2);
   const int tkf = (feat + 31) / 32;
-  const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + 3 * H * (H + 4) + 5 * H);
+  const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + (H == 64 ? 3 * H * (H + 4) : 0) + 5 * H);
   if (lds > kLdsMax) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: too many features");
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (tkf) {
-    case 1: launch2(k_encode_nodes<2, 1, false>, k_encode_nodes<2, 1, true>, train, grid, lds, s, a); break;
-    case 2: launch2(k_encode_nodes<2, 2, false>, k_encode_nodes<2, 2, true>, train, grid, lds, s, a); break;
-    case 3: launch2(k_encode_nodes<2, 3, false>, k_encode_nodes<2, 3, true>, train, grid, lds, s, a); break;
+    case 1:
+      if (H == 64) launch2(k_encode_nodes<2, 1, false>, k_encode_nodes<2, 1, true>, train, grid, lds, s, a);
+      else launch2(k_encode_nodes<4, 1, false>, k_encode_nodes<4, 1, true>, train, grid, lds, s, a);
+      break;
+    case 2:
+      if (H == 64) launch2(k_encode_nodes<2, 2, false>, k_encode_nodes<2, 2, true>, train, grid, lds, s, a);
+      else launch2(k_encode_nodes<4, 2, false>, k_encode_nodes<4, 2, true>, train, grid, lds, s, a);
+      break;
+    case 3:
+      if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: > 64 features at hidden 128");
+      launch2(k_encode_nodes<2, 3, false>, k_encode_nodes<2, 3, true>, train, grid, lds, s, a);
+      break;
     default: return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: > 96 node features");
   }
   return check_launch("encode_nodes");
@@ -538,7 +582,7 @@ extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t d
   const int H = enc->hidden;
   int st = check_mlp(enc, dim + 1, H, H, true, "encode_edges: encoder MLP shape");
   if (st) return st;
-  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_edges: hidden must be 64 in this build");
+  if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "encode_edges: hidden must be 64 or 128");
   EncEdgeArgs a{pos, pos_stride, dim, radius, rowptr, send, recv, n,
                 enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, e0t, {}};
   const bool train = want_saves(saves);
@@ -547,9 +591,10 @@ extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t d
     a.sv = *saves;
   }
   const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 4);
-  const size_t lds = sizeof(float) * (size_t)(H * 5 + H * (H + 4) + 4 * H);
+  const size_t lds = sizeof(float) * (size_t)(H * 5 + (H == 64 ? H * (H + 4) : 0) + 4 * H);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  launch2(k_encode_edges<2, false>, k_encode_edges<2, true>, train, grid, lds, s, a);
+  if (H == 64) launch2(k_encode_edges<2, false>, k_encode_edges<2, true>, train, grid, lds, s, a);
+  else launch2(k_encode_edges<4, false>, k_encode_edges<4, true>, train, grid, lds, s, a);
   return check_launch("encode_edges");
 }
 
@@ -564,7 +609,7 @@ extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t,
   const int H = edge_fn->hidden;
   int st = check_mlp(edge_fn, 3 * H, H, H, true, "edge_layer: edge MLP shape");
   if (st) return st;
-  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer: hidden must be 64 in this build");
+  if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer: hidden must be 64 or 128");
   EdgeLayerArgs a{u, v, e0t, e_scale, rowptr, send, recv, n, edge_fn->w1 + 2 * H, edge_fn->w2,
                   edge_fn->b2, edge_fn->ln_g, edge_fn->ln_b, agg, cin, cout, {}};
   const bool train = want_saves(saves);
@@ -572,10 +617,11 @@ extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t,
     if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "edge_layer: saves");
     a.sv = *saves;
   }
-  const size_t lds = sizeof(float) * (size_t)(2 * H * (H + 4) + 3 * H + kWaves * 32 * (H + 4));
+  const size_t lds = sizeof(float) * (size_t)((H == 64 ? 2 * H * (H + 4) : 0) + 3 * H + kWaves * 32 * (H + 4));
   const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 2);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  launch2(k_edge_layer<2, false>, k_edge_layer<2, true>, train, grid, lds, s, a);
+  if (H == 64) launch2(k_edge_layer<2, false>, k_edge_layer<2, true>, train, grid, lds, s, a);
+  else launch2(k_edge_layer<4, false>, k_edge_layer<4, true>, train, grid, lds, s, a);
   return check_launch("edge_layer");
 }
 
@@ -585,7 +631,7 @@ static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode
   const int H = node_fn ? node_fn->hidden : 0;
   int st = check_mlp(node_fn, 2 * H, H, H, true, "node_layer: node MLP shape");
   if (st) return st;
-  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "node_layer: hidden must be 64 in this build");
+  if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "node_layer: hidden must be 64 or 128");
   a.w1 = node_fn->w1; a.b1 = node_fn->b1; a.w2 = node_fn->w2; a.b2 = node_fn->b2;
   a.g = node_fn->ln_g; a.bb = node_fn->ln_b;
   const bool train = want_saves(saves);
@@ -594,11 +640,17 @@ static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode
       return set_error(SGNN_ERR_INVALID, "node_layer: saves");
     a.sv = *saves;
   }
-  const size_t lds = sizeof(float) * (size_t)(H * (2 * H + 4) + 3 * H * (H + 4) + 5 * H + 32);
-  const unsigned grid = persistent_grid(a.n, 32 * kWaves, 1);
+  const size_t lds = sizeof(float) * (size_t)(H == 64 ? H * (2 * H + 4) + 3 * H * (H + 4) + 5 * H + 32
+                                                      : H * (H + 4) + 5 * H + 32);
+  const unsigned grid = persistent_grid(a.n, 32 * kWaves, H == 64 ? 1 : 2);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (mode == 0) launch2(k_node_layer<2, 0, false>, k_node_layer<2, 0, true>, train, grid, lds, s, a);
-  else launch2(k_node_layer<2, 1, false>, k_node_layer<2, 1, true>, train, grid, lds, s, a);
+  if (H == 64) {
+    if (mode == 0) launch2(k_node_layer<2, 0, false>, k_node_layer<2, 0, true>, train, grid, lds, s, a);
+    else launch2(k_node_layer<2, 1, false>, k_node_layer<2, 1, true>, train, grid, lds, s, a);
+  } else {
+    if (mode == 0) launch2(k_node_layer<4, 0, false>, k_node_layer<4, 0, true>, train, grid, lds, s, a);
+    else launch2(k_node_layer<4, 1, false>, k_node_layer<4, 1, true>, train, grid, lds, s, a);
+  }
   return check_launch("node_layer");
 }
 

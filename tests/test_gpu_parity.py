@@ -38,7 +38,7 @@ def test_radius_graph_bit_exact(case):
     np.testing.assert_array_equal(ei, z["edge_index"])
 
 
-@pytest.mark.parametrize("case", FWD_H64)
+@pytest.mark.parametrize("case", FWD_H64 + ["tiny3d_h128"])
 def test_predict_positions_matches_reference(case):
     z = golden(case)
     hp = hparams(z)
@@ -112,3 +112,22 @@ def test_radius_graph_random_vs_bruteforce():
         e = ws.num_edges()
         got = torch.stack([ws.send[:e], ws.recv[:e]]).cpu().to(torch.int64)
         np.testing.assert_array_equal(got.numpy(), ref.numpy(), err_msg=f"trial {trial}")
+
+
+def test_3d_h128_against_oracle():
+    """Config-4 shapes (3D, H=128) at a size the oracle finishes quickly."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import synthetic
+    from tests.helpers import state_of, stats_of
+    z = golden("tiny3d_h128")
+    hp = hparams(z)
+    seq = synthetic.trajectory(synthetic.lattice_3d(16, 10, 8), hp["T"], seed=31)
+    sim = product_sim(z)
+    osim = O.OracleSimulator(state_of(z), 3, hp["L"], hp["R"], stats_of(z))
+    pos = torch.from_numpy(seq)
+    types_ = torch.zeros(seq.shape[0], dtype=torch.long)
+    ref_next, ref_strain = osim.predict_positions(pos, [seq.shape[0]], types_)
+    nxt, strain = sim.predict_positions(pos.cuda(), [seq.shape[0]], types_.cuda())
+    _close(strain.cpu().numpy(), ref_strain.numpy(), what="3d h128 strain")
+    scale = float(np.max(z["acc_std"]))
+    _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * scale, rtol=1e-6, what="3d h128 next_pos")
