@@ -172,7 +172,7 @@ typedef struct sgnn_reduce_desc {
   int32_t nslab, nrep, src_ld, nrows, ncols, dst_ld, accumulate;
   float scale;
 } sgnn_reduce_desc;
-/* block_start[d] = sum_{d' < d} ceil(nrows*ncols / 64) (device int32 [ndesc]);
+/* block_start[d] = sum_{d' < d} ceil(nrows*ncols / 32) (device int32 [ndesc]);
  * nblocks = the total.  Deterministic (fixed summation order). */
 int sgnn_reduce_slabs(const sgnn_reduce_desc* descs_dev, const int32_t* block_start,
                       int32_t ndesc, int32_t nblocks, void* stream);

@@ -867,13 +867,13 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
 
 // ===========================================================================
 // Slab reduction: out[r][c] = scale * sum_g sum_q slab_g[off + q*rep + r*ld + c].
-// Block = 64 consecutive output elements x 4 slab groups (thread q sums slabs
-// g = q, q+4, ...; coalesced 256-B rows per slab), then the 4 partials are
-// added in fixed order through LDS: deterministic.
+// Block = 32 consecutive output elements x 8 slab groups; thread q sums slabs
+// g = q, q+8, ... with 4 independent accumulators (coalesced 128-B rows per
+// slab), then the 8 partials are added in a fixed order through LDS:
+// deterministic.
 __global__ __launch_bounds__(256) void k_reduce_slabs(const sgnn_reduce_desc* descs,
                                                       const int32_t* block_start, int ndesc) {
-  __shared__ float part[4][64];
-  // descriptor of this block (block_start is an exclusive prefix of blocks per desc)
+  __shared__ float part[8][33];
   int lo = 0, hi = ndesc - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -881,23 +881,30 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const sgnn_reduce_desc* de
   }
   const sgnn_reduce_desc d = descs[lo];
   const int64_t total = (int64_t)d.nrows * d.ncols;
-  const int64_t idx = (int64_t)(blockIdx.x - block_start[lo]) * 64 + (threadIdx.x & 63);
-  const int q = threadIdx.x >> 6;
-  float s = 0.0f;
-  int64_t src_off = 0;
+  const int e = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int64_t idx = (int64_t)(blockIdx.x - block_start[lo]) * 32 + e;
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
   if (idx < total) {
     const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
-    src_off = d.offset + (int64_t)r * d.src_ld + cc;
-    for (int g = q; g < d.nslab; g += 4) {
-      const float* p = d.src + (int64_t)g * d.slab_stride + src_off;
-      for (int k = 0; k < d.nrep; ++k) s += p[(int64_t)k * d.rep_stride];
+    const float* base = d.src + d.offset + (int64_t)r * d.src_ld + cc;
+    for (int k = 0; k < d.nrep; ++k) {
+      const float* p = base + (int64_t)k * d.rep_stride;
+      int g = q;
+      for (; g + 24 < d.nslab; g += 32) {
+        s0 += p[(int64_t)g * d.slab_stride];
+        s1 += p[(int64_t)(g + 8) * d.slab_stride];
+        s2 += p[(int64_t)(g + 16) * d.slab_stride];
+        s3 += p[(int64_t)(g + 24) * d.slab_stride];
+      }
+      for (; g < d.nslab; g += 8) s0 += p[(int64_t)g * d.slab_stride];
     }
   }
-  part[q][threadIdx.x & 63] = s;
+  part[q][e] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (q == 0 && idx < total) {
-    const float t = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) +
-                    part[3][threadIdx.x];
+    float t = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][e];
     const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
     float* o = d.dst + (int64_t)r * d.dst_ld + cc;
     *o = d.accumulate ? *o + t * d.scale : t * d.scale;

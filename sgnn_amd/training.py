@@ -20,7 +20,8 @@ import torch.nn as nn
 from . import _hip, engine
 from ._hip import SgnnReduceDesc, SgnnSaves, check, lib, stream_ptr
 
-DEFAULT_NSLAB = 256  # persistent workgroups (one per CU) for the backward kernels
+DEFAULT_NSLAB = 256  # persistent workgroups (one per CU) for the edge backward kernels
+NODE_NSLAB = 256     # node-level backward kernels (128 measured slower: fewer CUs busy)
 
 
 class FlatParams:
@@ -54,6 +55,9 @@ class TrainWorkspace:
         L = lib()
         H, nl = epd.latent_dim, epd.nlayers
         self.H, self.L, self.n, self.T, self.dim, self.nslab = H, nl, n, T, dim, nslab
+        node_ns = max(1, min(nslab, NODE_NSLAB))
+        self.nslab_of = {_hip.SLAB_EDGE: nslab, _hip.SLAB_ENC_EDGE: nslab, _hip.SLAB_NODE: node_ns,
+                         _hip.SLAB_UV: node_ns, _hip.SLAB_DECODER: node_ns, _hip.SLAB_ENC_NODE: node_ns}
         self.feat = epd.nnode_in
         self.f = engine.StepWorkspace(n, T, dim, H, K, loop, device)
         cap = self.f.edge_cap
@@ -90,7 +94,7 @@ class TrainWorkspace:
                [(_hip.SLAB_ENC_NODE, 0), (_hip.SLAB_ENC_EDGE, 0)]
         for key in keys:
             self.slab_off[key] = off
-            off += nslab * self.slab_floats[key[0]]
+            off += self.nslab_of[key[0]] * self.slab_floats[key[0]]
         self.arena = torch.empty(off, **f32)
         self.loss_out = torch.zeros(8, **f32)
         self._descs_key = None
@@ -122,7 +126,7 @@ class TrainWorkspace:
             d.slab_stride = self.slab_floats[kind]
             d.offset = offset
             d.rep_stride = rep_stride
-            d.nslab, d.nrep, d.src_ld = ns, nrep, src_ld
+            d.nslab, d.nrep, d.src_ld = self.nslab_of[kind], nrep, src_ld
             d.nrows, d.ncols = nrows, ncols
             d.dst_ld = dst_ld if dst_ld is not None else ncols
             d.accumulate = 0
@@ -191,7 +195,7 @@ class TrainWorkspace:
         starts, nb = [], 0
         for d in descs:
             starts.append(nb)
-            nb += (d.nrows * d.ncols + 63) // 64
+            nb += (d.nrows * d.ncols + 31) // 32
         self._block_start = torch.tensor(starts, dtype=torch.int32).to(self.arena.device)
         self._nblocks = nb
         self._descs_key = key
@@ -299,34 +303,38 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                   p(next_strain), inp.acc_mean.data_ptr(), inp.acc_std.data_ptr(), n, T,
                                   d, float(w_pos), float(w_strain), float(inv_count), p(dpred),
                                   tw.hd.data_ptr(), tw.xs[tw.L].data_ptr(), ctypes.byref(pk.dec),
-                                  tw.g.data_ptr(), tw.slab(_hip.SLAB_DECODER), ns, s),
+                                  tw.g.data_ptr(), tw.slab(_hip.SLAB_DECODER), tw.nslab_of[_hip.SLAB_DECODER], s),
           "sgnn_decoder_loss_bwd")
     for k in range(tw.L - 1, -1, -1):
         check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, tw.n_yh[k].data_ptr(), tw.n_rstd[k].data_ptr(),
                                     tw.n_h[k].data_ptr(), tw.n_agg[k].data_ptr(), tw.xs[k].data_ptr(),
                                     ctypes.byref(pk.node[k]), tw.dagg.data_ptr(), tw.dxp.data_ptr(),
-                                    tw.slab(_hip.SLAB_NODE, k), ns, s), "sgnn_node_layer_bwd")
+                                    tw.slab(_hip.SLAB_NODE, k), tw.nslab_of[_hip.SLAB_NODE], s),
+              "sgnn_node_layer_bwd")
         with _Timer(timers, "k_edge_bwd"):
           check(L.sgnn_edge_layer_bwd(tw.dagg.data_ptr(), ws.rowptr.data_ptr(), ws.send.data_ptr(),
                                     ws.recv.data_ptr(), n, tw.e_h[k].data_ptr(), tw.e_yh[k].data_ptr(),
                                     tw.e_rstd[k].data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
                                     ctypes.byref(pk.edge[k]), tw.du.data_ptr(), ws.cin.data_ptr(),
                                     ws.cout.data_ptr(), tw.dh_rows.data_ptr(), tw.de0t.data_ptr(),
-                                    int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), ns, s),
+                                    int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), tw.nslab_of[_hip.SLAB_EDGE], s),
               "sgnn_edge_layer_bwd")
         check(L.sgnn_uv_bwd(tw.dxp.data_ptr(), tw.du.data_ptr(), ws.cin.data_ptr(), ws.cout.data_ptr(),
                             ws.rowptr.data_ptr(), tw.dh_rows.data_ptr(), tw.tptr.data_ptr(),
                             tw.tperm.data_ptr(), tw.xs[k].data_ptr(), n, ctypes.byref(pk.edge[k]),
-                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), ns, s), "sgnn_uv_bwd")
+                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV], s),
+              "sgnn_uv_bwd")
     check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d,
                                   inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius),
                                   tw.enc_h.data_ptr(), tw.enc_yh.data_ptr(), tw.enc_rstd.data_ptr(),
-                                  ctypes.byref(pk.enc_node), tw.slab(_hip.SLAB_ENC_NODE), ns, s),
+                                  ctypes.byref(pk.enc_node), tw.slab(_hip.SLAB_ENC_NODE),
+                                  tw.nslab_of[_hip.SLAB_ENC_NODE], s),
           "sgnn_encode_nodes_bwd")
     check(L.sgnn_encode_edges_bwd(tw.de0t.data_ptr(), inp.pos_seq.data_ptr() + 4 * (T - 1) * d, T * d,
                                   d, float(radius), ws.rowptr.data_ptr(), ws.send.data_ptr(),
                                   ws.recv.data_ptr(), n, tw.ee_yh.data_ptr(), tw.ee_rstd.data_ptr(),
-                                  ctypes.byref(pk.enc_edge), tw.slab(_hip.SLAB_ENC_EDGE), ns, s),
+                                  ctypes.byref(pk.enc_edge), tw.slab(_hip.SLAB_ENC_EDGE),
+                                  tw.nslab_of[_hip.SLAB_ENC_EDGE], s),
           "sgnn_encode_edges_bwd")
     check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
                               tw._nblocks, s), "sgnn_reduce_slabs")
