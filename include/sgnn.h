@@ -30,14 +30,17 @@ typedef enum sgnn_status {
 } sgnn_status;
 
 /* One build_mlp(...) (+ optional LayerNorm) parameter set,
- * sgnn/single_scale/graph_network.py:7-45 and :86-96 / :139-148.
- * nlin = number of Linear layers (nmlp_layers + 1). ln_g/ln_b may be NULL
- * (the Decoder has no LayerNorm, graph_network.py:321). */
+ * sgnn/single_scale/graph_network.py:7-45 and :86-96 / :139-148 (and the
+ * multi-scale copy, multi_scale_gnn.py:26-64).  nlin = number of Linear layers
+ * = nmlp_layers + 1, 2 or 3: w1 [hidden][in_dim]; nlin 2: w2 [out_dim][hidden];
+ * nlin 3: w2 [hidden][hidden] (middle) and w3 [out_dim][hidden].  ln_g/ln_b
+ * may be NULL (Decoder / prediction head have no LayerNorm). */
 typedef struct sgnn_mlp {
-  const float* w1; const float* b1; /* [hidden][in_dim] */
-  const float* w2; const float* b2; /* [out_dim][hidden] (nlin == 2) */
-  const float* ln_g; const float* ln_b; /* [out_dim] or NULL */
+  const float* w1; const float* b1;
+  const float* w2; const float* b2;
+  const float* ln_g; const float* ln_b;
   int32_t in_dim, hidden, out_dim, nlin;
+  const float* w3; const float* b3;
 } sgnn_mlp;
 
 /* Optional activation saves of the training forward (NULL pointer / NULL
@@ -74,10 +77,22 @@ int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n, int32_t d
                       int32_t loop, void* workspace, int32_t* rowptr, int32_t* send,
                       int32_t* recv, int64_t edge_cap, void* stream);
 
+/* Static graphs (multi-scale g2m/m2m/m2g edges, sgnn/multi_scale/
+ * multi_scale_graph.py:193-281, consumed by multi_scale_gnn.py:277-325):
+ * COO edge_index rows (src = edge_index[0] = sender, dst = edge_index[1] =
+ * receiver, int64, values in [0, n)) -> receiver-sorted CSR, stable (edges of
+ * one receiver keep their original order = PyG's scatter-add order).
+ * rowptr [n+1], send/recv [E]. */
+size_t sgnn_coo_workspace_bytes(int64_t n, int64_t E);
+int sgnn_coo_to_csr(const int64_t* src, const int64_t* dst, int64_t E, int64_t n, void* workspace,
+                    int32_t* rowptr, int32_t* send, int32_t* recv, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Encoder, node side: node features of LearnedSimulator._encoder_preprocessor
  * (learned_simulator.py:256-290: normalised velocity history, wall distance
- * clamp(x+2, 0, R), optional type embedding) fused with Encoder.node_fn
+ * clamp(x+2, 0, wall_max) / wall_div — single scale: (R, 1), learned_simulator.py:
+ * 282-284; multi scale: (R_g, R_g), multi_scale_simulator.py:190-193 —,
+ * optional type embedding) fused with Encoder.node_fn
  * (graph_network.py:86-90, :111) and with the receiver/sender projections of
  * the first InteractionNetwork's edge MLP:
  *   u = x0 W1[:, 0:H]^T + b1,  v = x0 W1[:, H:2H]^T   (W1 of edge0)
@@ -86,8 +101,9 @@ int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n, int32_t d
 int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int32_t dim,
                       const int64_t* types, const float* emb_w, int32_t emb_dim,
                       int32_t use_emb, const float* vel_mean, const float* vel_std,
-                      float radius, const sgnn_mlp* enc, const sgnn_mlp* edge0,
-                      float* x0, float* u, float* v, const sgnn_saves* saves, void* stream);
+                      float wall_max, float wall_div, const sgnn_mlp* enc,
+                      const sgnn_mlp* edge0, float* x0, float* u, float* v,
+                      const sgnn_saves* saves, void* stream);
 
 /* Encoder, edge side: edge features (learned_simulator.py:299-312:
  * (p_s - p_r)/R and its norm) fused with Encoder.edge_fn (graph_network.py:

@@ -23,7 +23,8 @@ class SgnnMlp(ctypes.Structure):
     """struct sgnn_mlp (include/sgnn.h)."""
     _fields_ = [("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p), ("b2", c_void_p),
                 ("ln_g", c_void_p), ("ln_b", c_void_p),
-                ("in_dim", c_int32), ("hidden", c_int32), ("out_dim", c_int32), ("nlin", c_int32)]
+                ("in_dim", c_int32), ("hidden", c_int32), ("out_dim", c_int32), ("nlin", c_int32),
+                ("w3", c_void_p), ("b3", c_void_p)]
 
 
 P_MLP = ctypes.POINTER(SgnnMlp)
@@ -55,8 +56,9 @@ SIGNATURES = {
                                          c_float, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_int64, c_void_p]),
     "sgnn_encode_nodes": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
-                                         c_int32, c_int32, c_void_p, c_void_p, c_float, P_MLP,
-                                         P_MLP, c_void_p, c_void_p, c_void_p, P_SAVES, c_void_p]),
+                                         c_int32, c_int32, c_void_p, c_void_p, c_float, c_float,
+                                         P_MLP, P_MLP, c_void_p, c_void_p, c_void_p, P_SAVES,
+                                         c_void_p]),
     "sgnn_edge_latent_floats": (c_int64, [c_int64, c_int32]),
     "sgnn_encode_edges": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
                                          c_void_p, c_int64, c_int64, P_MLP, c_void_p, P_SAVES,
@@ -71,6 +73,9 @@ SIGNATURES = {
                                               c_int64, P_MLP, P_MLP, c_void_p, c_int32, c_int32,
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p, P_SAVES, c_void_p]),
+    "sgnn_coo_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64]),
+    "sgnn_coo_to_csr": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p]),
     "sgnn_bwd_slab_floats": (c_int64, [c_int32, c_int32, c_int32]),
     "sgnn_reduce_slabs": (ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "sgnn_transpose_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64]),

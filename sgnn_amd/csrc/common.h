@@ -341,3 +341,21 @@ SGNN_DEV void stage_matrix_t(float* lds, int ld, const float* g, int ldg, int ro
     lds[c * ld + r] = v;
   }
 }
+
+// Tail of an MLP after its first ReLU: y = LAST(relu(MID(h))) for 3 Linear
+// layers (nmlp_layers = 2), y = LAST(h) for 2 (nmlp_layers = 1).
+template <int TH, int NL, int TO>
+SGNN_DEV void mlp_tail(f32x16 (&y)[TO], const f32x16 (&h)[TH], const float* Wm, int ldm,
+                       const float* bm_lds, const float* Wl, int ldl, const float* bl_lds) {
+  if constexpr (NL == 3) {
+    f32x16 h2[TH];
+    acc_bias<TH>(h2, bm_lds);
+    mfma_from_acc<TH, TH>(h2, Wm, ldm, 0, h);
+    acc_relu<TH>(h2);
+    acc_bias<TO>(y, bl_lds);
+    mfma_from_acc<TO, TH>(y, Wl, ldl, 0, h2);
+  } else {
+    acc_bias<TO>(y, bl_lds);
+    mfma_from_acc<TO, TH>(y, Wl, ldl, 0, h);
+  }
+}

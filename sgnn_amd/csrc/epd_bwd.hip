@@ -114,8 +114,8 @@ SGNN_DEV void load_resolved(f32x16 (&a)[TH], const float* rows, const float* cin
   if (t0 == t1) {
     load_row_clayout<TH>(a, rows + i * H);
   } else {
-    load_row_clayout<TH>(a, cout + (int64_t)t0 * H);
-    add_row_clayout<TH>(a, cin + (int64_t)t1 * H);
+    load_row_clayout<TH>(a, cout + (int64_t)t0 * H);  // segments may span > 2 tiles
+    for (int32_t t = t0 + 1; t <= t1; ++t) add_row_clayout<TH>(a, cin + (int64_t)t * H);
   }
 }
 

@@ -38,7 +38,9 @@ struct EncNodeArgs {
   const float* vel_std;
   float radius;
   int feat;  // number of real node features
-  const float *w1, *b1, *w2, *b2, *g, *bb;  // encoder node MLP
+  const float *w1, *b1, *w2, *b2, *g, *bb;  // encoder node MLP (w2/b2 = LAST Linear)
+  const float *wm, *bm;                     // middle Linear (nlin = 3) or null
+  float wall_max, wall_div;                 // clamp(x+2, 0, wall_max) / wall_div
   const float *we, *be;                     // edge0 W1 [H][3H], b1
   float *x0, *u, *v;
   sgnn_saves sv;
@@ -68,7 +70,7 @@ SGNN_DEV void store_uv2(const float* Wi, int ldi, const float* Wj, int ldj, cons
   if (valid) store_row_clayout<TH>(v_row, acc);
 }
 
-template <int TH, int TKF, bool TRAIN>
+template <int TH, int TKF, bool TRAIN, int NL>
 __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
   constexpr bool GW = TH > 2;  // H = 128: weights read from L2 (460 KB/layer > LDS)
   constexpr int H = 32 * TH, ldf = 32 * TKF + 4;
@@ -84,7 +86,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
   float* g = b2 + H;
   float* bb = g + H;
   float* b1e = bb + H;
+  float* bm = b1e + H;
   stage_matrix(W1, ldf, a.w1, a.feat, H, a.feat, H, 32 * TKF);
+  if (NL == 3) stage_vec(bm, a.bm, H, H);
   if (!GW) {
     stage_matrix(sW, ldh, a.w2, H, H, H, H, H);
     stage_matrix(sW + H * ldh, ldh, a.we, 3 * H, H, H, H, H);
@@ -117,7 +121,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
           const float vel = __fsub_rn(p[(t + 1) * a.dim + c], p[t * a.dim + c]);
           val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[c]), a.vel_std[c]);
         } else if (f == nvel) {  // :282-284
-          val = fminf(fmaxf(__fadd_rn(p[(a.T - 1) * a.dim], 2.0f), 0.0f), a.radius);
+          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(p[(a.T - 1) * a.dim], 2.0f), 0.0f), a.wall_max),
+                          a.wall_div);
         } else if (a.use_emb && f < nvel + 1 + a.emb_dim) {  // :287-290
           val = a.emb_w[a.types[ic] * a.emb_dim + (f - nvel - 1)];
         }
@@ -129,8 +134,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
     acc_relu<TH>(hacc);
     if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
     f32x16 y[TH];
-    acc_bias<TH>(y, b2);
-    mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
+    mlp_tail<TH, NL, TH>(y, hacc, a.wm, H, bm, W2, ldh, b2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -157,9 +161,10 @@ struct EncEdgeArgs {
   const float *w1, *b1, *w2, *b2, *g, *bb;
   float* e0t;
   sgnn_saves sv;
+  const float *wm, *bm;
 };
 
-template <int TH, bool TRAIN>
+template <int TH, bool TRAIN, int NL>
 __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
   constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = GW ? H : H + 4, ld1 = 5;
@@ -171,7 +176,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
   float* b2 = b1 + H;
   float* g = b2 + H;
   float* bb = g + H;
+  float* bm = bb + H;
   stage_matrix(W1, ld1, a.w1, a.dim + 1, H, a.dim + 1, H, 4);
+  if (NL == 3) stage_vec(bm, a.bm, H, H);
   if (!GW) stage_matrix(sW, ldh, a.w2, H, H, H, H, H);
   stage_vec(b1, a.b1, H, H);
   stage_vec(b2, a.b2, H, H);
@@ -201,8 +208,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
     mfma_step<TH>(hacc, W1, ld1, 2 + h, h ? f[3] : f[2]);
     acc_relu<TH>(hacc);
     f32x16 y[TH];
-    acc_bias<TH>(y, b2);
-    mfma_from_acc<TH, TH>(y, W2, ldh, 0, hacc);
+    mlp_tail<TH, NL, TH>(y, hacc, a.wm, H, bm, W2, ldh, b2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -230,12 +236,13 @@ struct EdgeLayerArgs {
   float e_scale;
   const int32_t *rowptr, *send, *recv;
   int64_t n;
-  const float *we, *w2, *b2, *g, *bb;  // we = edge W1 + 2H (ld 3H)
+  const float *we, *w2, *b2, *g, *bb;  // we = edge W1 + 2H (ld 3H); w2 = LAST Linear
   float *agg, *cin, *cout;
   sgnn_saves sv;
+  const float *wm, *bm;
 };
 
-template <int TH, bool TRAIN>
+template <int TH, bool TRAIN, int NL>
 __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
   constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4;            // ldh: LDS image leading dim
@@ -247,7 +254,9 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
   float* b2 = GW ? sW : sW + 2 * H * ldh;
   float* g = b2 + H;
   float* bb = g + H;
-  float* mbuf = bb + H;  // per wave [32][ldh]
+  float* bm = bb + H;
+  float* mbuf = bm + (NL == 3 ? H : 0);  // per wave [32][ldh]
+  if (NL == 3) stage_vec(bm, a.bm, H, H);
   if (!GW) {
     stage_matrix(sW, ldh, a.we, 3 * H, H, H, H, H);
     stage_matrix(sW + H * ldh, ldh, a.w2, H, H, H, H, H);
@@ -282,8 +291,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     acc_relu<TH>(hacc);
     if (TRAIN) store_tiled<TH>(a.sv.h + tile * (32 * H), hacc);
     f32x16 y[TH];
-    acc_bias<TH>(y, b2);
-    mfma_from_acc<TH, TH>(y, W2, ldw2, 0, hacc);
+    mlp_tail<TH, NL, TH>(y, hacc, a.wm, H, bm, W2, ldw2, b2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -350,6 +358,8 @@ struct NodeLayerArgs {
   float *pred, *next_pos, *window_out;
   float* x_out;
   sgnn_saves sv;
+  const float *wm, *bm;    // node MLP middle Linear (nlin = 3)
+  const float *wdm, *bdm;  // decoder middle Linear (nlin = 3)
 };
 
 template <int TH>
@@ -367,12 +377,14 @@ SGNN_DEV void load_agg(f32x16 (&a)[TH], const NodeLayerArgs& p, int64_t i) {
   if (t0 == t1) {
     load_row_clayout<TH>(a, p.agg + i * H);
   } else {
+    // head partial + every later tile's partial (a segment longer than 32
+    // edges leaves whole-tile sums in cin of the tiles it spans)
     load_row_clayout<TH>(a, p.cout + (int64_t)t0 * H);
-    add_row_clayout<TH>(a, p.cin + (int64_t)t1 * H);
+    for (int32_t t = t0 + 1; t <= t1; ++t) add_row_clayout<TH>(a, p.cin + (int64_t)t * H);
   }
 }
 
-template <int TH, int MODE, bool TRAIN>
+template <int TH, int MODE, bool TRAIN, int NL>
 __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
   constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4;
@@ -393,6 +405,12 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
   float* bb = g + H;
   float* ba = bb + H;  // mode 0: b1e   mode 1: decoder b1
   float* bd2 = ba + H;  // mode 1: decoder b2 (32)
+  float* bm = bd2 + 32;  // nlin 3: node MLP middle bias
+  float* bdm = bm + H;   // nlin 3: decoder middle bias
+  if (NL == 3) {
+    stage_vec(bm, a.bm, H, H);
+    if (MODE == 1) stage_vec(bdm, a.bdm, H, H);
+  }
   if (!GW) {
     stage_matrix(sW, ld2, a.w1, 2 * H, H, 2 * H, H, 2 * H);
     stage_matrix(sW + H * ld2, ldh, a.w2, H, H, H, H, H);
@@ -432,8 +450,7 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
     acc_relu<TH>(hacc);
     if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
     f32x16 y[TH];
-    acc_bias<TH>(y, b2);
-    mfma_from_acc<TH, TH>(y, W2, ldw2, 0, hacc);
+    mlp_tail<TH, NL, TH>(y, hacc, a.wm, H, bm, W2, ldw2, b2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -459,8 +476,7 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
       acc_relu<TH>(hd);
       if (TRAIN && valid) store_row_clayout<TH>(a.sv.hd + i * H, hd);
       f32x16 o[1];
-      acc_bias<1>(o, bd2);
-      mfma_from_acc<1, TH>(o, Wb, ldh, 0, hd);
+      mlp_tail<TH, NL, 1>(o, hd, a.wdm, H, bdm, Wb, ldh, bd2);
       if (valid && h == 0) {  // lanes with h == 0 hold units 0..3 in registers 0..3
         const int D = a.dim;
         for (int c = 0; c <= D; ++c) a.pred[i * (D + 1) + c] = o[0][c];
@@ -487,33 +503,67 @@ int check_mlp(const sgnn_mlp* m, int in_dim, int hidden, int out_dim, bool need_
               const char* what) {
   if (!m || !m->w1 || !m->b1 || !m->w2 || !m->b2)
     return sgnn::set_error(SGNN_ERR_INVALID, what);
-  if (m->nlin != 2) return sgnn::set_error(SGNN_ERR_UNSUPPORTED, "only nmlp_layers=1 (2 Linear) MLPs");
+  if (m->nlin != 2 && m->nlin != 3)
+    return sgnn::set_error(SGNN_ERR_UNSUPPORTED, "MLPs must have 2 or 3 Linear layers (nmlp_layers 1 or 2)");
+  if (m->nlin == 3 && (!m->w3 || !m->b3)) return sgnn::set_error(SGNN_ERR_INVALID, what);
   if ((in_dim >= 0 && m->in_dim != in_dim) || m->hidden != hidden || m->out_dim != out_dim)
     return sgnn::set_error(SGNN_ERR_INVALID, what);
   if (need_ln && (!m->ln_g || !m->ln_b)) return sgnn::set_error(SGNN_ERR_INVALID, what);
   return SGNN_OK;
 }
 
+const float* last_w(const sgnn_mlp* m) { return m->nlin == 3 ? m->w3 : m->w2; }
+const float* last_b(const sgnn_mlp* m) { return m->nlin == 3 ? m->b3 : m->b2; }
+const float* mid_w(const sgnn_mlp* m) { return m->nlin == 3 ? m->w2 : nullptr; }
+const float* mid_b(const sgnn_mlp* m) { return m->nlin == 3 ? m->b2 : nullptr; }
+
 template <typename K>
 void set_lds(K kernel, size_t bytes) {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <typename K, typename A>
+void launch1(K k, unsigned grid, size_t lds, hipStream_t s, const A& a) {
+  set_lds(k, lds);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, s, a);
 }
 
 constexpr size_t kLdsMax = 160 * 1024;
 
-template <typename KI, typename KT, typename A>
-void launch2(KI ki, KT kt, bool train, unsigned grid, size_t lds, hipStream_t s, const A& a) {
-  if (train) {
-    set_lds(kt, lds);
-    hipLaunchKernelGGL(kt, dim3(grid), dim3(kBlock), lds, s, a);
-  } else {
-    set_lds(ki, lds);
-    hipLaunchKernelGGL(ki, dim3(grid), dim3(kBlock), lds, s, a);
+bool want_saves(const sgnn_saves* sv) { return sv != nullptr && sv->yhat != nullptr; }
+
+template <int TH, int TKF, int NL>
+void go_encode_nodes(bool train, unsigned grid, size_t lds, hipStream_t s, const EncNodeArgs& a) {
+  if constexpr (NL == 2) {
+    if (train) return launch1(k_encode_nodes<TH, TKF, true, 2>, grid, lds, s, a);
   }
+  launch1(k_encode_nodes<TH, TKF, false, NL>, grid, lds, s, a);
 }
 
-bool want_saves(const sgnn_saves* sv) { return sv != nullptr && sv->yhat != nullptr; }
+template <int TH, int NL>
+void go_encode_edges(bool train, unsigned grid, size_t lds, hipStream_t s, const EncEdgeArgs& a) {
+  if constexpr (NL == 2) {
+    if (train) return launch1(k_encode_edges<TH, true, 2>, grid, lds, s, a);
+  }
+  launch1(k_encode_edges<TH, false, NL>, grid, lds, s, a);
+}
+
+template <int TH, int NL>
+void go_edge_layer(bool train, unsigned grid, size_t lds, hipStream_t s, const EdgeLayerArgs& a) {
+  if constexpr (NL == 2) {
+    if (train) return launch1(k_edge_layer<TH, true, 2>, grid, lds, s, a);
+  }
+  launch1(k_edge_layer<TH, false, NL>, grid, lds, s, a);
+}
+
+template <int TH, int MODE, int NL>
+void go_node_layer(bool train, unsigned grid, size_t lds, hipStream_t s, const NodeLayerArgs& a) {
+  if constexpr (NL == 2) {
+    if (train) return launch1(k_node_layer<TH, MODE, true, 2>, grid, lds, s, a);
+  }
+  launch1(k_node_layer<TH, MODE, false, NL>, grid, lds, s, a);
+}
 
 }  // namespace
 
@@ -521,12 +571,26 @@ extern "C" int64_t sgnn_edge_latent_floats(int64_t edge_cap, int32_t hidden) {
   return ((edge_cap + 31) / 32) * 32 * (int64_t)hidden;
 }
 
+#define SGNN_DISPATCH_H_NL(H, NL, CALL)                                   \
+  do {                                                                    \
+    if ((H) == 64 && (NL) == 2) { constexpr int TH_ = 2, NL_ = 2; CALL; } \
+    else if ((H) == 64) { constexpr int TH_ = 2, NL_ = 3; CALL; }         \
+    else if ((NL) == 2) { constexpr int TH_ = 4, NL_ = 2; CALL; }         \
+    else { constexpr int TH_ = 4, NL_ = 3; CALL; }                        \
+  } while (0)
+
+static int check_train(bool train, const sgnn_mlp* m, const char* what) {
+  if (train && m->nlin != 2)
+    return sgnn::set_error(SGNN_ERR_UNSUPPORTED, what);
+  return SGNN_OK;
+}
+
 extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int32_t dim,
                                  const int64_t* types, const float* emb_w, int32_t emb_dim,
                                  int32_t use_emb, const float* vel_mean, const float* vel_std,
-                                 float radius, const sgnn_mlp* enc, const sgnn_mlp* edge0,
-                                 float* x0, float* u, float* v, const sgnn_saves* saves,
-                                 void* stream) {
+                                 float wall_max, float wall_div, const sgnn_mlp* enc,
+                                 const sgnn_mlp* edge0, float* x0, float* u, float* v,
+                                 const sgnn_saves* saves, void* stream) {
   using namespace sgnn;
   if (n <= 0) return SGNN_OK;
   if (!pos_seq || !vel_mean || !vel_std || !x0 || !u || !v || T < 2 || dim < 1 || dim > 3)
@@ -539,33 +603,27 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
   if (st) return st;
   if (use_emb && (!types || !emb_w)) return set_error(SGNN_ERR_INVALID, "encode_nodes: embedding");
   if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: hidden must be 64 or 128");
-  EncNodeArgs a{pos_seq, n, T, dim, types, emb_w, emb_dim, use_emb, vel_mean, vel_std, radius,
-                feat, enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, edge0->w1,
-                edge0->b1, x0, u, v, {}};
+  EncNodeArgs a{pos_seq, n, T, dim, types, emb_w, emb_dim, use_emb, vel_mean, vel_std, wall_max,
+                feat, enc->w1, enc->b1, last_w(enc), last_b(enc), enc->ln_g, enc->ln_b,
+                mid_w(enc), mid_b(enc), wall_max, wall_div, edge0->w1, edge0->b1, x0, u, v, {}};
   const bool train = want_saves(saves);
+  if ((st = check_train(train, enc, "encode_nodes: training saves need nmlp_layers = 1"))) return st;
   if (train) {
     if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "encode_nodes: saves");
     a.sv = *saves;
   }
   const unsigned grid = persistent_grid(n, 32 * kWaves, 2);
   const int tkf = (feat + 31) / 32;
-  const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + (H == 64 ? 3 * H * (H + 4) : 0) + 5 * H);
+  const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + (H == 64 ? 3 * H * (H + 4) : 0) + 6 * H);
   if (lds > kLdsMax) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: too many features");
+  if (tkf > 3 || (tkf == 3 && H != 64))
+    return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: too many node features");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (tkf) {
-    case 1:
-      if (H == 64) launch2(k_encode_nodes<2, 1, false>, k_encode_nodes<2, 1, true>, train, grid, lds, s, a);
-      else launch2(k_encode_nodes<4, 1, false>, k_encode_nodes<4, 1, true>, train, grid, lds, s, a);
-      break;
-    case 2:
-      if (H == 64) launch2(k_encode_nodes<2, 2, false>, k_encode_nodes<2, 2, true>, train, grid, lds, s, a);
-      else launch2(k_encode_nodes<4, 2, false>, k_encode_nodes<4, 2, true>, train, grid, lds, s, a);
-      break;
-    case 3:
-      if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: > 64 features at hidden 128");
-      launch2(k_encode_nodes<2, 3, false>, k_encode_nodes<2, 3, true>, train, grid, lds, s, a);
-      break;
-    default: return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes: > 96 node features");
+  if (tkf == 1) SGNN_DISPATCH_H_NL(H, enc->nlin, (go_encode_nodes<TH_, 1, NL_>(train, grid, lds, s, a)));
+  else if (tkf == 2) SGNN_DISPATCH_H_NL(H, enc->nlin, (go_encode_nodes<TH_, 2, NL_>(train, grid, lds, s, a)));
+  else {
+    if (enc->nlin == 2) go_encode_nodes<2, 3, 2>(train, grid, lds, s, a);
+    else go_encode_nodes<2, 3, 3>(train, grid, lds, s, a);
   }
   return check_launch("encode_nodes");
 }
@@ -583,18 +641,18 @@ extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t d
   int st = check_mlp(enc, dim + 1, H, H, true, "encode_edges: encoder MLP shape");
   if (st) return st;
   if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "encode_edges: hidden must be 64 or 128");
-  EncEdgeArgs a{pos, pos_stride, dim, radius, rowptr, send, recv, n,
-                enc->w1, enc->b1, enc->w2, enc->b2, enc->ln_g, enc->ln_b, e0t, {}};
+  EncEdgeArgs a{pos, pos_stride, dim, radius, rowptr, send, recv, n, enc->w1, enc->b1,
+                last_w(enc), last_b(enc), enc->ln_g, enc->ln_b, e0t, {}, mid_w(enc), mid_b(enc)};
   const bool train = want_saves(saves);
+  if ((st = check_train(train, enc, "encode_edges: training saves need nmlp_layers = 1"))) return st;
   if (train) {
     if (!saves->rstd) return set_error(SGNN_ERR_INVALID, "encode_edges: saves");
     a.sv = *saves;
   }
   const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 4);
-  const size_t lds = sizeof(float) * (size_t)(H * 5 + (H == 64 ? H * (H + 4) : 0) + 4 * H);
+  const size_t lds = sizeof(float) * (size_t)(H * 5 + (H == 64 ? H * (H + 4) : 0) + 5 * H);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (H == 64) launch2(k_encode_edges<2, false>, k_encode_edges<2, true>, train, grid, lds, s, a);
-  else launch2(k_encode_edges<4, false>, k_encode_edges<4, true>, train, grid, lds, s, a);
+  SGNN_DISPATCH_H_NL(H, enc->nlin, (go_encode_edges<TH_, NL_>(train, grid, lds, s, a)));
   return check_launch("encode_edges");
 }
 
@@ -610,47 +668,48 @@ extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t,
   int st = check_mlp(edge_fn, 3 * H, H, H, true, "edge_layer: edge MLP shape");
   if (st) return st;
   if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer: hidden must be 64 or 128");
-  EdgeLayerArgs a{u, v, e0t, e_scale, rowptr, send, recv, n, edge_fn->w1 + 2 * H, edge_fn->w2,
-                  edge_fn->b2, edge_fn->ln_g, edge_fn->ln_b, agg, cin, cout, {}};
+  EdgeLayerArgs a{u, v, e0t, e_scale, rowptr, send, recv, n, edge_fn->w1 + 2 * H, last_w(edge_fn),
+                  last_b(edge_fn), edge_fn->ln_g, edge_fn->ln_b, agg, cin, cout, {},
+                  mid_w(edge_fn), mid_b(edge_fn)};
   const bool train = want_saves(saves);
+  if ((st = check_train(train, edge_fn, "edge_layer: training saves need nmlp_layers = 1"))) return st;
   if (train) {
     if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "edge_layer: saves");
     a.sv = *saves;
   }
-  const size_t lds = sizeof(float) * (size_t)((H == 64 ? 2 * H * (H + 4) : 0) + 3 * H + kWaves * 32 * (H + 4));
+  const size_t lds = sizeof(float) * (size_t)((H == 64 ? 2 * H * (H + 4) : 0) + 4 * H + kWaves * 32 * (H + 4));
   const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 2);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (H == 64) launch2(k_edge_layer<2, false>, k_edge_layer<2, true>, train, grid, lds, s, a);
-  else launch2(k_edge_layer<4, false>, k_edge_layer<4, true>, train, grid, lds, s, a);
+  SGNN_DISPATCH_H_NL(H, edge_fn->nlin, (go_edge_layer<TH_, NL_>(train, grid, lds, s, a)));
   return check_launch("edge_layer");
 }
 
-static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode,
+static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode, int dec_nlin,
                              const sgnn_saves* saves, void* stream) {
   using namespace sgnn;
   const int H = node_fn ? node_fn->hidden : 0;
   int st = check_mlp(node_fn, 2 * H, H, H, true, "node_layer: node MLP shape");
   if (st) return st;
   if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "node_layer: hidden must be 64 or 128");
-  a.w1 = node_fn->w1; a.b1 = node_fn->b1; a.w2 = node_fn->w2; a.b2 = node_fn->b2;
+  if (mode == 1 && dec_nlin != node_fn->nlin)
+    return set_error(SGNN_ERR_UNSUPPORTED, "node_layer_decode: decoder and node MLP depths differ");
+  a.w1 = node_fn->w1; a.b1 = node_fn->b1; a.w2 = last_w(node_fn); a.b2 = last_b(node_fn);
+  a.wm = mid_w(node_fn); a.bm = mid_b(node_fn);
   a.g = node_fn->ln_g; a.bb = node_fn->ln_b;
   const bool train = want_saves(saves);
+  if ((st = check_train(train, node_fn, "node_layer: training saves need nmlp_layers = 1"))) return st;
   if (train) {
     if (!saves->h || !saves->rstd || !saves->agg || (mode == 1 && (!saves->hd || !a.x_out)))
       return set_error(SGNN_ERR_INVALID, "node_layer: saves");
     a.sv = *saves;
   }
-  const size_t lds = sizeof(float) * (size_t)(H == 64 ? H * (2 * H + 4) + 3 * H * (H + 4) + 5 * H + 32
-                                                      : H * (H + 4) + 5 * H + 32);
+  const size_t vec = 5 * H + 32 + 2 * H;
+  const size_t lds = sizeof(float) * (H == 64 ? H * (2 * H + 4) + 3 * H * (H + 4) + vec
+                                              : H * (H + 4) + vec);
   const unsigned grid = persistent_grid(a.n, 32 * kWaves, H == 64 ? 1 : 2);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (H == 64) {
-    if (mode == 0) launch2(k_node_layer<2, 0, false>, k_node_layer<2, 0, true>, train, grid, lds, s, a);
-    else launch2(k_node_layer<2, 1, false>, k_node_layer<2, 1, true>, train, grid, lds, s, a);
-  } else {
-    if (mode == 0) launch2(k_node_layer<4, 0, false>, k_node_layer<4, 0, true>, train, grid, lds, s, a);
-    else launch2(k_node_layer<4, 1, false>, k_node_layer<4, 1, true>, train, grid, lds, s, a);
-  }
+  if (mode == 0) SGNN_DISPATCH_H_NL(H, node_fn->nlin, (go_node_layer<TH_, 0, NL_>(train, grid, lds, s, a)));
+  else SGNN_DISPATCH_H_NL(H, node_fn->nlin, (go_node_layer<TH_, 1, NL_>(train, grid, lds, s, a)));
   return check_launch("node_layer");
 }
 
@@ -668,7 +727,7 @@ extern "C" int sgnn_node_layer(const float* x_in, const float* agg, const float*
   NodeLayerArgs a{};
   a.x_in = x_in; a.agg = agg; a.cin = cin; a.cout = cout; a.rowptr = rowptr; a.n = n;
   a.we = next_edge->w1; a.be = next_edge->b1; a.u = u; a.v = v; a.x_out = x_out;
-  return node_layer_common(a, node_fn, 0, saves, stream);
+  return node_layer_common(a, node_fn, 0, 0, saves, stream);
 }
 
 extern "C" int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin,
@@ -688,9 +747,10 @@ extern "C" int sgnn_node_layer_decode(const float* x_in, const float* agg, const
   if (st) return st;
   NodeLayerArgs a{};
   a.x_in = x_in; a.agg = agg; a.cin = cin; a.cout = cout; a.rowptr = rowptr; a.n = n;
-  a.wd1 = decoder->w1; a.bd1 = decoder->b1; a.wd2 = decoder->w2; a.bd2 = decoder->b2;
+  a.wd1 = decoder->w1; a.bd1 = decoder->b1; a.wd2 = last_w(decoder); a.bd2 = last_b(decoder);
+  a.wdm = mid_w(decoder); a.bdm = mid_b(decoder);
   a.pos_seq = pos_seq; a.T = T; a.dim = dim; a.acc_mean = acc_mean; a.acc_std = acc_std;
   a.pred = pred; a.next_pos = next_pos; a.window_out = window_out; a.x_out = x_out;
   if (window_out == pos_seq) return set_error(SGNN_ERR_INVALID, "node_layer_decode: window_out aliases pos_seq");
-  return node_layer_common(a, node_fn, 1, saves, stream);
+  return node_layer_common(a, node_fn, 1, decoder->nlin, saves, stream);
 }

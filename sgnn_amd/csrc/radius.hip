@@ -469,3 +469,80 @@ extern "C" int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n
                      w.nbr, w.deg, rowptr, send, recv);
   return check_launch("radius_graph");
 }
+
+// ---------------------------------------------------------------------------
+// Static graphs (multi-scale g2m / m2m / m2g, sgnn/multi_scale/
+// multi_scale_graph.py:193-281): COO edge_index [2][E] (int64, row 0 =
+// sender j, row 1 = receiver i, PyG flow source_to_target) -> the receiver-
+// sorted CSR the layer kernels consume.  Stable: within a receiver, edges keep
+// their original order, i.e. the order PyG's scatter-add sums them in.
+namespace {
+
+__global__ __launch_bounds__(256) void k_coo_count(const int64_t* dst, int64_t E, int32_t* cnt) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[dst[e]], 1);
+}
+
+__global__ __launch_bounds__(256) void k_coo_fill(const int64_t* dst, int64_t E, const int32_t* ptr,
+                                                  int32_t* fill, int32_t* raw) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = dst[e];
+    raw[ptr[d] + atomicAdd(&fill[d], 1)] = (int32_t)e;
+  }
+}
+
+// one wave per receiver: rank = number of smaller edge ids in its segment
+__global__ __launch_bounds__(256) void k_coo_sort(const int32_t* ptr, int64_t n, const int32_t* raw,
+                                                  const int64_t* src, const int64_t* dst,
+                                                  int32_t* send, int32_t* recv) {
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int32_t b = ptr[i], len = ptr[i + 1] - b;
+  for (int q = lane; q < len; q += 64) {
+    const int32_t key = raw[b + q];
+    int rank = 0;
+    for (int t = 0; t < len; ++t) rank += raw[b + t] < key;
+    send[b + rank] = (int32_t)src[key];
+    recv[b + rank] = (int32_t)dst[key];
+  }
+}
+
+}  // namespace
+
+extern "C" size_t sgnn_coo_workspace_bytes(int64_t n, int64_t E) {
+  return sizeof(int32_t) * (size_t)(2 * (n + 1) + E) + 3 * 256 + 65536;
+}
+
+extern "C" int sgnn_coo_to_csr(const int64_t* src, const int64_t* dst, int64_t E, int64_t n,
+                               void* workspace, int32_t* rowptr, int32_t* send, int32_t* recv,
+                               void* stream_) {
+  using namespace sgnn;
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  if (n <= 0 || E < 0 || !rowptr || !workspace || (E > 0 && (!src || !dst || !send || !recv)))
+    return set_error(SGNN_ERR_INVALID, "coo_to_csr: bad arguments");
+  if (E >= ((int64_t)1 << 31)) return set_error(SGNN_ERR_UNSUPPORTED, "coo_to_csr: E >= 2^31");
+  char* p = static_cast<char*>(workspace);
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += (bytes + 255) & ~size_t(255);
+    return r;
+  };
+  int32_t* cnt = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 2 * (n + 1)));
+  int32_t* fill = cnt + (n + 1);
+  int32_t* raw = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (E > 0 ? E : 1)));
+  int32_t* partials = reinterpret_cast<int32_t*>(take(65536 - 512));
+  (void)hipMemsetAsync(cnt, 0, sizeof(int32_t) * 2 * (n + 1), s);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((E + 255) / 256, 2048));
+  if (E > 0) hipLaunchKernelGGL(k_coo_count, dim3(g), dim3(256), 0, s, dst, E, cnt);
+  int st = scan_exclusive(cnt, rowptr, n + 1, partials, s);
+  if (st) return st;
+  if (E > 0) {
+    hipLaunchKernelGGL(k_coo_fill, dim3(g), dim3(256), 0, s, dst, E, rowptr, fill, raw);
+    hipLaunchKernelGGL(k_coo_sort, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, rowptr, n, raw,
+                       src, dst, send, recv);
+  }
+  return check_launch("coo_to_csr");
+}

@@ -45,14 +45,16 @@ def mlp_struct(seq: nn.Module, has_ln: bool) -> SgnnMlp:
         if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
             raise ValueError("sgnn_amd parameters must be contiguous fp32 GPU tensors "
                              "(call simulator.to('cuda'))")
-    if len(lin) != 2:
-        raise NotImplementedError("libsgnn_hip implements nmlp_layers=1 (Linear-ReLU-Linear) MLPs")
+    if len(lin) not in (2, 3):
+        raise NotImplementedError("libsgnn_hip implements nmlp_layers = 1 or 2 MLPs")
     return SgnnMlp(w1=lin[0].weight.data_ptr(), b1=lin[0].bias.data_ptr(),
                    w2=lin[1].weight.data_ptr(), b2=lin[1].bias.data_ptr(),
                    ln_g=_ptr(ln.weight) if ln is not None else 0,
                    ln_b=_ptr(ln.bias) if ln is not None else 0,
                    in_dim=lin[0].in_features, hidden=lin[0].out_features,
-                   out_dim=lin[-1].out_features, nlin=len(lin))
+                   out_dim=lin[-1].out_features, nlin=len(lin),
+                   w3=lin[2].weight.data_ptr() if len(lin) == 3 else 0,
+                   b3=lin[2].bias.data_ptr() if len(lin) == 3 else 0)
 
 
 class ParamPack:
@@ -142,6 +144,81 @@ def radius_graph(ws: StepWorkspace, pos: torch.Tensor, pos_offset_floats: int, p
 
 
 @dataclass
+class CsrGraph:
+    """A static receiver-sorted CSR graph over n nodes (int32, on the GPU)."""
+    rowptr: torch.Tensor   # [n+1]
+    send: torch.Tensor     # [max(E,1)]
+    recv: torch.Tensor     # [max(E,1)]
+    n: int
+    num_edges: int
+
+    @property
+    def edge_cap(self) -> int:
+        return max(1, self.num_edges)
+
+    @property
+    def ntiles(self) -> int:
+        return (self.edge_cap + 31) // 32
+
+    def edge_index(self) -> torch.Tensor:
+        """[2, E] int64 = [senders; receivers] in CSR order."""
+        e = self.num_edges
+        return torch.stack([self.send[:e], self.recv[:e]]).to(torch.int64)
+
+
+def coo_to_csr(edge_index: torch.Tensor, n: int) -> CsrGraph:
+    """edge_index [2, E] (row 0 senders, row 1 receivers, PyG source_to_target)
+    -> stable receiver-sorted CSR through sgnn_coo_to_csr.  Index range is
+    checked here (one host sync: static graphs are built once)."""
+    if edge_index.dim() != 2 or edge_index.shape[0] != 2:
+        raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+    require = _hip.require_gpu_tensor
+    require(edge_index, "edge_index")
+    ei = edge_index.to(torch.int64).contiguous()
+    E = int(ei.shape[1])
+    dev = ei.device
+    if E > 0:
+        lo, hi = int(ei.min().item()), int(ei.max().item())
+        if lo < 0 or hi >= n:
+            raise ValueError(f"edge_index values must lie in [0, {n}), got [{lo}, {hi}]")
+    L = lib()
+    ws = torch.empty(int(L.sgnn_coo_workspace_bytes(n, E)) + 256, dtype=torch.uint8, device=dev)
+    rowptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    send = torch.zeros(max(E, 1), dtype=torch.int32, device=dev)
+    recv = torch.zeros(max(E, 1), dtype=torch.int32, device=dev)
+    src, dst = ei[0].contiguous(), ei[1].contiguous()
+    check(L.sgnn_coo_to_csr(src.data_ptr() if E else None, dst.data_ptr() if E else None, E, n,
+                            (ws.data_ptr() + 255) & ~255, rowptr.data_ptr(), send.data_ptr(),
+                            recv.data_ptr(), stream_ptr(dev)), "sgnn_coo_to_csr")
+    return CsrGraph(rowptr, send, recv, n, E)
+
+
+def radius_graph_csr(pos: torch.Tensor, radius: float, K: int, loop: bool,
+                     counts: Optional[Sequence[int]] = None) -> CsrGraph:
+    """torch_cluster radius_graph(pos, r, batch, loop, max_num_neighbors=K) as a
+    CSR graph sized to its edge count (one host sync: for static graphs)."""
+    _hip.require_gpu_tensor(pos, "positions")
+    p = pos.to(torch.float32).contiguous()
+    n, d = p.shape
+    dev = p.device
+    counts = [n] if counts is None else list(counts)
+    ex_ptr = ex_ptr_tensor(counts, dev)
+    L = lib()
+    cap = max(1, n * (K + (0 if loop else 1)))
+    ws = torch.empty(int(L.sgnn_radius_workspace_bytes(n, K, int(loop))) + 256, dtype=torch.uint8,
+                     device=dev)
+    rowptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    send = torch.empty(cap, dtype=torch.int32, device=dev)
+    recv = torch.empty(cap, dtype=torch.int32, device=dev)
+    check(L.sgnn_radius_graph(p.data_ptr(), d, n, d, ex_ptr.data_ptr(), len(counts), float(radius),
+                              K, int(loop), (ws.data_ptr() + 255) & ~255, rowptr.data_ptr(),
+                              send.data_ptr(), recv.data_ptr(), cap, stream_ptr(dev)),
+          "sgnn_radius_graph")
+    E = int(rowptr[n].item())
+    return CsrGraph(rowptr, send[:max(E, 1)].clone(), recv[:max(E, 1)].clone(), n, E)
+
+
+@dataclass
 class StepInputs:
     pos_seq: torch.Tensor           # [n, T, dim] fp32 contiguous, GPU
     ex_ptr: torch.Tensor            # [n_ex+1] int64, GPU
@@ -167,7 +244,7 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
     emb_dim = emb_weight.shape[1] if (use_emb and emb_weight is not None) else 0
     check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, _ptr(inp.types) if use_emb else 0,
                               _ptr(emb_weight) if use_emb else 0, emb_dim, int(use_emb),
-                              inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius),
+                              inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius), 1.0,
                               ctypes.byref(pk.enc_node), ctypes.byref(pk.edge[0]),
                               ws.x_a.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), None, s),
           "sgnn_encode_nodes")

@@ -245,7 +245,7 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
     engine.radius_graph(ws, pos, (T - 1) * d, T * d, inp.ex_ptr, inp.n_ex, radius)
     sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd)
     check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, 0, 0, 0, 0, inp.vel_mean.data_ptr(),
-                              inp.vel_std.data_ptr(), float(radius), ctypes.byref(pk.enc_node),
+                              inp.vel_std.data_ptr(), float(radius), 1.0, ctypes.byref(pk.enc_node),
                               ctypes.byref(pk.edge[0]), tw.xs[0].data_ptr(), ws.u.data_ptr(),
                               ws.v.data_ptr(), ctypes.byref(sv), s), "sgnn_encode_nodes")
     sv = _saves(yhat=tw.ee_yh, rstd=tw.ee_rstd)

@@ -244,9 +244,71 @@ def train_case(name, seed=0):
 
 
 from sgnn import noise_utils as ref_noise  # noqa: E402
+from sgnn.multi_scale.multi_scale_graph import MultiScaleConfig as RefMSConfig  # noqa: E402
+from sgnn.multi_scale.multi_scale_graph import MultiScaleGraph as RefMSGraph  # noqa: E402
+from sgnn.multi_scale.multi_scale_simulator import MultiScaleSimulator as RefMSSim  # noqa: E402
+from sgnn.multi_scale import multi_scale_evaluate as ref_ms_eval  # noqa: E402
 
 
-def main():
+def multi_scale_case(name, base, nframes, T, H, L, num_scales, window, mult, ntypes=1, emb=9,
+                     nmlp=2, seed=0, traj_seed=0, rollout_steps=0):
+    """MultiScaleSimulator forward (+ rollout) exactly as the reference runs it:
+    static graph from the exact initial lattice (static_graph_data_loader.py:96-106),
+    then predict_positions on the trajectory window (multi_scale_simulator.py:281-326)."""
+    dim = base.shape[1]
+    seq = synthetic.trajectory(base, nframes, seed=traj_seed)
+    st = synthetic.normalization_stats(dim)
+    norm = {k: {kk: torch.tensor(vv) for kk, vv in v.items()} for k, v in st.items()}
+    torch.manual_seed(seed)
+    nnode_in = (T - 1) * dim + 1 + (emb if ntypes > 1 else 0)
+    sim = RefMSSim(kinematic_dimensions=dim, nnode_in=nnode_in, nedge_in=dim + 1, nedge_out=H,
+                   latent_dim=H, nmessage_passing_steps=L, nmlp_layers=nmlp, normalization_stats=norm,
+                   nparticle_types=ntypes, particle_type_embedding_size=emb, num_scales=num_scales,
+                   window_size=window, radius_multiplier=mult, device="cpu")
+    sim.eval()
+    graph = RefMSGraph(RefMSConfig(num_scales=num_scales, window_size=window, radius_multiplier=mult)
+                       ).create_all_edges(torch.tensor(seq[:, 0]))
+    sim.set_static_graph(graph)
+    types_ = np.random.default_rng(seed + 1).integers(0, ntypes, seq.shape[0]).astype(np.int64)
+    pt = torch.tensor(types_)
+    pos = torch.tensor(seq[:, :T])
+    out = {"hp_dim": np.int64(dim), "hp_T": np.int64(T), "hp_H": np.int64(H), "hp_L": np.int64(L),
+           "hp_ntypes": np.int64(ntypes), "hp_emb": np.int64(emb), "hp_nmlp": np.int64(nmlp),
+           "hp_num_scales": np.int64(num_scales), "hp_window": np.int64(window),
+           "hp_mult": np.float32(mult), **stats_arrays(st), **sd_arrays(sim),
+           "positions": seq, "particle_types": types_,
+           "g2m": graph["grid2mesh_edges"].numpy(), "m2m": graph["mesh2mesh_edges"].numpy(),
+           "m2g": graph["mesh2grid_edges"].numpy()}
+    for s_, d_ in graph["graph_hierarchy"].items():
+        out[f"scale{s_}_indices"] = d_["sampling_indices"].numpy()
+        out[f"scale{s_}_spacing"] = np.float32(d_["spacing"])
+    with torch.no_grad():
+        nf, ei, ef = sim._encoder_preprocessor(pos, torch.tensor([seq.shape[0]]), pt)
+        out["node_features"] = nf.numpy()
+        for k in ("g2m", "m2m", "m2g"):
+            out[f"ef_{k}"] = ef[k].numpy()
+        gnn = sim._multi_scale_gnn
+        out["pred"] = gnn(nf, ei["g2m"], ef["g2m"], ei["m2m"], ef["m2m"], ei["m2g"], ef["m2g"],
+                          graph["graph_hierarchy"]).numpy()
+        nxt, strain = sim.predict_positions(pos, torch.tensor([seq.shape[0]]), pt)
+        out["next_position"], out["strain"] = nxt.numpy(), strain.numpy()
+        if rollout_steps:
+            strains = torch.zeros(nframes, seq.shape[0])
+            ro = ref_ms_eval.evaluate_multi_scale_rollout(
+                sim, torch.tensor(seq), pt, torch.tensor([seq.shape[0]]), strains, nsteps=rollout_steps,
+                dim=dim, device="cpu", input_sequence_length=T)
+            out["rollout_predicted"] = ro["predicted_rollout"]
+            out["rollout_strain"] = ro["predicted_strain"]
+            out["rollout_rmse_position"] = ro["rmse_position"]
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: N={seq.shape[0]} g2m={out['g2m'].shape[1]} m2m={out['m2m'].shape[1]} "
+          f"m2g={out['m2g'].shape[1]} -> {os.path.getsize(path)/1e3:.0f} KB")
+
+
+def main(only=None):
+    if only == "ms":
+        return main_ms()
     T = 11
     # 1) tiny 2D, reference default radius 0.6, per-layer latents + 3-step rollout
     seq = synthetic.trajectory(synthetic.lattice_2d(10, 8), T + 3, seed=1)
@@ -271,7 +333,20 @@ def main():
     forward_case("tiny3d_h128", seq, [seq.shape[0]], np.zeros(seq.shape[0]), 3, 6, 128, 3, 0.75)
     # 7) one training step (loss, grads, Adam update)
     train_case("train2d_r06")
+    # 8-9) multi-scale cases
+    main_ms()
+
+
+def main_ms():
+    # multi-scale 2D: 3 scales (grid + 2 meshes), nmlp_layers 2, wall feature active
+    # (x starts at -1.75 so x+2 spans the clamp range)
+    multi_scale_case("ms2d_s3", synthetic.lattice_2d(20, 14, x0=-1.75), 9, 6, 64, 3, 3, 2, 2.0,
+                     seed=3, traj_seed=8, rollout_steps=3)
+    # multi-scale 3D, H=128 (config-5 widths), 2 scales, particle types (embedding);
+    # 27 lattice neighbours inside r, so the max_neighbors=24 truncation binds
+    multi_scale_case("ms3d_h128", synthetic.lattice_3d(8, 6, 5, x0=-1.75), 6, 6, 128, 2, 2, 2, 2.0,
+                     ntypes=2, seed=4, traj_seed=9)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

@@ -72,3 +72,37 @@ def test_reference_input_validation():
         sim.predict_positions(torch.zeros(5, 1, 2), [5], torch.zeros(5, dtype=torch.long))
     with pytest.raises(ValueError, match="2D positions"):
         sim._compute_graph_connectivity(torch.zeros(5, 1, 2), [5], 0.6)
+
+
+@pytest.mark.parametrize("case,seed", [("ms2d_s3", 3), ("ms3d_h128", 4)])
+def test_multi_scale_state_dict_and_init_match_reference(case, seed):
+    """MultiScaleSimulator: same keys, same construction order => same init."""
+    from sgnn_amd.multi_scale import MultiScaleSimulator
+    z = golden(case)
+    hp = hparams(z)
+    d, T, H = hp["dim"], hp["T"], hp["H"]
+    torch.manual_seed(seed)
+    nnode_in = (T - 1) * d + 1 + (hp["emb"] if hp["ntypes"] > 1 else 0)
+    sim = MultiScaleSimulator(d, nnode_in, d + 1, H, H, hp["L"], hp["nmlp"], stats_of(z), hp["ntypes"],
+                              hp["emb"], hp["num_scales"], hp["window"], hp["mult"])
+    sd = sim.state_dict()
+    ref_keys = sorted(k[2:] for k in z.files if k.startswith("w/"))
+    assert sorted(sd.keys()) == ref_keys
+    for k in ref_keys:
+        np.testing.assert_array_equal(sd[k].numpy(), z["w/" + k], err_msg=k)
+
+
+def test_multi_scale_validation():
+    from sgnn_amd.multi_scale import MultiScaleConfig, MultiScaleSimulator
+    with pytest.raises(ValueError, match="num_scales"):
+        MultiScaleConfig(num_scales=1)
+    z = golden("ms2d_s3")
+    hp = hparams(z)
+    sim = MultiScaleSimulator(2, 11, 3, 64, 64, 1, 2, stats_of(z), 1, 9, 3, 2, 2.0)
+    with pytest.raises(ValueError, match="Static graph data not set"):
+        sim._validate_static_graph()
+    sim.set_static_graph({"graph_hierarchy": {}})
+    with pytest.raises(ValueError, match="Missing required graph data key"):
+        sim._validate_static_graph()
+    with pytest.raises(ValueError, match="GPU"):
+        sim.predict_positions(torch.zeros(5, 6, 2), [5], None)

@@ -1,0 +1,136 @@
+"""GPU parity for the multi-scale path: the HIP
+chain through the C-ABI against the reference's golden outputs and the
+multi-scale oracle.  Tolerances as tests/test_gpu_parity.py (fp32, different
+summation order than MKL / PyG): |got - ref| <= 2e-4 + 1e-4 |ref| on the
+normalised prediction, the same bound x acc_std on positions; graphs and
+CSR conversions bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import MS_CASES, golden, hparams, ms_graph_of, ms_oracle_sim, ms_product_sim
+from tests.test_gpu_parity import ATOL, _close
+
+pytestmark = pytest.mark.gpu
+
+
+def _stable_csr(ei: np.ndarray, n: int):
+    order = np.argsort(ei[1], kind="stable")
+    rowptr = np.zeros(n + 1, np.int64)
+    np.add.at(rowptr, ei[1] + 1, 1)
+    return np.cumsum(rowptr), ei[0][order], ei[1][order]
+
+
+def test_coo_to_csr_stable_bit_exact():
+    from sgnn_amd import engine
+    rng = np.random.default_rng(0)
+    for n, E in [(1, 0), (7, 1), (300, 5000), (1000, 37), (64, 4000)]:
+        ei = np.stack([rng.integers(0, n, E), rng.integers(0, n, E)]).astype(np.int64)
+        g = engine.coo_to_csr(torch.from_numpy(ei).cuda(), n)
+        rp, s, r = _stable_csr(ei, n)
+        assert g.num_edges == E
+        np.testing.assert_array_equal(g.rowptr.cpu().numpy(), rp)
+        np.testing.assert_array_equal(g.send[:E].cpu().numpy(), s)
+        np.testing.assert_array_equal(g.recv[:E].cpu().numpy(), r)
+    with pytest.raises(ValueError):
+        engine.coo_to_csr(torch.tensor([[0, 5], [1, 2]]).cuda(), 3)
+
+
+@pytest.mark.parametrize("case", MS_CASES)
+def test_static_graph_on_gpu_bit_exact(case):
+    from sgnn_amd.multi_scale import build_static_multi_scale_graph
+    z = golden(case)
+    hp = hparams(z)
+    g = build_static_multi_scale_graph(torch.from_numpy(z["positions"][:, 0]).cuda(), hp["num_scales"],
+                                       hp["window"], hp["mult"])
+    for s in range(hp["num_scales"]):
+        np.testing.assert_array_equal(g["graph_hierarchy"][s]["sampling_indices"].cpu().numpy(),
+                                      z[f"scale{s}_indices"])
+    for k, key in [("g2m", "grid2mesh_edges"), ("m2m", "mesh2mesh_edges"), ("m2g", "mesh2grid_edges")]:
+        np.testing.assert_array_equal(g[key].cpu().numpy(), z[k], err_msg=k)
+
+
+@pytest.mark.parametrize("case", MS_CASES)
+def test_predict_positions_matches_reference(case):
+    z = golden(case)
+    hp = hparams(z)
+    sim = ms_product_sim(z)
+    pos = torch.from_numpy(z["positions"][:, :hp["T"]]).cuda()
+    types_ = torch.from_numpy(z["particle_types"]).cuda()
+    nxt, strain = sim.predict_positions(pos, [pos.shape[0]], types_)
+    torch.cuda.synchronize()
+    _close(strain.cpu().numpy(), z["strain"], what=f"{case} strain")
+    scale = float(np.max(z["acc_std"]))
+    _close(nxt.cpu().numpy(), z["next_position"], atol=ATOL * scale, rtol=1e-6, what=f"{case} next_pos")
+    with torch.no_grad():
+        pa, ta, ps = sim.predict_accelerations(pos[:, -1], torch.zeros_like(pos), pos, [pos.shape[0]], types_)
+    _close(pa.cpu().numpy(), z["pred"][:, :hp["dim"]], what=f"{case} pred_acc")
+
+
+def test_rollout_matches_reference():
+    from sgnn_amd.multi_scale.multi_scale_evaluate import evaluate_multi_scale_rollout
+    z = golden("ms2d_s3")
+    hp = hparams(z)
+    sim = ms_product_sim(z)
+    pos = torch.from_numpy(z["positions"]).cuda()
+    n = pos.shape[0]
+    out = evaluate_multi_scale_rollout(sim, pos, torch.zeros(n, dtype=torch.long).cuda(), [n],
+                                       torch.zeros(pos.shape[1], n).cuda(), 3, hp["dim"], "cuda", hp["T"])
+    scale = float(np.max(z["acc_std"]))
+    _close(out["predicted_rollout"], z["rollout_predicted"], atol=3 * ATOL * scale, rtol=1e-6,
+           what="ms rollout positions")
+    _close(out["predicted_strain"], z["rollout_strain"], atol=3 * ATOL, what="ms rollout strain")
+
+
+@pytest.mark.parametrize("dims,case", [((60, 40), "ms2d_s3"), ((20, 16, 12), "ms3d_h128")])
+def test_larger_against_oracle(dims, case):
+    """Bigger lattices than the fixtures (graph built on the GPU, checked against
+    the oracle's graph first), prediction vs the oracle."""
+    from oracle import multi_scale_oracle as MO
+    from sgnn_amd import synthetic
+    from sgnn_amd.multi_scale import build_static_multi_scale_graph
+    z = golden(case)
+    hp = hparams(z)
+    base = (synthetic.lattice_2d(*dims, x0=-1.75) if len(dims) == 2
+            else synthetic.lattice_3d(*dims, x0=-1.75))
+    seq = synthetic.trajectory(base, hp["T"], seed=41)
+    g_ref = MO.create_all_edges(torch.from_numpy(seq[:, 0]), hp["num_scales"], hp["window"], hp["mult"])
+    g = build_static_multi_scale_graph(torch.from_numpy(seq[:, 0]).cuda(), hp["num_scales"], hp["window"],
+                                       hp["mult"])
+    for key in ("grid2mesh_edges", "mesh2mesh_edges", "mesh2grid_edges"):
+        np.testing.assert_array_equal(g[key].cpu().numpy(), g_ref[key].numpy(), err_msg=key)
+    n = seq.shape[0]
+    types_ = torch.from_numpy(np.random.default_rng(2).integers(0, hp["ntypes"], n))
+    sim = ms_product_sim(z)
+    sim.set_static_graph(g)
+    osim = ms_oracle_sim(z, g_ref)
+    pos = torch.from_numpy(seq)
+    ref_next, ref_strain = osim.predict_positions(pos, types_)
+    nxt, strain = sim.predict_positions(pos.cuda(), [n], types_.cuda())
+    _close(strain.cpu().numpy(), ref_strain.numpy(), what=f"{dims} strain")
+    _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * float(np.max(z["acc_std"])), rtol=1e-6,
+           what=f"{dims} next_pos")
+
+
+def test_high_degree_user_graph_against_oracle():
+    """A user-supplied static graph whose receivers have up to 100 incoming
+    edges (segments spanning several 32-edge tiles) and nodes with none."""
+    z = golden("ms2d_s3")
+    hp = hparams(z)
+    n = z["positions"].shape[0]
+    rng = np.random.default_rng(9)
+    graph = ms_graph_of(z)
+    hubs = np.repeat(np.arange(0, 40, 4), 100)          # 10 receivers x 100 edges
+    extra = np.stack([rng.integers(0, n, hubs.size), hubs]).astype(np.int64)
+    m2m = np.concatenate([z["m2m"], extra], 1)
+    m2m = m2m[:, rng.permutation(m2m.shape[1])]
+    graph["mesh2mesh_edges"] = torch.from_numpy(m2m)
+    osim = ms_oracle_sim(z, graph)
+    sim = ms_product_sim(z)
+    sim.set_static_graph({k: (v.cuda() if isinstance(v, torch.Tensor) else v) for k, v in graph.items()})
+    pos = torch.from_numpy(z["positions"][:, :hp["T"]])
+    ref_next, ref_strain = osim.predict_positions(pos, None)
+    nxt, strain = sim.predict_positions(pos.cuda(), [n], None)
+    _close(strain.cpu().numpy(), ref_strain.numpy(), what="high-degree strain")
+    _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * float(np.max(z["acc_std"])), rtol=1e-6,
+           what="high-degree next_pos")
