@@ -52,6 +52,8 @@ typedef struct sgnn_saves {
   float* rstd;  /* LayerNorm 1/std per item */
   float* agg;   /* node layers: resolved aggregate [N][H] */
   float* hd;    /* node_layer_decode: decoder hidden [N][H] */
+  float* h2;    /* nlin = 3: post-ReLU hidden of the middle Linear */
+  float* hd2;   /* node_layer_decode, nlin = 3: decoder second hidden [N][H] */
 } sgnn_saves;
 
 const char* sgnn_version(void);
@@ -166,19 +168,25 @@ int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin
  *   sgnn_encode_nodes_bwd(g), sgnn_encode_edges_bwd(dE0)
  *   sgnn_reduce_slabs                     -> parameter gradients
  * Each *_bwd launches `nslab` persistent workgroups and writes one partial
- * slab of sgnn_bwd_slab_floats(kind, H, feat) floats per workgroup.  Slab
- * layouts (row-major, W = 4 waves per workgroup, vectors as W partial rows):
- *   EDGE    : dW2[H][H] | dW1e[H][H] (x 2^k in the reduce) | db2, dgamma, dbeta [W][H]
- *   NODE    : dW2[H][H] | dW1[H][2H] | db1, db2, dgamma, dbeta [W][H]
+ * slab of sgnn_bwd_slab_floats(kind, H, feat, nlin) floats per workgroup.
+ * Slab layouts (row-major, W = 4 waves per workgroup, vectors as W partial
+ * rows; Wl = last Linear, Wm = middle Linear (nlin = 3 only, appended), W1 =
+ * first):
+ *   EDGE    : dWl[H][H] | dW1e[H][H] (x 2^k in the reduce) | dWm |
+ *             dbl, dgamma, dbeta [W][H] | dbm
+ *   NODE    : dWl[H][H] | dW1[H][2H] | dWm | db1, dbl, dgamma, dbeta [W][H] | dbm
  *   UV      : dW1[:, 0:2H] as [H][2H] | db1 [W][H]
- *   DECODER : dW2[32][H] (rows > dim zero) | dW1[H][H] | db2 [W][32] | db1 [W][H] |
- *             loss [W][8] = (total, x, y, z, strain) sums of squared errors
- *   ENC_NODE: dW2[H][H] | dW1[H][32*ceil(F/32)] | db1, db2, dgamma, dbeta [W][H]
- *   ENC_EDGE: dW2[H][H] | dW1[H][32] | db1, db2, dgamma, dbeta [W][H]
+ *   DECODER : dWl[32][H] (rows > dim zero) | dW1[H][H] | dWm | dbl [W][32] |
+ *             db1 [W][H] | loss [W][8] = (total, x, y, z, strain) sums of
+ *             squared errors | dbm [W][H]
+ *   ENC_NODE: dWl[H][H] | dW1[H][32*ceil(F/32)] | dWm | db1, dbl, dgamma, dbeta [W][H] | dbm
+ *   ENC_EDGE: dWl[H][H] | dW1[H][32] | dWm | db1, dbl, dgamma, dbeta [W][H] | dbm
+ * Hidden 64 or 128, nlin 2 or 3 (nmlp_layers 1 or 2).  Saved activations come
+ * through struct sgnn_saves as the training forward wrote them.
  * ------------------------------------------------------------------------- */
 enum { SGNN_SLAB_EDGE = 0, SGNN_SLAB_NODE = 1, SGNN_SLAB_UV = 2, SGNN_SLAB_DECODER = 3,
        SGNN_SLAB_ENC_NODE = 4, SGNN_SLAB_ENC_EDGE = 5 };
-int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat);
+int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat, int32_t nlin);
 
 /* out[r*dst_ld + c] (+)= scale * sum_{g<nslab} sum_{q<nrep}
  *                         src[g*slab_stride + offset + q*rep_stride + r*src_ld + c] */
@@ -199,19 +207,20 @@ int sgnn_transpose_csr(const int32_t* rowptr, const int32_t* send, int64_t n, in
 
 /* dpred != NULL: use it as dL/dpred [n][dim+1] (autograd path) instead of the
  * fused loss gradient 2*w*(pred - target)*inv_count of train.py:257-268. */
+/* saves: hd (+ hd2 for nlin 3) as node_layer_decode wrote them. */
 int sgnn_decoder_loss_bwd(const float* pred, const float* pos_seq, const float* next_pos,
                           const float* noise, const float* next_strain, const float* acc_mean,
                           const float* acc_std, int64_t n, int32_t T, int32_t dim, float w_pos,
                           float w_strain, float inv_count, const float* dpred,
-                          const float* hd_save, const float* x_last, const sgnn_mlp* decoder,
+                          const sgnn_saves* saves, const float* x_last, const sgnn_mlp* decoder,
                           float* g, float* slab, int32_t nslab, void* stream);
-int sgnn_node_layer_bwd(const float* g, int64_t n, const float* yhat_save,
-                        const float* rstd_save, const float* h_save, const float* agg_save,
-                        const float* x_in, const sgnn_mlp* node_fn, float* dagg, float* dxp,
-                        float* slab, int32_t nslab, void* stream);
+/* saves: yhat, rstd, h, agg (+ h2) as node_layer wrote them. */
+int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* saves, const float* x_in,
+                        const sgnn_mlp* node_fn, float* dagg, float* dxp, float* slab,
+                        int32_t nslab, void* stream);
+/* saves: h, yhat, rstd (+ h2) as edge_layer wrote them. */
 int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t* send,
-                        const int32_t* recv, int64_t n, const float* h_save,
-                        const float* yhat_save, const float* rstd_save, const float* e0t,
+                        const int32_t* recv, int64_t n, const sgnn_saves* saves, const float* e0t,
                         float e_scale, const sgnn_mlp* edge_fn, float* du, float* cin,
                         float* cout, float* dh_rows, float* de0t, int32_t de0_accumulate,
                         float* slab, int32_t nslab, void* stream);
@@ -219,15 +228,17 @@ int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, const float
                 const int32_t* rowptr, const float* dh_rows, const int32_t* tptr,
                 const int32_t* tperm, const float* x_in, int64_t n, const sgnn_mlp* edge_fn,
                 float* g, float* slab, int32_t nslab, void* stream);
+/* Wall feature as sgnn_encode_nodes: clamp(x + 2, 0, wall_max) / wall_div.
+ * saves: h, yhat, rstd (+ h2). */
 int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
-                          int32_t dim, const float* vel_mean, const float* vel_std, float radius,
-                          const float* h_save, const float* yhat_save, const float* rstd_save,
+                          int32_t dim, const float* vel_mean, const float* vel_std,
+                          float wall_max, float wall_div, const sgnn_saves* saves,
                           const sgnn_mlp* enc, float* slab, int32_t nslab, void* stream);
+/* saves: yhat, rstd (+ h2); the first hidden is recomputed. */
 int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_stride, int32_t dim,
                           float radius, const int32_t* rowptr, const int32_t* send,
-                          const int32_t* recv, int64_t n, const float* yhat_save,
-                          const float* rstd_save, const sgnn_mlp* enc, float* slab,
-                          int32_t nslab, void* stream);
+                          const int32_t* recv, int64_t n, const sgnn_saves* saves,
+                          const sgnn_mlp* enc, float* slab, int32_t nslab, void* stream);
 
 /* Fused Adam over a flat fp32 buffer; same update as torch.optim.Adam
  * (amsgrad=False, weight_decay=0) used by train.py:199,271-273. step >= 1. */

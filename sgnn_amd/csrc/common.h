@@ -19,6 +19,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define SGNN_DEV __device__ __forceinline__
+#define SGNN_HOST_DEV __host__ __device__
 
 SGNN_DEV int lane_id() { return threadIdx.x & 63; }
 
@@ -344,11 +345,12 @@ SGNN_DEV void stage_matrix_t(float* lds, int ld, const float* g, int ldg, int ro
 
 // Tail of an MLP after its first ReLU: y = LAST(relu(MID(h))) for 3 Linear
 // layers (nmlp_layers = 2), y = LAST(h) for 2 (nmlp_layers = 1).
+// h2 receives the second hidden (NL = 3; untouched for NL = 2) for the
+// training saves.
 template <int TH, int NL, int TO>
-SGNN_DEV void mlp_tail(f32x16 (&y)[TO], const f32x16 (&h)[TH], const float* Wm, int ldm,
-                       const float* bm_lds, const float* Wl, int ldl, const float* bl_lds) {
+SGNN_DEV void mlp_tail(f32x16 (&y)[TO], f32x16 (&h2)[TH], const f32x16 (&h)[TH], const float* Wm,
+                       int ldm, const float* bm_lds, const float* Wl, int ldl, const float* bl_lds) {
   if constexpr (NL == 3) {
-    f32x16 h2[TH];
     acc_bias<TH>(h2, bm_lds);
     mfma_from_acc<TH, TH>(h2, Wm, ldm, 0, h);
     acc_relu<TH>(h2);
@@ -358,4 +360,11 @@ SGNN_DEV void mlp_tail(f32x16 (&y)[TO], const f32x16 (&h)[TH], const float* Wm, 
     acc_bias<TO>(y, bl_lds);
     mfma_from_acc<TO, TH>(y, Wl, ldl, 0, h);
   }
+}
+
+template <int TH, int NL, int TO>
+SGNN_DEV void mlp_tail(f32x16 (&y)[TO], const f32x16 (&h)[TH], const float* Wm, int ldm,
+                       const float* bm_lds, const float* Wl, int ldl, const float* bl_lds) {
+  f32x16 h2[TH];
+  mlp_tail<TH, NL, TO>(y, h2, h, Wm, ldm, bm_lds, Wl, ldl, bl_lds);
 }

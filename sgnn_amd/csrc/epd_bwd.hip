@@ -167,6 +167,146 @@ SGNN_DEV void store_lane_vec(float* dst, const float (&acc)[TH / 2 > 0 ? TH / 2 
 }
 
 #define LANEVEC(name) float name[TH / 2 > 0 ? TH / 2 : 1] = {}
+template <int TH>
+using LaneVec = float[TH / 2 > 0 ? TH / 2 : 1];
+
+// acc[t][u] += sum_k W[k][u] x[k]: the input gradient of a Linear layer
+// (dIn = W^T dOut).  LDS mode (GW = false): w is a staged W^T image [u][k]
+// with leading dim ld.  Global mode (GW, H = 128 where the images do not fit
+// next to the item buffers): w is the row-major torch weight [k][u] itself
+// (ld = its row length), read transposed from L2 — consecutive lanes read
+// consecutive u, so every load is two 128-B segments.
+template <int TH, int TK, bool GW>
+SGNN_DEV void matvec_t(f32x16 (&acc)[TH], const float* w, int ld, const f32x16 (&x)[TK]) {
+  if constexpr (!GW) {
+    mfma_from_acc<TH, TK>(acc, w, ld, 0, x);
+  } else {
+    const int l = lane_id() & 31, h = lane_id() >> 5;
+#pragma unroll
+    for (int tk = 0; tk < TK; ++tk)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float* row = w + (int64_t)(32 * tk + 8 * g + 4 * h + c) * ld + l;
+          float wv[TH];
+#pragma unroll
+          for (int t = 0; t < TH; ++t) wv[t] = row[32 * t];
+#pragma unroll
+          for (int t = 0; t < TH; ++t) acc[t] = mfma32(wv[t], x[tk][4 * g + c], acc[t]);
+        }
+  }
+}
+
+// Per-wave item images in LDS: the workgroup's [128 items][units] operands of
+// the weight-gradient outer products.
+struct Imgs {
+  float *bufA, *bufB, *sA, *sB;
+  int lda, ldb, j;
+};
+
+SGNN_DEV Imgs make_imgs(float* bufA, int lda, float* bufB, int ldb) {
+  const int w = threadIdx.x >> 6;
+  return Imgs{bufA, bufB, bufA + w * 32 * lda, bufB + w * 32 * ldb, lda, ldb, lane_id() & 31};
+}
+
+template <int TH>
+SGNN_DEV void relu_mask(f32x16 (&d)[TH], const f32x16 (&act)[TH], bool valid) {
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) d[t][r] = (valid && act[t][r] > 0.0f) ? d[t][r] : 0.0f;
+}
+
+// Backward of one hidden Linear + the ReLU in front of it:
+//   dW += dy (x) act, db += dy, dact = (W^T dy) * [act > 0]
+// (act = post-ReLU input of the layer, zeroed for invalid items).
+template <int TH, bool GW, int NT>
+SGNN_DEV void hidden_linear_bwd(const f32x16 (&dy)[TH], const f32x16 (&act)[TH], const float* w,
+                                int ld, bool valid, int nvalid, const Imgs& im, f32x16 (&acc)[NT],
+                                LaneVec<TH>& s_b, f32x16 (&dact)[TH]) {
+  lds_store_items<TH>(im.sA, im.lda, im.j, dy);
+  lds_store_items<TH>(im.sB, im.ldb, im.j, act);
+  wave_lds_sync();
+  lane_sums<TH>(s_b, im.sA, im.lda, nvalid);
+  __syncthreads();
+  outer_tiles<NT>(acc, TH, TH, im.bufA, im.lda, 0, im.bufB, im.ldb, 0);
+  __syncthreads();
+  zero<TH>(dact);
+  matvec_t<TH, TH, GW>(dact, w, ld, dy);
+  relu_mask<TH>(dact, act, valid);
+}
+
+// Backward of LN(LAST(relu(MID(h1)))) (NL = 3) or LN(LAST(h1)) (NL = 2)
+// from dm = dL/d(LN output): LayerNorm affine sums, last (+ middle) Linear
+// weight/bias gradients, and dh1 = dL/d(pre-ReLU first hidden).
+template <int TH, int NL, bool GW, int NT>
+SGNN_DEV void ln_mlp_tail_bwd(const f32x16 (&dm_in)[TH], const f32x16 (&yh_in)[TH], float rs,
+                              const float* gam, const f32x16 (&h1)[TH], const f32x16 (&h2)[TH],
+                              const float* wl, int ldl, const float* wm, int ldm, bool valid,
+                              int nvalid, const Imgs& im, f32x16 (&acc_wl)[NT],
+                              f32x16 (&acc_wm)[NT], LaneVec<TH>& s_db, LaneVec<TH>& s_dg,
+                              LaneVec<TH>& s_dbl, LaneVec<TH>& s_dbm, f32x16 (&dh1)[TH]) {
+  f32x16 dm[TH], dy[TH];
+#pragma unroll
+  for (int t = 0; t < TH; ++t) dm[t] = dm_in[t];
+  zero_if<TH>(dm, !valid);
+  acc_layernorm_bwd<TH>(dm, yh_in, rs, gam, dy);
+  zero_if<TH>(dy, !valid);
+  {
+    // d beta = sum dm, d gamma = sum dm * yhat (graph_network.py:148 LayerNorm)
+    f32x16 t2[TH];
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t2[t][r] = valid ? yh_in[t][r] * dm[t][r] : 0.0f;
+    lds_store_items<TH>(im.sA, im.lda, im.j, dm);
+    lds_store_items<TH>(im.sB, im.ldb, im.j, t2);
+    wave_lds_sync();
+    lane_sums<TH>(s_db, im.sA, im.lda, nvalid);
+    lane_sums<TH>(s_dg, im.sB, im.ldb, nvalid);
+    wave_lds_sync();
+  }
+  if constexpr (NL == 3) {
+    f32x16 d2[TH];
+    hidden_linear_bwd<TH, GW, NT>(dy, h2, wl, ldl, valid, nvalid, im, acc_wl, s_dbl, d2);
+    hidden_linear_bwd<TH, GW, NT>(d2, h1, wm, ldm, valid, nvalid, im, acc_wm, s_dbm, dh1);
+  } else {
+    hidden_linear_bwd<TH, GW, NT>(dy, h1, wl, ldl, valid, nvalid, im, acc_wl, s_dbl, dh1);
+  }
+}
+
+// Slab layouts (floats; W = kWaves partial rows per vector).  Matrices first,
+// then vectors; kept in sync with training.py's reduction table.
+struct SlabLayout {
+  int64_t total, vb;
+};
+
+SGNN_HOST_DEV inline int64_t slab_nmat_floats(int kind, int64_t H, int64_t fpad, int nl) {
+  const int64_t mid = nl == 3 ? H * H : 0;
+  switch (kind) {
+    case SGNN_SLAB_EDGE: return 2 * H * H + mid;            // dWl | dW1e | dWm
+    case SGNN_SLAB_NODE: return 3 * H * H + mid;            // dWl | dW1[H][2H] | dWm
+    case SGNN_SLAB_UV: return 2 * H * H;                    // dW1[H][2H] (i | j)
+    case SGNN_SLAB_DECODER: return 32 * H + H * H + mid;    // dWl[32][H] | dW1 | dWm
+    case SGNN_SLAB_ENC_NODE: return H * H + H * fpad + mid; // dWl | dW1[H][fpad] | dWm
+    case SGNN_SLAB_ENC_EDGE: return H * H + H * 32 + mid;   // dWl | dW1[H][32] | dWm
+    default: return -1;
+  }
+}
+
+SGNN_HOST_DEV inline int64_t slab_nvec_floats(int kind, int64_t H, int nl) {
+  const int64_t W = kWaves, mid = nl == 3 ? W * H : 0;
+  switch (kind) {
+    case SGNN_SLAB_EDGE: return 3 * W * H + mid;                  // dbl dg db | dbm
+    case SGNN_SLAB_NODE: return 4 * W * H + mid;                  // db1 dbl dg db | dbm
+    case SGNN_SLAB_UV: return W * H;                              // db1
+    case SGNN_SLAB_DECODER: return W * 32 + W * H + W * 8 + mid;  // dbl[32] db1 loss[8] | dbm
+    case SGNN_SLAB_ENC_NODE:
+    case SGNN_SLAB_ENC_EDGE: return 4 * W * H + mid;              // db1 dbl dg db | dbm
+    default: return -1;
+  }
+}
 
 // ===========================================================================
 // Edge layer backward
@@ -174,36 +314,52 @@ struct EdgeBwdArgs {
   const float* dagg;
   const int32_t *rowptr, *send, *recv;
   int64_t n;
-  const float *hs, *yh, *rstd, *e0t;
+  const float *hs, *hs2, *yh, *rstd, *e0t;
   float e_scale;
-  const float *w2, *we, *gamma;  // we = edge W1 + 2H (ld 3H)
+  const float *wl, *wm, *we, *gamma;  // we = edge W1 + 2H (ld 3H)
   float *du, *cin, *cout, *dh_rows, *de0t;
   int de0_accumulate;
   float* slab;
   int64_t slab_stride;
 };
 
-template <int TH>
+template <int TH, int NL>
 __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
+  constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4;
+  constexpr int ldl = GW ? H : ldh, lde = GW ? 3 * H : ldh;
   extern __shared__ float lds[];
-  float* W2T = lds;
-  float* WeT = W2T + H * ldh;
-  float* gam = WeT + H * ldh;
+  float* p = lds;
+  const float* WlT = a.wl;
+  const float* WmT = a.wm;
+  const float* WeT = a.we;
+  if (!GW) {
+    stage_matrix_t(p, ldh, a.wl, H, H, H, H, H);
+    WlT = p;
+    p += H * ldh;
+    stage_matrix_t(p, ldh, a.we, 3 * H, H, H, H, H);
+    WeT = p;
+    p += H * ldh;
+    if (NL == 3) {
+      stage_matrix_t(p, ldh, a.wm, H, H, H, H, H);
+      WmT = p;
+      p += H * ldh;
+    }
+  }
+  float* gam = p;
   float* bufA = gam + H;
   float* bufB = bufA + kChunk * ldh;
-  stage_matrix_t(W2T, ldh, a.w2, H, H, H, H, H);
-  stage_matrix_t(WeT, ldh, a.we, 3 * H, H, H, H, H);
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
-  float* sA = bufA + w * 32 * ldh;
-  float* sB = bufB + w * 32 * ldh;
+  const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
+  const int j = im.j, w = threadIdx.x >> 6;
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
-  f32x16 acc_w2[NT], acc_w1[NT];
-  zero_acc<NT>(acc_w2);
+  f32x16 acc_wl[NT], acc_wm[NT], acc_w1[NT];
+  zero_acc<NT>(acc_wl);
+  zero_acc<NT>(acc_wm);
   zero_acc<NT>(acc_w1);
-  LANEVEC(s_db2);
+  LANEVEC(s_dbl);
+  LANEVEC(s_dbm);
   LANEVEC(s_dg);
   LANEVEC(s_db);
   const int64_t E = a.rowptr[a.n];
@@ -213,56 +369,34 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
     const int nvalid = clamp_items(E - base);
     const bool valid = e < E;
     const int64_t ec = valid ? e : E - 1;
-    f32x16 dy[TH], hh[TH];
+    f32x16 dm[TH], yh[TH], h1[TH], h2[TH];
+    float rs = 0.0f;
     int rv = 0;
-    if (nvalid > 0) {
+    if (nvalid > 0) {  // tiles past the last valid one are not allocated
       rv = a.recv[ec];
-      f32x16 dm[TH], yh[TH];
       load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
       load_tiled<TH>(yh, a.yh + tile * (32 * H));
-      load_tiled<TH>(hh, a.hs + tile * (32 * H));
-      const float rs = a.rstd[ec];
-      zero_if<TH>(dm, !valid);
-      acc_layernorm_bwd<TH>(dm, yh, rs, gam, dy);
-      zero_if<TH>(dy, !valid);
-      zero_if<TH>(hh, !valid);
-      // d beta = sum dm, d gamma = sum dm * yhat  (graph_network.py:148 LayerNorm)
-#pragma unroll
-      for (int t = 0; t < TH; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];
-      lds_store_items<TH>(sA, ldh, j, dm);
-      lds_store_items<TH>(sB, ldh, j, yh);
-      wave_lds_sync();
-      lane_sums<TH>(s_db, sA, ldh, nvalid);
-      lane_sums<TH>(s_dg, sB, ldh, nvalid);
-      wave_lds_sync();
-      lds_store_items<TH>(sA, ldh, j, dy);
-      lds_store_items<TH>(sB, ldh, j, hh);
-      wave_lds_sync();
-      lane_sums<TH>(s_db2, sA, ldh, nvalid);
+      load_tiled<TH>(h1, a.hs + tile * (32 * H));
+      if (NL == 3) load_tiled<TH>(h2, a.hs2 + tile * (32 * H));
+      rs = a.rstd[ec];
     } else {
-      zero<TH>(dy);
-      zero<TH>(hh);
-      lds_store_items<TH>(sA, ldh, j, dy);
-      lds_store_items<TH>(sB, ldh, j, hh);
+      zero<TH>(dm);
+      zero<TH>(yh);
+      zero<TH>(h1);
+      if (NL == 3) zero<TH>(h2);
     }
-    __syncthreads();
-    outer_tiles<NT>(acc_w2, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW2 = sum dy (x) h
-    __syncthreads();
+    zero_if<TH>(h1, !valid);
+    if (NL == 3) zero_if<TH>(h2, !valid);
     f32x16 dh[TH];
-    zero<TH>(dh);
+    ln_mlp_tail_bwd<TH, NL, GW, NT>(dm, yh, rs, gam, h1, h2, WlT, ldl, WmT, ldl, valid, nvalid, im,
+                                    acc_wl, acc_wm, s_db, s_dg, s_dbl, s_dbm, dh);
+    f32x16 e0[TH];
+    zero<TH>(e0);
     if (nvalid > 0) {
-      mfma_from_acc<TH, TH>(dh, W2T, ldh, 0, dy);  // W2^T dy
-#pragma unroll
-      for (int t = 0; t < TH; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dh[t][r] = hh[t][r] > 0.0f ? dh[t][r] : 0.0f;
-      zero_if<TH>(dh, !valid);
       // dE0 += 2^k W1e^T dh (the edge latent feeding layer k is 2^k e0)
       f32x16 de[TH];
       zero<TH>(de);
-      mfma_from_acc<TH, TH>(de, WeT, ldh, 0, dh);
+      matvec_t<TH, TH, GW>(de, WeT, lde, dh);
       float* dtile = a.de0t + tile * (32 * H);
       if (a.de0_accumulate) {
         f32x16 old[TH];
@@ -279,29 +413,27 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
       }
       store_tiled<TH>(dtile, de);
       if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
-      f32x16 e0[TH];
       load_tiled<TH>(e0, a.e0t + tile * (32 * H));
       zero_if<TH>(e0, !valid);
-      lds_store_items<TH>(sA, ldh, j, dh);
-      lds_store_items<TH>(sB, ldh, j, e0);
-      wave_lds_sync();
-      segment_sum_store<TH>(sA, ldh, rv, nvalid, base, tile, a.rowptr, a.du, a.cin, a.cout);
-    } else {
-      f32x16 z[TH];
-      zero<TH>(z);
-      lds_store_items<TH>(sA, ldh, j, z);
-      lds_store_items<TH>(sB, ldh, j, z);
     }
+    lds_store_items<TH>(im.sA, ldh, j, dh);
+    lds_store_items<TH>(im.sB, ldh, j, e0);
+    wave_lds_sync();
+    if (nvalid > 0)
+      segment_sum_store<TH>(im.sA, ldh, rv, nvalid, base, tile, a.rowptr, a.du, a.cin, a.cout);
     __syncthreads();
     outer_tiles<NT>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1e = sum dh (x) e0
     __syncthreads();
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
-  store_outer<NT>(slab, H, TH, TH, acc_w2);
+  store_outer<NT>(slab, H, TH, TH, acc_wl);
   store_outer<NT>(slab + H * H, H, TH, TH, acc_w1);
-  store_lane_vec<TH>(slab + 2 * H * H, s_db2);
-  store_lane_vec<TH>(slab + 2 * H * H + kWaves * H, s_dg);
-  store_lane_vec<TH>(slab + 2 * H * H + 2 * kWaves * H, s_db);
+  if (NL == 3) store_outer<NT>(slab + 2 * H * H, H, TH, TH, acc_wm);
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, NL);
+  store_lane_vec<TH>(v, s_dbl);
+  store_lane_vec<TH>(v + kWaves * H, s_dg);
+  store_lane_vec<TH>(v + 2 * kWaves * H, s_db);
+  if (NL == 3) store_lane_vec<TH>(v + 3 * kWaves * H, s_dbm);
 }
 
 // ===========================================================================
@@ -309,35 +441,54 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
 struct NodeBwdArgs {
   const float* g;  // dL/dx_out
   int64_t n;
-  const float *yh, *rstd, *hn, *agg, *x;
-  const float *w1, *w2, *gamma;
+  const float *yh, *rstd, *hn, *hn2, *agg, *x;
+  const float *w1, *wl, *wm, *gamma;
   float *dagg, *dxp;
   float* slab;
   int64_t slab_stride;
 };
 
-template <int TH>
+template <int TH, int NL>
 __global__ __launch_bounds__(kBlock) void k_node_bwd(NodeBwdArgs a) {
+  constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4;
+  constexpr int ldl = GW ? H : ldh, ld1 = GW ? 2 * H : ldh;
   extern __shared__ float lds[];
-  float* W2T = lds;                 // [H][ldh]
-  float* W1T = W2T + H * ldh;       // [2H][ldh]: W1T[i][k] = W1[k][i]
-  float* gam = W1T + 2 * H * ldh;
+  float* p = lds;
+  const float* WlT = a.wl;
+  const float* WmT = a.wm;
+  const float* W1T = a.w1;  // W1T[i][k] = W1[k][i], i < 2H
+  if (!GW) {
+    stage_matrix_t(p, ldh, a.wl, H, H, H, H, H);
+    WlT = p;
+    p += H * ldh;
+    stage_matrix_t(p, ldh, a.w1, 2 * H, H, 2 * H, H, 2 * H);
+    W1T = p;
+    p += 2 * H * ldh;
+    if (NL == 3) {
+      stage_matrix_t(p, ldh, a.wm, H, H, H, H, H);
+      WmT = p;
+      p += H * ldh;
+    }
+  }
+  // agg / x halves of W1^T: LDS rows 0..H-1 / H..2H-1; global columns 0.. / H..
+  const float* W1aT = W1T;
+  const float* W1xT = GW ? a.w1 + H : W1T + H * ldh;
+  float* gam = p;
   float* bufA = gam + H;
   float* bufB = bufA + kChunk * ldh;
-  stage_matrix_t(W2T, ldh, a.w2, H, H, H, H, H);
-  stage_matrix_t(W1T, ldh, a.w1, 2 * H, H, 2 * H, H, 2 * H);
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
-  float* sA = bufA + w * 32 * ldh;
-  float* sB = bufB + w * 32 * ldh;
+  const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
+  const int j = im.j, w = threadIdx.x >> 6;
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
-  f32x16 acc_w2[NT], acc_w1a[NT], acc_w1x[NT];
-  zero_acc<NT>(acc_w2);
+  f32x16 acc_wl[NT], acc_wm[NT], acc_w1a[NT], acc_w1x[NT];
+  zero_acc<NT>(acc_wl);
+  zero_acc<NT>(acc_wm);
   zero_acc<NT>(acc_w1a);
   zero_acc<NT>(acc_w1x);
-  LANEVEC(s_db2);
+  LANEVEC(s_dbl);
+  LANEVEC(s_dbm);
   LANEVEC(s_dg);
   LANEVEC(s_db);
   LANEVEC(s_db1);
@@ -347,77 +498,58 @@ __global__ __launch_bounds__(kBlock) void k_node_bwd(NodeBwdArgs a) {
     const int nvalid = clamp_items(a.n - (c * kChunk + w * 32));
     const bool valid = i < a.n;
     const int64_t ic = valid ? i : a.n - 1;
-    f32x16 gi[TH], dy[TH], hn[TH];
+    f32x16 gi[TH], yh[TH], h1[TH], h2[TH], dh[TH];
     load_row_clayout<TH>(gi, a.g + ic * H);
     zero_if<TH>(gi, !valid);
-    {
-      f32x16 yh[TH];
-      load_row_clayout<TH>(yh, a.yh + ic * H);
-      const float rs = a.rstd[ic];
-      acc_layernorm_bwd<TH>(gi, yh, rs, gam, dy);
-      zero_if<TH>(dy, !valid);
-#pragma unroll
-      for (int t = 0; t < TH; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) yh[t][r] *= gi[t][r];
-      lds_store_items<TH>(sA, ldh, j, gi);
-      lds_store_items<TH>(sB, ldh, j, yh);
-      wave_lds_sync();
-      lane_sums<TH>(s_db, sA, ldh, nvalid);
-      lane_sums<TH>(s_dg, sB, ldh, nvalid);
-      wave_lds_sync();
+    load_row_clayout<TH>(yh, a.yh + ic * H);
+    load_row_clayout<TH>(h1, a.hn + ic * H);
+    zero_if<TH>(h1, !valid);
+    if (NL == 3) {
+      load_row_clayout<TH>(h2, a.hn2 + ic * H);
+      zero_if<TH>(h2, !valid);
     }
-    load_row_clayout<TH>(hn, a.hn + ic * H);
-    zero_if<TH>(hn, !valid);
-    lds_store_items<TH>(sA, ldh, j, dy);
-    lds_store_items<TH>(sB, ldh, j, hn);
-    wave_lds_sync();
-    lane_sums<TH>(s_db2, sA, ldh, nvalid);
-    __syncthreads();
-    outer_tiles<NT>(acc_w2, TH, TH, bufA, ldh, 0, bufB, ldh, 0);
-    __syncthreads();
-    f32x16 dh[TH];
-    zero<TH>(dh);
-    mfma_from_acc<TH, TH>(dh, W2T, ldh, 0, dy);
-#pragma unroll
-    for (int t = 0; t < TH; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dh[t][r] = hn[t][r] > 0.0f ? dh[t][r] : 0.0f;
-    f32x16 ag[TH];
-    load_row_clayout<TH>(ag, a.agg + ic * H);
-    zero_if<TH>(ag, !valid);
-    lds_store_items<TH>(sA, ldh, j, dh);
-    lds_store_items<TH>(sB, ldh, j, ag);
-    wave_lds_sync();
-    lane_sums<TH>(s_db1, sA, ldh, nvalid);
-    __syncthreads();
-    outer_tiles<NT>(acc_w1a, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, :H] = dh (x) agg
-    __syncthreads();
-    f32x16 xx[TH];
-    load_row_clayout<TH>(xx, a.x + ic * H);
-    zero_if<TH>(xx, !valid);
-    lds_store_items<TH>(sB, ldh, j, xx);
-    __syncthreads();
-    outer_tiles<NT>(acc_w1x, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, H:] = dh (x) x
-    __syncthreads();
+    ln_mlp_tail_bwd<TH, NL, GW, NT>(gi, yh, a.rstd[ic], gam, h1, h2, WlT, ldl, WmT, ldl, valid,
+                                    nvalid, im, acc_wl, acc_wm, s_db, s_dg, s_dbl, s_dbm, dh);
+    {
+      f32x16 ag[TH];
+      load_row_clayout<TH>(ag, a.agg + ic * H);
+      zero_if<TH>(ag, !valid);
+      lds_store_items<TH>(im.sA, ldh, j, dh);
+      lds_store_items<TH>(im.sB, ldh, j, ag);
+      wave_lds_sync();
+      lane_sums<TH>(s_db1, im.sA, ldh, nvalid);
+      __syncthreads();
+      outer_tiles<NT>(acc_w1a, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, :H] = dh (x) agg
+      __syncthreads();
+    }
+    {
+      f32x16 xx[TH];
+      load_row_clayout<TH>(xx, a.x + ic * H);
+      zero_if<TH>(xx, !valid);
+      lds_store_items<TH>(im.sB, ldh, j, xx);
+      __syncthreads();
+      outer_tiles<NT>(acc_w1x, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, H:] = dh (x) x
+      __syncthreads();
+    }
     // d agg = W1[:, :H]^T dh ; dx' = g + W1[:, H:]^T dh
     f32x16 o[TH];
     zero<TH>(o);
-    mfma_from_acc<TH, TH>(o, W1T, ldh, 0, dh);
+    matvec_t<TH, TH, GW>(o, W1aT, ld1, dh);
     if (valid) store_row_clayout<TH>(a.dagg + i * H, o);
-    mfma_from_acc<TH, TH>(gi, W1T + H * ldh, ldh, 0, dh);
+    matvec_t<TH, TH, GW>(gi, W1xT, ld1, dh);
     if (valid) store_row_clayout<TH>(a.dxp + i * H, gi);
-    (void)h;
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
-  store_outer<NT>(slab, H, TH, TH, acc_w2);
+  store_outer<NT>(slab, H, TH, TH, acc_wl);
   store_outer<NT>(slab + H * H, 2 * H, TH, TH, acc_w1a);
   store_outer<NT>(slab + H * H + H, 2 * H, TH, TH, acc_w1x);
-  float* v = slab + 3 * H * H;
+  if (NL == 3) store_outer<NT>(slab + 3 * H * H, H, TH, TH, acc_wm);
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_NODE, H, 0, NL);
   store_lane_vec<TH>(v, s_db1);
-  store_lane_vec<TH>(v + kWaves * H, s_db2);
+  store_lane_vec<TH>(v + kWaves * H, s_dbl);
   store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
   store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
+  if (NL == 3) store_lane_vec<TH>(v + 4 * kWaves * H, s_dbm);
 }
 
 // ===========================================================================
@@ -438,17 +570,24 @@ struct UvBwdArgs {
 
 template <int TH>
 __global__ __launch_bounds__(kBlock) void k_uv_bwd(UvBwdArgs a) {
-  constexpr int H = 32 * TH, ldh = H + 4;
+  constexpr bool GW = TH > 2;
+  constexpr int H = 32 * TH, ldh = H + 4, ldw = GW ? 3 * H : ldh;
   extern __shared__ float lds[];
-  float* WiT = lds;
-  float* WjT = WiT + H * ldh;
-  float* bufA = WjT + H * ldh;
+  float* p = lds;
+  const float* WiT = a.w1;
+  const float* WjT = a.w1 + H;
+  if (!GW) {
+    stage_matrix_t(p, ldh, a.w1, 3 * H, H, H, H, H);
+    stage_matrix_t(p + H * ldh, ldh, a.w1 + H, 3 * H, H, H, H, H);
+    WiT = p;
+    WjT = p + H * ldh;
+    p += 2 * H * ldh;
+  }
+  float* bufA = p;
   float* bufB = bufA + kChunk * ldh;
-  stage_matrix_t(WiT, ldh, a.w1, 3 * H, H, H, H, H);
-  stage_matrix_t(WjT, ldh, a.w1 + H, 3 * H, H, H, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
-  float* sA = bufA + w * 32 * ldh;
+  const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
+  const int j = im.j, w = threadIdx.x >> 6;
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   f32x16 acc_i[NT], acc_j[NT];
   zero_acc<NT>(acc_i);
@@ -470,17 +609,17 @@ __global__ __launch_bounds__(kBlock) void k_uv_bwd(UvBwdArgs a) {
     load_row_clayout<TH>(xx, a.x + ic * H);
     zero_if<TH>(xx, !valid);
     load_row_clayout<TH>(gg, a.dxp + ic * H);
-    mfma_from_acc<TH, TH>(gg, WiT, ldh, 0, du);
-    mfma_from_acc<TH, TH>(gg, WjT, ldh, 0, dv);
+    matvec_t<TH, TH, GW>(gg, WiT, ldw, du);
+    matvec_t<TH, TH, GW>(gg, WjT, ldw, dv);
     if (valid) store_row_clayout<TH>(a.g + i * H, gg);
-    lds_store_items<TH>(sA, ldh, j, du);
-    lds_store_items<TH>(bufB + w * 32 * ldh, ldh, j, xx);
+    lds_store_items<TH>(im.sA, ldh, j, du);
+    lds_store_items<TH>(im.sB, ldh, j, xx);
     wave_lds_sync();
-    lane_sums<TH>(s_db1, sA, ldh, nvalid);
+    lane_sums<TH>(s_db1, im.sA, ldh, nvalid);
     __syncthreads();
     outer_tiles<NT>(acc_i, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, 0:H] = dU (x) x
     __syncthreads();
-    lds_store_items<TH>(sA, ldh, j, dv);
+    lds_store_items<TH>(im.sA, ldh, j, dv);
     __syncthreads();
     outer_tiles<NT>(acc_j, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, H:2H] = dV (x) x
     __syncthreads();
@@ -492,7 +631,8 @@ __global__ __launch_bounds__(kBlock) void k_uv_bwd(UvBwdArgs a) {
 }
 
 // ===========================================================================
-// Loss (train.py:257-268) + Decoder backward (graph_network.py:321-333)
+// Loss (train.py:257-268) + Decoder / prediction-head backward
+// (graph_network.py:321-333, multi_scale_gnn.py:275; no LayerNorm)
 struct DecBwdArgs {
   const float* pred;      // [n][D+1]
   const float* pos_seq;   // noisy input window [n][T][D]
@@ -504,34 +644,48 @@ struct DecBwdArgs {
   int T, D;
   float w_pos, w_strain, inv_count;
   const float* dpred;
-  const float *hd, *x;
-  const float *wd1, *wd2;
+  const float *hd, *hd2, *x;
+  const float *wd1, *wdm, *wdl;
   float* g;
   float* slab;
   int64_t slab_stride;
 };
 
-template <int TH>
+template <int TH, int NL>
 __global__ __launch_bounds__(kBlock) void k_dec_bwd(DecBwdArgs a) {
+  constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4, ldo = 32 + 4;
+  constexpr int ld1 = GW ? H : ldh;
   extern __shared__ float lds[];
-  float* W1T = lds;                 // [H][ldh]
-  float* W2T = W1T + H * ldh;       // [H][ldo]: W2T[i][k] = Wd2[k][i], k < 32 (D+1 valid)
-  float* bufA = W2T + H * ldo;
+  float* WlT = lds;                 // [H][ldo]: WlT[i][k] = Wdl[k][i], k < 32 (D+1 valid)
+  float* p = WlT + H * ldo;
+  stage_matrix_t(WlT, ldo, a.wdl, H, a.D + 1, H, 32, H);
+  const float* W1T = a.wd1;
+  const float* WmT = a.wdm;
+  if (!GW) {
+    stage_matrix_t(p, ldh, a.wd1, H, H, H, H, H);
+    W1T = p;
+    p += H * ldh;
+    if (NL == 3) {
+      stage_matrix_t(p, ldh, a.wdm, H, H, H, H, H);
+      WmT = p;
+      p += H * ldh;
+    }
+  }
+  float* bufA = p;
   float* bufB = bufA + kChunk * ldh;
-  stage_matrix_t(W1T, ldh, a.wd1, H, H, H, H, H);
-  stage_matrix_t(W2T, ldo, a.wd2, H, a.D + 1, H, 32, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
-  float* sA = bufA + w * 32 * ldh;
-  float* sB = bufB + w * 32 * ldh;
-  constexpr int NT2 = (TH + kWaves - 1) / kWaves;     // [32 x H] decoder W2
-  constexpr int NT1 = (TH * TH + kWaves - 1) / kWaves;
-  f32x16 acc_w2[NT2], acc_w1[NT1];
-  zero_acc<NT2>(acc_w2);
-  zero_acc<NT1>(acc_w1);
-  float s_db2 = 0.0f;  // lane = output unit (< 32)
+  const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
+  const int l = lane_id(), j = im.j, h = l >> 5, w = threadIdx.x >> 6;
+  constexpr int NT2 = (TH + kWaves - 1) / kWaves;     // [32 x H] last layer
+  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
+  f32x16 acc_wl[NT2], acc_wm[NT], acc_w1[NT];
+  zero_acc<NT2>(acc_wl);
+  zero_acc<NT>(acc_wm);
+  zero_acc<NT>(acc_w1);
+  float s_dbl = 0.0f;  // lane = output unit (< 32)
   LANEVEC(s_db1);
+  LANEVEC(s_dbm);
   float loss_acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // total, x, y, z, strain
   const int64_t nchunks = (a.n + kChunk - 1) / kChunk;
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
@@ -545,13 +699,13 @@ __global__ __launch_bounds__(kBlock) void k_dec_bwd(DecBwdArgs a) {
       for (int cc = 0; cc <= a.D; ++cc) dp[0][cc] = a.dpred[ic * (a.D + 1) + cc];
     } else if (valid && h == 0) {
       const int D = a.D, T = a.T;
-      const float* p = a.pos_seq + ic * T * D;
+      const float* pp = a.pos_seq + ic * T * D;
       float tot = 0.0f;
       for (int cc = 0; cc < D; ++cc) {  // learned_simulator.py:479-481, :509-517
         const float nz = a.noise ? a.noise[(ic * T + T - 1) * D + cc] : 0.0f;
         const float nxt = __fadd_rn(a.next_pos[ic * D + cc], nz);
-        const float prev = p[(T - 1) * D + cc];
-        const float pvel = __fsub_rn(prev, p[(T - 2) * D + cc]);
+        const float prev = pp[(T - 1) * D + cc];
+        const float pvel = __fsub_rn(prev, pp[(T - 2) * D + cc]);
         const float acc = __fsub_rn(__fsub_rn(nxt, prev), pvel);
         const float tgt = __fdiv_rn(__fsub_rn(acc, a.acc_mean[cc]), a.acc_std[cc]);
         const float d = a.pred[ic * (D + 1) + cc] - tgt;
@@ -565,12 +719,17 @@ __global__ __launch_bounds__(kBlock) void k_dec_bwd(DecBwdArgs a) {
       loss_acc[4] += ds * ds;
     }
     constexpr int ldp = 32 + 4;
-    float* sP = sA;  // reuse: [32][ldp] image of dpred
+    f32x16 h1[TH], h2[TH], hl[TH];
+    load_row_clayout<TH>(h1, a.hd + ic * H);
+    zero_if<TH>(h1, !valid);
+    if (NL == 3) {
+      load_row_clayout<TH>(h2, a.hd2 + ic * H);
+      zero_if<TH>(h2, !valid);
+    }
+#pragma unroll
+    for (int t = 0; t < TH; ++t) hl[t] = NL == 3 ? h2[t] : h1[t];
     {
-      f32x16 hd[TH];
-      load_row_clayout<TH>(hd, a.hd + ic * H);
-      zero_if<TH>(hd, !valid);
-      // d pred image (32 units) and hd image for dW2 = dpred (x) hd
+      // d pred image (32 units) and hl image for dWl = dpred (x) hl
       f32x4 v;
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
@@ -578,43 +737,46 @@ __global__ __launch_bounds__(kBlock) void k_dec_bwd(DecBwdArgs a) {
         for (int cc = 0; cc < 4; ++cc) v[cc] = dp[0][4 * gq + cc];
         st4(bufA + (w * 32 + j) * ldp + 8 * gq + 4 * h, v);
       }
-      lds_store_items<TH>(sB, ldh, j, hd);
+      lds_store_items<TH>(im.sB, ldh, j, hl);
       wave_lds_sync();
-      if (l < 32) s_db2 += lane_sum(bufA + w * 32 * ldp, ldp, nvalid, l);
+      if (l < 32) s_dbl += lane_sum(bufA + w * 32 * ldp, ldp, nvalid, l);
       __syncthreads();
-      outer_tiles<NT2>(acc_w2, 1, TH, bufA, ldp, 0, bufB, ldh, 0);
+      outer_tiles<NT2>(acc_wl, 1, TH, bufA, ldp, 0, bufB, ldh, 0);
       __syncthreads();
-      f32x16 dh[TH];
-      zero<TH>(dh);
-      mfma_from_acc<TH, 1>(dh, W2T, ldo, 0, dp);
-#pragma unroll
-      for (int t = 0; t < TH; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dh[t][r] = hd[t][r] > 0.0f ? dh[t][r] : 0.0f;
-      f32x16 xx[TH];
-      load_row_clayout<TH>(xx, a.x + ic * H);
-      zero_if<TH>(xx, !valid);
-      lds_store_items<TH>(sA, ldh, j, dh);
-      lds_store_items<TH>(sB, ldh, j, xx);
-      wave_lds_sync();
-      lane_sums<TH>(s_db1, sA, ldh, nvalid);
-      __syncthreads();
-      outer_tiles<NT1>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);
-      __syncthreads();
-      f32x16 gg[TH];
-      zero<TH>(gg);
-      mfma_from_acc<TH, TH>(gg, W1T, ldh, 0, dh);
-      if (valid) store_row_clayout<TH>(a.g + i * H, gg);
     }
-    (void)sP;
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    mfma_from_acc<TH, 1>(dh, WlT, ldo, 0, dp);
+    relu_mask<TH>(dh, hl, valid);
+    if constexpr (NL == 3) {
+      f32x16 d1[TH];
+      hidden_linear_bwd<TH, GW, NT>(dh, h1, WmT, ld1, valid, nvalid, im, acc_wm, s_dbm, d1);
+#pragma unroll
+      for (int t = 0; t < TH; ++t) dh[t] = d1[t];
+    }
+    f32x16 xx[TH];
+    load_row_clayout<TH>(xx, a.x + ic * H);
+    zero_if<TH>(xx, !valid);
+    lds_store_items<TH>(im.sA, ldh, j, dh);
+    lds_store_items<TH>(im.sB, ldh, j, xx);
+    wave_lds_sync();
+    lane_sums<TH>(s_db1, im.sA, ldh, nvalid);
+    __syncthreads();
+    outer_tiles<NT>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);
+    __syncthreads();
+    f32x16 gg[TH];
+    zero<TH>(gg);
+    matvec_t<TH, TH, GW>(gg, W1T, ld1, dh);
+    if (valid) store_row_clayout<TH>(a.g + i * H, gg);
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
-  store_outer<NT2>(slab, H, 1, TH, acc_w2);           // [32][H] (rows >= D+1 are zero)
-  store_outer<NT1>(slab + 32 * H, H, TH, TH, acc_w1);  // [H][H]
-  float* v = slab + 32 * H + H * H;
-  if (l < 32) v[w * 32 + l] = s_db2;
+  store_outer<NT2>(slab, H, 1, TH, acc_wl);           // [32][H] (rows >= D+1 are zero)
+  store_outer<NT>(slab + 32 * H, H, TH, TH, acc_w1);  // [H][H]
+  if (NL == 3) store_outer<NT>(slab + 32 * H + H * H, H, TH, TH, acc_wm);
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_DECODER, H, 0, NL);
+  if (l < 32) v[w * 32 + l] = s_dbl;
   store_lane_vec<TH>(v + kWaves * 32, s_db1);
-  // loss partials: reduce over lanes, one row of 4 per wave
+  // loss partials: reduce over lanes, one row of 8 per wave
   float* lp = v + kWaves * 32 + kWaves * H;
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
@@ -622,45 +784,60 @@ __global__ __launch_bounds__(kBlock) void k_dec_bwd(DecBwdArgs a) {
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if (l == 0) lp[w * 8 + q] = s;
   }
+  if (NL == 3) store_lane_vec<TH>(lp + kWaves * 8, s_dbm);
 }
 
 // ===========================================================================
-// Encoder node MLP backward (graph_network.py:86-90)
+// Encoder node MLP backward (graph_network.py:86-90; multi_scale_gnn.py:241)
 struct EncNodeBwdArgs {
   const float* g;
   const float* pos_seq;
   int64_t n;
   int T, dim, feat;
   const float *vel_mean, *vel_std;
-  float radius;
-  const float *h1, *yh, *rstd;
-  const float *w2, *gamma;
+  float wall_max, wall_div;
+  const float *h1, *h2, *yh, *rstd;
+  const float *wl, *wm, *gamma;
   float* slab;
   int64_t slab_stride;
 };
 
-template <int TH, int TKF>
+template <int TH, int TKF, int NL>
 __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
+  constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4, ldf = 32 * TKF + 4;
-  extern __shared__ float lds[];
-  float* W2T = lds;
-  float* gam = W2T + H * ldh;
-  float* bufA = gam + H;
-  float* bufB = bufA + kChunk * ldh;  // sized max(ldh, ldf) per row
+  constexpr int ldl = GW ? H : ldh;
   constexpr int ldb = ldh > ldf ? ldh : ldf;
-  stage_matrix_t(W2T, ldh, a.w2, H, H, H, H, H);
+  extern __shared__ float lds[];
+  float* p = lds;
+  const float* WlT = a.wl;
+  const float* WmT = a.wm;
+  if (!GW) {
+    stage_matrix_t(p, ldh, a.wl, H, H, H, H, H);
+    WlT = p;
+    p += H * ldh;
+    if (NL == 3) {
+      stage_matrix_t(p, ldh, a.wm, H, H, H, H, H);
+      WmT = p;
+      p += H * ldh;
+    }
+  }
+  float* gam = p;
+  float* bufA = gam + H;
+  float* bufB = bufA + kChunk * ldh;  // rows of max(ldh, ldf)
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
-  float* sA = bufA + w * 32 * ldh;
-  float* sB = bufB + w * 32 * ldb;
-  constexpr int NT2 = (TH * TH + kWaves - 1) / kWaves;
+  const Imgs im = make_imgs(bufA, ldh, bufB, ldb);
+  const int l = lane_id(), j = im.j, h = l >> 5, w = threadIdx.x >> 6;
+  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   constexpr int NT1 = (TH * TKF + kWaves - 1) / kWaves;
-  f32x16 acc_w2[NT2], acc_w1[NT1];
-  zero_acc<NT2>(acc_w2);
+  f32x16 acc_wl[NT], acc_wm[NT], acc_w1[NT1];
+  zero_acc<NT>(acc_wl);
+  zero_acc<NT>(acc_wm);
   zero_acc<NT1>(acc_w1);
   LANEVEC(s_db1);
-  LANEVEC(s_db2);
+  LANEVEC(s_dbl);
+  LANEVEC(s_dbm);
   LANEVEC(s_dg);
   LANEVEC(s_db);
   const int nvel = (a.T - 1) * a.dim;
@@ -670,45 +847,21 @@ __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
     const int nvalid = clamp_items(a.n - (c * kChunk + w * 32));
     const bool valid = i < a.n;
     const int64_t ic = valid ? i : a.n - 1;
-    f32x16 gi[TH], dy[TH];
+    f32x16 gi[TH], yh[TH], h1[TH], h2[TH], dh[TH];
     load_row_clayout<TH>(gi, a.g + ic * H);
-    zero_if<TH>(gi, !valid);
-    {
-      f32x16 yh[TH];
-      load_row_clayout<TH>(yh, a.yh + ic * H);
-      acc_layernorm_bwd<TH>(gi, yh, a.rstd[ic], gam, dy);
-      zero_if<TH>(dy, !valid);
-#pragma unroll
-      for (int t = 0; t < TH; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) yh[t][r] *= gi[t][r];
-      lds_store_items<TH>(sA, ldh, j, gi);
-      lds_store_items<TH>(sB, ldb, j, yh);
-      wave_lds_sync();
-      lane_sums<TH>(s_db, sA, ldh, nvalid);
-      lane_sums<TH>(s_dg, sB, ldb, nvalid);
-      wave_lds_sync();
-    }
-    f32x16 h1[TH];
+    load_row_clayout<TH>(yh, a.yh + ic * H);
     load_row_clayout<TH>(h1, a.h1 + ic * H);
     zero_if<TH>(h1, !valid);
-    lds_store_items<TH>(sA, ldh, j, dy);
-    lds_store_items<TH>(sB, ldb, j, h1);
-    wave_lds_sync();
-    lane_sums<TH>(s_db2, sA, ldh, nvalid);
-    __syncthreads();
-    outer_tiles<NT2>(acc_w2, TH, TH, bufA, ldh, 0, bufB, ldb, 0);
-    __syncthreads();
-    f32x16 dh[TH];
-    zero<TH>(dh);
-    mfma_from_acc<TH, TH>(dh, W2T, ldh, 0, dy);
-#pragma unroll
-    for (int t = 0; t < TH; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dh[t][r] = (h1[t][r] > 0.0f && valid) ? dh[t][r] : 0.0f;
-    // node features recomputed exactly as the forward (learned_simulator.py:272-284)
+    if (NL == 3) {
+      load_row_clayout<TH>(h2, a.h2 + ic * H);
+      zero_if<TH>(h2, !valid);
+    }
+    ln_mlp_tail_bwd<TH, NL, GW, NT>(gi, yh, a.rstd[ic], gam, h1, h2, WlT, ldl, WmT, ldl, valid,
+                                    nvalid, im, acc_wl, acc_wm, s_db, s_dg, s_dbl, s_dbm, dh);
+    // node features recomputed exactly as the forward (learned_simulator.py:272-284,
+    // multi_scale_simulator.py:176-196)
     f32x16 xf[TKF];
-    const float* p = a.pos_seq + ic * a.T * a.dim;
+    const float* pp = a.pos_seq + ic * a.T * a.dim;
 #pragma unroll
     for (int tk = 0; tk < TKF; ++tk)
 #pragma unroll
@@ -717,33 +870,37 @@ __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
         float val = 0.0f;
         if (valid && f < nvel) {
           const int t = f / a.dim, cc = f - t * a.dim;
-          const float vel = __fsub_rn(p[(t + 1) * a.dim + cc], p[t * a.dim + cc]);
+          const float vel = __fsub_rn(pp[(t + 1) * a.dim + cc], pp[t * a.dim + cc]);
           val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[cc]), a.vel_std[cc]);
         } else if (valid && f == nvel) {
-          val = fminf(fmaxf(__fadd_rn(p[(a.T - 1) * a.dim], 2.0f), 0.0f), a.radius);
+          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(pp[(a.T - 1) * a.dim], 2.0f), 0.0f), a.wall_max),
+                          a.wall_div);
         }
         xf[tk][r] = val;
       }
-    lds_store_items<TH>(sA, ldh, j, dh);
-    lds_store_items<TKF>(sB, ldb, j, xf);
+    lds_store_items<TH>(im.sA, ldh, j, dh);
+    lds_store_items<TKF>(im.sB, ldb, j, xf);
     wave_lds_sync();
-    lane_sums<TH>(s_db1, sA, ldh, nvalid);
+    lane_sums<TH>(s_db1, im.sA, ldh, nvalid);
     __syncthreads();
     outer_tiles<NT1>(acc_w1, TH, TKF, bufA, ldh, 0, bufB, ldb, 0);
     __syncthreads();
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
-  store_outer<NT2>(slab, H, TH, TH, acc_w2);
+  store_outer<NT>(slab, H, TH, TH, acc_wl);
   store_outer<NT1>(slab + H * H, 32 * TKF, TH, TKF, acc_w1);
-  float* v = slab + H * H + H * 32 * TKF;
+  if (NL == 3) store_outer<NT>(slab + H * H + H * 32 * TKF, H, TH, TH, acc_wm);
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_ENC_NODE, H, 32 * TKF, NL);
   store_lane_vec<TH>(v, s_db1);
-  store_lane_vec<TH>(v + kWaves * H, s_db2);
+  store_lane_vec<TH>(v + kWaves * H, s_dbl);
   store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
   store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
+  if (NL == 3) store_lane_vec<TH>(v + 4 * kWaves * H, s_dbm);
 }
 
 // ===========================================================================
-// Encoder edge MLP backward (graph_network.py:92-96) from dE0
+// Encoder edge MLP backward (graph_network.py:92-96; multi_scale_gnn.py:247-258)
+// from dE0
 struct EncEdgeBwdArgs {
   const float* de0t;
   const float* pos;
@@ -752,37 +909,51 @@ struct EncEdgeBwdArgs {
   float radius;
   const int32_t *rowptr, *send, *recv;
   int64_t n;
-  const float *yh, *rstd;
-  const float *w1, *b1, *w2, *gamma;
+  const float *h2, *yh, *rstd;
+  const float *w1, *b1, *wl, *wm, *gamma;
   float* slab;
   int64_t slab_stride;
 };
 
-template <int TH>
+template <int TH, int NL>
 __global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
+  constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4, ld1 = 5, ldf = 32 + 4;
+  constexpr int ldl = GW ? H : ldh;
   extern __shared__ float lds[];
   float* W1 = lds;
-  float* W2T = W1 + H * ld1;
-  float* b1 = W2T + H * ldh;
+  float* p = W1 + H * ld1;
+  stage_matrix(W1, ld1, a.w1, a.dim + 1, H, a.dim + 1, H, 4);
+  const float* WlT = a.wl;
+  const float* WmT = a.wm;
+  if (!GW) {
+    stage_matrix_t(p, ldh, a.wl, H, H, H, H, H);
+    WlT = p;
+    p += H * ldh;
+    if (NL == 3) {
+      stage_matrix_t(p, ldh, a.wm, H, H, H, H, H);
+      WmT = p;
+      p += H * ldh;
+    }
+  }
+  float* b1 = p;
   float* gam = b1 + H;
   float* bufA = gam + H;
   float* bufB = bufA + kChunk * ldh;
-  stage_matrix(W1, ld1, a.w1, a.dim + 1, H, a.dim + 1, H, 4);
-  stage_matrix_t(W2T, ldh, a.w2, H, H, H, H, H);
   stage_vec(b1, a.b1, H, H);
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
-  float* sA = bufA + w * 32 * ldh;
-  float* sB = bufB + w * 32 * ldh;
-  constexpr int NT2 = (TH * TH + kWaves - 1) / kWaves;
+  const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
+  const int l = lane_id(), j = im.j, h = l >> 5, w = threadIdx.x >> 6;
+  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   constexpr int NT1 = (TH + kWaves - 1) / kWaves;
-  f32x16 acc_w2[NT2], acc_w1[NT1];
-  zero_acc<NT2>(acc_w2);
+  f32x16 acc_wl[NT], acc_wm[NT], acc_w1[NT1];
+  zero_acc<NT>(acc_wl);
+  zero_acc<NT>(acc_wm);
   zero_acc<NT1>(acc_w1);
   LANEVEC(s_db1);
-  LANEVEC(s_db2);
+  LANEVEC(s_dbl);
+  LANEVEC(s_dbm);
   LANEVEC(s_dg);
   LANEVEC(s_db);
   const int64_t E = a.rowptr[a.n];
@@ -792,27 +963,18 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
     const int nvalid = clamp_items(E - base);
     const bool valid = e < E;
     const int64_t ec = valid ? e : (E > 0 ? E - 1 : 0);
-    f32x16 dy[TH], h1[TH], fx[1];
-    zero<TH>(dy);
+    f32x16 dm[TH], yh[TH], h1[TH], h2[TH], fx[1];
+    float rs = 0.0f;
+    zero<TH>(dm);
+    zero<TH>(yh);
     zero<TH>(h1);
+    zero<TH>(h2);
     zero<1>(fx);
     if (nvalid > 0) {
-      f32x16 dm[TH], yh[TH];
       load_tiled<TH>(dm, a.de0t + tile * (32 * H));
       load_tiled<TH>(yh, a.yh + tile * (32 * H));
-      zero_if<TH>(dm, !valid);
-      acc_layernorm_bwd<TH>(dm, yh, a.rstd[ec], gam, dy);
-      zero_if<TH>(dy, !valid);
-#pragma unroll
-      for (int t = 0; t < TH; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];
-      lds_store_items<TH>(sA, ldh, j, dm);
-      lds_store_items<TH>(sB, ldh, j, yh);
-      wave_lds_sync();
-      lane_sums<TH>(s_db, sA, ldh, nvalid);
-      lane_sums<TH>(s_dg, sB, ldh, nvalid);
-      wave_lds_sync();
+      if (NL == 3) load_tiled<TH>(h2, a.h2 + tile * (32 * H));
+      rs = a.rstd[ec];
       // recompute edge features and the first hidden layer (cheap: K = dim+1)
       const int64_t s = a.send[ec], r = a.recv[ec];
       float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -827,42 +989,34 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
       mfma_step<TH>(h1, W1, ld1, h, h ? f[1] : f[0]);
       mfma_step<TH>(h1, W1, ld1, 2 + h, h ? f[3] : f[2]);
       acc_relu<TH>(h1);
-      zero_if<TH>(h1, !valid);
       if (valid && h == 0) {
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) fx[0][cc] = f[cc];
       }
     }
-    lds_store_items<TH>(sA, ldh, j, dy);
-    lds_store_items<TH>(sB, ldh, j, h1);
-    wave_lds_sync();
-    lane_sums<TH>(s_db2, sA, ldh, nvalid);
-    __syncthreads();
-    outer_tiles<NT2>(acc_w2, TH, TH, bufA, ldh, 0, bufB, ldh, 0);
-    __syncthreads();
+    zero_if<TH>(h1, !valid);
+    zero_if<TH>(h2, !valid);
     f32x16 dh[TH];
-    zero<TH>(dh);
-    mfma_from_acc<TH, TH>(dh, W2T, ldh, 0, dy);
-#pragma unroll
-    for (int t = 0; t < TH; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dh[t][r] = h1[t][r] > 0.0f ? dh[t][r] : 0.0f;
-    lds_store_items<TH>(sA, ldh, j, dh);
+    ln_mlp_tail_bwd<TH, NL, GW, NT>(dm, yh, rs, gam, h1, h2, WlT, ldl, WmT, ldl, valid, nvalid,
+                                    im, acc_wl, acc_wm, s_db, s_dg, s_dbl, s_dbm, dh);
+    lds_store_items<TH>(im.sA, ldh, j, dh);
     lds_store_items<1>(bufB + w * 32 * ldf, ldf, j, fx);
     wave_lds_sync();
-    lane_sums<TH>(s_db1, sA, ldh, nvalid);
+    lane_sums<TH>(s_db1, im.sA, ldh, nvalid);
     __syncthreads();
     outer_tiles<NT1>(acc_w1, TH, 1, bufA, ldh, 0, bufB, ldf, 0);
     __syncthreads();
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
-  store_outer<NT2>(slab, H, TH, TH, acc_w2);
+  store_outer<NT>(slab, H, TH, TH, acc_wl);
   store_outer<NT1>(slab + H * H, 32, TH, 1, acc_w1);
-  float* v = slab + H * H + H * 32;
+  if (NL == 3) store_outer<NT>(slab + H * H + H * 32, H, TH, TH, acc_wm);
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_ENC_EDGE, H, 0, NL);
   store_lane_vec<TH>(v, s_db1);
-  store_lane_vec<TH>(v + kWaves * H, s_db2);
+  store_lane_vec<TH>(v + kWaves * H, s_dbl);
   store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
   store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
+  if (NL == 3) store_lane_vec<TH>(v + 4 * kWaves * H, s_dbm);
 }
 
 // ===========================================================================
@@ -954,82 +1108,105 @@ void set_lds(K kernel, size_t bytes) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-}  // namespace
-
-// ---------------------------------------------------------------------------
-extern "C" int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat) {
-  const int64_t H = hidden, W = kWaves;
-  const int64_t fpad = 32 * ((feat + 31) / 32);
-  switch (kind) {
-    case SGNN_SLAB_EDGE: return 2 * H * H + 3 * W * H;
-    case SGNN_SLAB_NODE: return 3 * H * H + 4 * W * H;
-    case SGNN_SLAB_UV: return 2 * H * H + W * H;
-    case SGNN_SLAB_DECODER: return 32 * H + H * H + W * 32 + W * H + W * 8;
-    case SGNN_SLAB_ENC_NODE: return H * H + H * fpad + 4 * W * H;
-    case SGNN_SLAB_ENC_EDGE: return H * H + H * 32 + 4 * W * H;
-    default: return -1;
-  }
+template <typename K, typename A>
+void launch_bwd(K kernel, int nslab, size_t lds, void* stream, const A& a) {
+  set_lds(kernel, lds);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)nslab), dim3(kBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
 }
 
-static size_t bwd_lds(int kind, int H, int tkf) {
+// LDS bytes per kind: weight images (H = 64 only) + vectors + the two
+// [128 items][H+4] operand images of the outer products.
+size_t bwd_lds(int kind, int H, int tkf, int nl) {
   const size_t ldh = H + 4, chunk = kChunk;
+  const bool gw = H > 64;
+  const size_t img = gw ? 0 : H * ldh;        // one staged H x H weight image
+  const size_t mid = nl == 3 ? img : 0;
+  const size_t bufs = 2 * chunk * ldh;
   switch (kind) {
-    case SGNN_SLAB_EDGE: return 4 * (2 * H * ldh + H + 2 * chunk * ldh);
-    case SGNN_SLAB_NODE: return 4 * (3 * H * ldh + H + 2 * chunk * ldh);
-    case SGNN_SLAB_UV: return 4 * (2 * H * ldh + 2 * chunk * ldh);
-    case SGNN_SLAB_DECODER: return 4 * (H * ldh + H * 36 + 2 * chunk * ldh);
+    case SGNN_SLAB_EDGE: return 4 * (2 * img + mid + H + bufs);
+    case SGNN_SLAB_NODE: return 4 * (3 * img + mid + H + bufs);
+    case SGNN_SLAB_UV: return 4 * (2 * img + bufs);
+    case SGNN_SLAB_DECODER: return 4 * (H * 36 + img + mid + bufs);
     case SGNN_SLAB_ENC_NODE: {
       const size_t ldb = std::max<size_t>(ldh, 32 * tkf + 4);
-      return 4 * (H * ldh + H + chunk * ldh + chunk * ldb);
+      return 4 * (img + mid + H + chunk * ldh + chunk * ldb);
     }
-    case SGNN_SLAB_ENC_EDGE: return 4 * (H * 5 + H * ldh + 2 * H + 2 * chunk * ldh);
+    case SGNN_SLAB_ENC_EDGE: return 4 * (H * 5 + img + mid + 2 * H + bufs);
     default: return 0;
   }
 }
 
-#define CHECK_H(H, what) \
-  if ((H) != 64) return sgnn::set_error(SGNN_ERR_UNSUPPORTED, what ": hidden must be 64 in this build")
+int check_bwd_mlp(const sgnn_mlp* m, const char* what) {
+  if (!m || !m->w1 || !m->w2) return sgnn::set_error(SGNN_ERR_INVALID, what);
+  if (m->hidden != 64 && m->hidden != 128)
+    return sgnn::set_error(SGNN_ERR_UNSUPPORTED, "backward: hidden must be 64 or 128");
+  if (m->nlin != 2 && m->nlin != 3)
+    return sgnn::set_error(SGNN_ERR_UNSUPPORTED, "backward: MLPs must have 2 or 3 Linear layers");
+  if (m->nlin == 3 && !m->w3) return sgnn::set_error(SGNN_ERR_INVALID, what);
+  return SGNN_OK;
+}
+
+const float* last_w(const sgnn_mlp* m) { return m->nlin == 3 ? m->w3 : m->w2; }
+const float* mid_w(const sgnn_mlp* m) { return m->nlin == 3 ? m->w2 : nullptr; }
+
+#define SGNN_BWD_DISPATCH(H, NL, CALL)                                    \
+  do {                                                                    \
+    if ((H) == 64 && (NL) == 2) { constexpr int TH_ = 2, NL_ = 2; CALL; } \
+    else if ((H) == 64) { constexpr int TH_ = 2, NL_ = 3; CALL; }         \
+    else if ((NL) == 2) { constexpr int TH_ = 4, NL_ = 2; CALL; }         \
+    else { constexpr int TH_ = 4, NL_ = 3; CALL; }                        \
+  } while (0)
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+extern "C" int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat, int32_t nlin) {
+  if (kind < 0 || kind > SGNN_SLAB_ENC_EDGE || (nlin != 2 && nlin != 3) || hidden <= 0) return -1;
+  const int64_t fpad = 32 * ((feat + 31) / 32);
+  return slab_nmat_floats(kind, hidden, fpad, nlin) + slab_nvec_floats(kind, hidden, nlin);
+}
 
 extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t* send,
-                                   const int32_t* recv, int64_t n, const float* h_save,
-                                   const float* yhat_save, const float* rstd_save,
+                                   const int32_t* recv, int64_t n, const sgnn_saves* saves,
                                    const float* e0t, float e_scale, const sgnn_mlp* edge_fn,
                                    float* du, float* cin, float* cout, float* dh_rows, float* de0t,
                                    int32_t de0_accumulate, float* slab, int32_t nslab,
                                    void* stream) {
   using namespace sgnn;
-  if (!edge_fn || !dagg || !rowptr || !send || !recv || !h_save || !yhat_save || !rstd_save ||
-      !e0t || !du || !cin || !cout || !dh_rows || !de0t || !slab || nslab < 1 || n <= 0)
+  if (!edge_fn || !dagg || !rowptr || !send || !recv || !saves || !saves->h || !saves->yhat ||
+      !saves->rstd || !e0t || !du || !cin || !cout || !dh_rows || !de0t || !slab || nslab < 1 ||
+      n <= 0)
     return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: bad arguments");
+  int st = check_bwd_mlp(edge_fn, "edge_layer_bwd: edge MLP");
+  if (st) return st;
+  if (edge_fn->nlin == 3 && !saves->h2) return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: saves->h2");
   const int H = edge_fn->hidden;
-  CHECK_H(H, "edge_layer_bwd");
-  EdgeBwdArgs a{dagg, rowptr, send, recv, n, h_save, yhat_save, rstd_save, e0t, e_scale,
-                edge_fn->w2, edge_fn->w1 + 2 * H, edge_fn->ln_g, du, cin, cout, dh_rows, de0t,
-                de0_accumulate, slab, sgnn_bwd_slab_floats(SGNN_SLAB_EDGE, H, 0)};
-  const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0);
-  set_lds(k_edge_bwd<2>, lds);
-  hipLaunchKernelGGL((k_edge_bwd<2>), dim3(nslab), dim3(kBlock), lds,
-                     static_cast<hipStream_t>(stream), a);
+  EdgeBwdArgs a{dagg, rowptr, send, recv, n, saves->h, saves->h2, saves->yhat, saves->rstd, e0t,
+                e_scale, last_w(edge_fn), mid_w(edge_fn), edge_fn->w1 + 2 * H, edge_fn->ln_g, du,
+                cin, cout, dh_rows, de0t, de0_accumulate, slab,
+                sgnn_bwd_slab_floats(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin)};
+  const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin);
+  SGNN_BWD_DISPATCH(H, edge_fn->nlin, (launch_bwd(k_edge_bwd<TH_, NL_>, nslab, lds, stream, a)));
   return check_launch("edge_layer_bwd");
 }
 
-extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const float* yhat_save,
-                                   const float* rstd_save, const float* h_save,
-                                   const float* agg_save, const float* x_in,
-                                   const sgnn_mlp* node_fn, float* dagg, float* dxp, float* slab,
-                                   int32_t nslab, void* stream) {
+extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* saves,
+                                   const float* x_in, const sgnn_mlp* node_fn, float* dagg,
+                                   float* dxp, float* slab, int32_t nslab, void* stream) {
   using namespace sgnn;
-  if (!node_fn || !g || !yhat_save || !rstd_save || !h_save || !agg_save || !x_in || !dagg ||
-      !dxp || !slab || nslab < 1 || n <= 0)
+  if (!node_fn || !g || !saves || !saves->yhat || !saves->rstd || !saves->h || !saves->agg ||
+      !x_in || !dagg || !dxp || !slab || nslab < 1 || n <= 0)
     return set_error(SGNN_ERR_INVALID, "node_layer_bwd: bad arguments");
+  int st = check_bwd_mlp(node_fn, "node_layer_bwd: node MLP");
+  if (st) return st;
+  if (node_fn->nlin == 3 && !saves->h2) return set_error(SGNN_ERR_INVALID, "node_layer_bwd: saves->h2");
   const int H = node_fn->hidden;
-  CHECK_H(H, "node_layer_bwd");
-  NodeBwdArgs a{g, n, yhat_save, rstd_save, h_save, agg_save, x_in, node_fn->w1, node_fn->w2,
-                node_fn->ln_g, dagg, dxp, slab, sgnn_bwd_slab_floats(SGNN_SLAB_NODE, H, 0)};
-  const size_t lds = bwd_lds(SGNN_SLAB_NODE, H, 0);
-  set_lds(k_node_bwd<2>, lds);
-  hipLaunchKernelGGL((k_node_bwd<2>), dim3(nslab), dim3(kBlock), lds,
-                     static_cast<hipStream_t>(stream), a);
+  NodeBwdArgs a{g, n, saves->yhat, saves->rstd, saves->h, saves->h2, saves->agg, x_in, node_fn->w1,
+                last_w(node_fn), mid_w(node_fn), node_fn->ln_g, dagg, dxp, slab,
+                sgnn_bwd_slab_floats(SGNN_SLAB_NODE, H, 0, node_fn->nlin)};
+  const size_t lds = bwd_lds(SGNN_SLAB_NODE, H, 0, node_fn->nlin);
+  SGNN_BWD_DISPATCH(H, node_fn->nlin, (launch_bwd(k_node_bwd<TH_, NL_>, nslab, lds, stream, a)));
   return check_launch("node_layer_bwd");
 }
 
@@ -1042,14 +1219,14 @@ extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, 
   if (!edge_fn || !dxp || !du || !cin || !cout || !rowptr || !dh_rows || !tptr || !tperm ||
       !x_in || !g || !slab || nslab < 1 || n <= 0)
     return set_error(SGNN_ERR_INVALID, "uv_bwd: bad arguments");
+  int st = check_bwd_mlp(edge_fn, "uv_bwd: edge MLP");
+  if (st) return st;
   const int H = edge_fn->hidden;
-  CHECK_H(H, "uv_bwd");
   UvBwdArgs a{dxp, du, cin, cout, rowptr, dh_rows, tptr, tperm, x_in, n, edge_fn->w1, g, slab,
-              sgnn_bwd_slab_floats(SGNN_SLAB_UV, H, 0)};
-  const size_t lds = bwd_lds(SGNN_SLAB_UV, H, 0);
-  set_lds(k_uv_bwd<2>, lds);
-  hipLaunchKernelGGL((k_uv_bwd<2>), dim3(nslab), dim3(kBlock), lds,
-                     static_cast<hipStream_t>(stream), a);
+              sgnn_bwd_slab_floats(SGNN_SLAB_UV, H, 0, edge_fn->nlin)};
+  const size_t lds = bwd_lds(SGNN_SLAB_UV, H, 0, 2);
+  if (H == 64) launch_bwd(k_uv_bwd<2>, nslab, lds, stream, a);
+  else launch_bwd(k_uv_bwd<4>, nslab, lds, stream, a);
   return check_launch("uv_bwd");
 }
 
@@ -1058,53 +1235,53 @@ extern "C" int sgnn_decoder_loss_bwd(const float* pred, const float* pos_seq,
                                      const float* next_strain, const float* acc_mean,
                                      const float* acc_std, int64_t n, int32_t T, int32_t dim,
                                      float w_pos, float w_strain, float inv_count,
-                                     const float* dpred, const float* hd_save, const float* x_last,
-                                     const sgnn_mlp* decoder, float* g, float* slab,
-                                     int32_t nslab, void* stream) {
+                                     const float* dpred, const sgnn_saves* saves,
+                                     const float* x_last, const sgnn_mlp* decoder, float* g,
+                                     float* slab, int32_t nslab, void* stream) {
   using namespace sgnn;
-  if (!decoder || !pred || !hd_save || !x_last || !g || !slab || nslab < 1 || n <= 0 || T < 2 ||
-      dim < 1 || dim > 3 ||
+  if (!decoder || !pred || !saves || !saves->hd || !x_last || !g || !slab || nslab < 1 || n <= 0 ||
+      T < 2 || dim < 1 || dim > 3 ||
       (!dpred && (!pos_seq || !next_pos || !next_strain || !acc_mean || !acc_std)))
     return set_error(SGNN_ERR_INVALID, "decoder_loss_bwd: bad arguments");
+  int st = check_bwd_mlp(decoder, "decoder_loss_bwd: decoder MLP");
+  if (st) return st;
+  if (decoder->nlin == 3 && !saves->hd2) return set_error(SGNN_ERR_INVALID, "decoder_loss_bwd: saves->hd2");
   const int H = decoder->hidden;
-  CHECK_H(H, "decoder_loss_bwd");
   if (decoder->out_dim != dim + 1) return set_error(SGNN_ERR_INVALID, "decoder_loss_bwd: out dim");
   DecBwdArgs a{pred, pos_seq, next_pos, noise, next_strain, acc_mean, acc_std, n, T, dim,
-               w_pos, w_strain, inv_count, dpred, hd_save, x_last, decoder->w1, decoder->w2, g, slab,
-               sgnn_bwd_slab_floats(SGNN_SLAB_DECODER, H, 0)};
-  const size_t lds = bwd_lds(SGNN_SLAB_DECODER, H, 0);
-  set_lds(k_dec_bwd<2>, lds);
-  hipLaunchKernelGGL((k_dec_bwd<2>), dim3(nslab), dim3(kBlock), lds,
-                     static_cast<hipStream_t>(stream), a);
+               w_pos, w_strain, inv_count, dpred, saves->hd, saves->hd2, x_last, decoder->w1,
+               mid_w(decoder), last_w(decoder), g, slab,
+               sgnn_bwd_slab_floats(SGNN_SLAB_DECODER, H, 0, decoder->nlin)};
+  const size_t lds = bwd_lds(SGNN_SLAB_DECODER, H, 0, decoder->nlin);
+  SGNN_BWD_DISPATCH(H, decoder->nlin, (launch_bwd(k_dec_bwd<TH_, NL_>, nslab, lds, stream, a)));
   return check_launch("decoder_loss_bwd");
 }
 
 extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
                                      int32_t dim, const float* vel_mean, const float* vel_std,
-                                     float radius, const float* h_save, const float* yhat_save,
-                                     const float* rstd_save, const sgnn_mlp* enc, float* slab,
-                                     int32_t nslab, void* stream) {
+                                     float wall_max, float wall_div, const sgnn_saves* saves,
+                                     const sgnn_mlp* enc, float* slab, int32_t nslab,
+                                     void* stream) {
   using namespace sgnn;
-  if (!enc || !g || !pos_seq || !vel_mean || !vel_std || !h_save || !yhat_save || !rstd_save ||
-      !slab || nslab < 1 || n <= 0)
+  if (!enc || !g || !pos_seq || !vel_mean || !vel_std || !saves || !saves->h || !saves->yhat ||
+      !saves->rstd || !slab || nslab < 1 || n <= 0)
     return set_error(SGNN_ERR_INVALID, "encode_nodes_bwd: bad arguments");
+  int st = check_bwd_mlp(enc, "encode_nodes_bwd: encoder MLP");
+  if (st) return st;
+  if (enc->nlin == 3 && !saves->h2) return set_error(SGNN_ERR_INVALID, "encode_nodes_bwd: saves->h2");
   const int H = enc->hidden;
-  CHECK_H(H, "encode_nodes_bwd");
   const int feat = (T - 1) * dim + 1;
   if (enc->in_dim != feat)
     return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd: particle-type embeddings not supported");
   const int tkf = (feat + 31) / 32;
-  EncNodeBwdArgs a{g, pos_seq, n, T, dim, feat, vel_mean, vel_std, radius, h_save, yhat_save,
-                   rstd_save, enc->w2, enc->ln_g, slab,
-                   sgnn_bwd_slab_floats(SGNN_SLAB_ENC_NODE, H, feat)};
-  const size_t lds = bwd_lds(SGNN_SLAB_ENC_NODE, H, tkf);
-  hipStream_t s = static_cast<hipStream_t>(stream);
+  EncNodeBwdArgs a{g, pos_seq, n, T, dim, feat, vel_mean, vel_std, wall_max, wall_div, saves->h,
+                   saves->h2, saves->yhat, saves->rstd, last_w(enc), mid_w(enc), enc->ln_g, slab,
+                   sgnn_bwd_slab_floats(SGNN_SLAB_ENC_NODE, H, feat, enc->nlin)};
+  const size_t lds = bwd_lds(SGNN_SLAB_ENC_NODE, H, tkf, enc->nlin);
   if (tkf == 1) {
-    set_lds(k_enc_node_bwd<2, 1>, lds);
-    hipLaunchKernelGGL((k_enc_node_bwd<2, 1>), dim3(nslab), dim3(kBlock), lds, s, a);
+    SGNN_BWD_DISPATCH(H, enc->nlin, (launch_bwd(k_enc_node_bwd<TH_, 1, NL_>, nslab, lds, stream, a)));
   } else if (tkf == 2) {
-    set_lds(k_enc_node_bwd<2, 2>, lds);
-    hipLaunchKernelGGL((k_enc_node_bwd<2, 2>), dim3(nslab), dim3(kBlock), lds, s, a);
+    SGNN_BWD_DISPATCH(H, enc->nlin, (launch_bwd(k_enc_node_bwd<TH_, 2, NL_>, nslab, lds, stream, a)));
   } else {
     return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd: > 64 node features");
   }
@@ -1114,22 +1291,21 @@ extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64
 extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_stride,
                                      int32_t dim, float radius, const int32_t* rowptr,
                                      const int32_t* send, const int32_t* recv, int64_t n,
-                                     const float* yhat_save, const float* rstd_save,
-                                     const sgnn_mlp* enc, float* slab, int32_t nslab,
-                                     void* stream) {
+                                     const sgnn_saves* saves, const sgnn_mlp* enc, float* slab,
+                                     int32_t nslab, void* stream) {
   using namespace sgnn;
-  if (!enc || !de0t || !pos || !rowptr || !send || !recv || !yhat_save || !rstd_save || !slab ||
-      nslab < 1 || n <= 0)
+  if (!enc || !de0t || !pos || !rowptr || !send || !recv || !saves || !saves->yhat ||
+      !saves->rstd || !slab || nslab < 1 || n <= 0)
     return set_error(SGNN_ERR_INVALID, "encode_edges_bwd: bad arguments");
+  int st = check_bwd_mlp(enc, "encode_edges_bwd: encoder MLP");
+  if (st) return st;
+  if (enc->nlin == 3 && !saves->h2) return set_error(SGNN_ERR_INVALID, "encode_edges_bwd: saves->h2");
   const int H = enc->hidden;
-  CHECK_H(H, "encode_edges_bwd");
-  EncEdgeBwdArgs a{de0t, pos, pos_stride, dim, radius, rowptr, send, recv, n, yhat_save,
-                   rstd_save, enc->w1, enc->b1, enc->w2, enc->ln_g, slab,
-                   sgnn_bwd_slab_floats(SGNN_SLAB_ENC_EDGE, H, 0)};
-  const size_t lds = bwd_lds(SGNN_SLAB_ENC_EDGE, H, 0);
-  set_lds(k_enc_edge_bwd<2>, lds);
-  hipLaunchKernelGGL((k_enc_edge_bwd<2>), dim3(nslab), dim3(kBlock), lds,
-                     static_cast<hipStream_t>(stream), a);
+  EncEdgeBwdArgs a{de0t, pos, pos_stride, dim, radius, rowptr, send, recv, n, saves->h2,
+                   saves->yhat, saves->rstd, enc->w1, enc->b1, last_w(enc), mid_w(enc), enc->ln_g,
+                   slab, sgnn_bwd_slab_floats(SGNN_SLAB_ENC_EDGE, H, 0, enc->nlin)};
+  const size_t lds = bwd_lds(SGNN_SLAB_ENC_EDGE, H, 0, enc->nlin);
+  SGNN_BWD_DISPATCH(H, enc->nlin, (launch_bwd(k_enc_edge_bwd<TH_, NL_>, nslab, lds, stream, a)));
   return check_launch("encode_edges_bwd");
 }
 

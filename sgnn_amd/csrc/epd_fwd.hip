@@ -133,8 +133,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
     mfma_from_acc<TH, TKF>(hacc, W1, ldf, 0, xf);
     acc_relu<TH>(hacc);
     if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
-    f32x16 y[TH];
-    mlp_tail<TH, NL, TH>(y, hacc, a.wm, H, bm, W2, ldh, b2);
+    f32x16 y[TH], h2[TH];
+    mlp_tail<TH, NL, TH>(y, h2, hacc, a.wm, H, bm, W2, ldh, b2);
+    if (TRAIN && NL == 3 && valid) store_row_clayout<TH>(a.sv.h2 + i * H, h2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -207,8 +208,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
     mfma_step<TH>(hacc, W1, ld1, h, h ? f[1] : f[0]);
     mfma_step<TH>(hacc, W1, ld1, 2 + h, h ? f[3] : f[2]);
     acc_relu<TH>(hacc);
-    f32x16 y[TH];
-    mlp_tail<TH, NL, TH>(y, hacc, a.wm, H, bm, W2, ldh, b2);
+    f32x16 y[TH], h2[TH];
+    mlp_tail<TH, NL, TH>(y, h2, hacc, a.wm, H, bm, W2, ldh, b2);
+    if (TRAIN && NL == 3) store_tiled<TH>(a.sv.h2 + tile * (32 * H), h2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -290,8 +292,9 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     mfma_from_groups<TH, TH>(hacc, We, lde, 0, xg, a.e_scale);
     acc_relu<TH>(hacc);
     if (TRAIN) store_tiled<TH>(a.sv.h + tile * (32 * H), hacc);
-    f32x16 y[TH];
-    mlp_tail<TH, NL, TH>(y, hacc, a.wm, H, bm, W2, ldw2, b2);
+    f32x16 y[TH], h2[TH];
+    mlp_tail<TH, NL, TH>(y, h2, hacc, a.wm, H, bm, W2, ldw2, b2);
+    if (TRAIN && NL == 3) store_tiled<TH>(a.sv.h2 + tile * (32 * H), h2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -449,8 +452,9 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
     mfma_from_acc<TH, TH>(hacc, W1, ld2, H, x);
     acc_relu<TH>(hacc);
     if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
-    f32x16 y[TH];
-    mlp_tail<TH, NL, TH>(y, hacc, a.wm, H, bm, W2, ldw2, b2);
+    f32x16 y[TH], h2[TH];
+    mlp_tail<TH, NL, TH>(y, h2, hacc, a.wm, H, bm, W2, ldw2, b2);
+    if (TRAIN && NL == 3 && valid) store_row_clayout<TH>(a.sv.h2 + i * H, h2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
@@ -475,8 +479,9 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
       mfma_from_acc<TH, TH>(hd, Wa, lda, 0, x);
       acc_relu<TH>(hd);
       if (TRAIN && valid) store_row_clayout<TH>(a.sv.hd + i * H, hd);
-      f32x16 o[1];
-      mlp_tail<TH, NL, 1>(o, hd, a.wdm, H, bdm, Wb, ldh, bd2);
+      f32x16 o[1], hd2[TH];
+      mlp_tail<TH, NL, 1>(o, hd2, hd, a.wdm, H, bdm, Wb, ldh, bd2);
+      if (TRAIN && NL == 3 && valid) store_row_clayout<TH>(a.sv.hd2 + i * H, hd2);
       if (valid && h == 0) {  // lanes with h == 0 hold units 0..3 in registers 0..3
         const int D = a.dim;
         for (int c = 0; c <= D; ++c) a.pred[i * (D + 1) + c] = o[0][c];
@@ -535,33 +540,25 @@ bool want_saves(const sgnn_saves* sv) { return sv != nullptr && sv->yhat != null
 
 template <int TH, int TKF, int NL>
 void go_encode_nodes(bool train, unsigned grid, size_t lds, hipStream_t s, const EncNodeArgs& a) {
-  if constexpr (NL == 2) {
-    if (train) return launch1(k_encode_nodes<TH, TKF, true, 2>, grid, lds, s, a);
-  }
+  if (train) return launch1(k_encode_nodes<TH, TKF, true, NL>, grid, lds, s, a);
   launch1(k_encode_nodes<TH, TKF, false, NL>, grid, lds, s, a);
 }
 
 template <int TH, int NL>
 void go_encode_edges(bool train, unsigned grid, size_t lds, hipStream_t s, const EncEdgeArgs& a) {
-  if constexpr (NL == 2) {
-    if (train) return launch1(k_encode_edges<TH, true, 2>, grid, lds, s, a);
-  }
+  if (train) return launch1(k_encode_edges<TH, true, NL>, grid, lds, s, a);
   launch1(k_encode_edges<TH, false, NL>, grid, lds, s, a);
 }
 
 template <int TH, int NL>
 void go_edge_layer(bool train, unsigned grid, size_t lds, hipStream_t s, const EdgeLayerArgs& a) {
-  if constexpr (NL == 2) {
-    if (train) return launch1(k_edge_layer<TH, true, 2>, grid, lds, s, a);
-  }
+  if (train) return launch1(k_edge_layer<TH, true, NL>, grid, lds, s, a);
   launch1(k_edge_layer<TH, false, NL>, grid, lds, s, a);
 }
 
 template <int TH, int MODE, int NL>
 void go_node_layer(bool train, unsigned grid, size_t lds, hipStream_t s, const NodeLayerArgs& a) {
-  if constexpr (NL == 2) {
-    if (train) return launch1(k_node_layer<TH, MODE, true, 2>, grid, lds, s, a);
-  }
+  if (train) return launch1(k_node_layer<TH, MODE, true, NL>, grid, lds, s, a);
   launch1(k_node_layer<TH, MODE, false, NL>, grid, lds, s, a);
 }
 
@@ -579,9 +576,8 @@ extern "C" int64_t sgnn_edge_latent_floats(int64_t edge_cap, int32_t hidden) {
     else { constexpr int TH_ = 4, NL_ = 3; CALL; }                        \
   } while (0)
 
-static int check_train(bool train, const sgnn_mlp* m, const char* what) {
-  if (train && m->nlin != 2)
-    return sgnn::set_error(SGNN_ERR_UNSUPPORTED, what);
+static int check_train(bool train, const sgnn_mlp* m, const sgnn_saves* sv, const char* what) {
+  if (train && m->nlin == 3 && !sv->h2) return sgnn::set_error(SGNN_ERR_INVALID, what);
   return SGNN_OK;
 }
 
@@ -607,7 +603,7 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
                 feat, enc->w1, enc->b1, last_w(enc), last_b(enc), enc->ln_g, enc->ln_b,
                 mid_w(enc), mid_b(enc), wall_max, wall_div, edge0->w1, edge0->b1, x0, u, v, {}};
   const bool train = want_saves(saves);
-  if ((st = check_train(train, enc, "encode_nodes: training saves need nmlp_layers = 1"))) return st;
+  if ((st = check_train(train, enc, saves, "encode_nodes: nmlp_layers = 2 training needs saves->h2"))) return st;
   if (train) {
     if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "encode_nodes: saves");
     a.sv = *saves;
@@ -644,7 +640,7 @@ extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t d
   EncEdgeArgs a{pos, pos_stride, dim, radius, rowptr, send, recv, n, enc->w1, enc->b1,
                 last_w(enc), last_b(enc), enc->ln_g, enc->ln_b, e0t, {}, mid_w(enc), mid_b(enc)};
   const bool train = want_saves(saves);
-  if ((st = check_train(train, enc, "encode_edges: training saves need nmlp_layers = 1"))) return st;
+  if ((st = check_train(train, enc, saves, "encode_edges: nmlp_layers = 2 training needs saves->h2"))) return st;
   if (train) {
     if (!saves->rstd) return set_error(SGNN_ERR_INVALID, "encode_edges: saves");
     a.sv = *saves;
@@ -672,7 +668,7 @@ extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t,
                   last_b(edge_fn), edge_fn->ln_g, edge_fn->ln_b, agg, cin, cout, {},
                   mid_w(edge_fn), mid_b(edge_fn)};
   const bool train = want_saves(saves);
-  if ((st = check_train(train, edge_fn, "edge_layer: training saves need nmlp_layers = 1"))) return st;
+  if ((st = check_train(train, edge_fn, saves, "edge_layer: nmlp_layers = 2 training needs saves->h2"))) return st;
   if (train) {
     if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "edge_layer: saves");
     a.sv = *saves;
@@ -697,9 +693,10 @@ static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode
   a.wm = mid_w(node_fn); a.bm = mid_b(node_fn);
   a.g = node_fn->ln_g; a.bb = node_fn->ln_b;
   const bool train = want_saves(saves);
-  if ((st = check_train(train, node_fn, "node_layer: training saves need nmlp_layers = 1"))) return st;
+  if ((st = check_train(train, node_fn, saves, "node_layer: nmlp_layers = 2 training needs saves->h2"))) return st;
   if (train) {
-    if (!saves->h || !saves->rstd || !saves->agg || (mode == 1 && (!saves->hd || !a.x_out)))
+    if (!saves->h || !saves->rstd || !saves->agg || (mode == 1 && (!saves->hd || !a.x_out)) ||
+        (mode == 1 && dec_nlin == 3 && !saves->hd2))
       return set_error(SGNN_ERR_INVALID, "node_layer: saves");
     a.sv = *saves;
   }

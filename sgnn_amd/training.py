@@ -47,6 +47,175 @@ class FlatParams:
         self.numel = total
 
 
+W_PARTIALS = 4  # per-wave partial rows of every slab vector (kWaves in epd_bwd.hip)
+
+
+def _lin(prefix: str, nl: int, has_ln: bool):
+    """Parameter names of one reference MLP (graph_network.py:7-45 build_mlp,
+    optionally wrapped Sequential(mlp, LayerNorm)): (first, middle, last, ln)."""
+    mp = prefix + ("0." if has_ln else "")
+    first = mp + "NN-0."
+    mid = mp + "NN-1." if nl == 3 else None
+    last = mp + f"NN-{nl - 1}."
+    ln = prefix + "1." if has_ln else None
+    return first, mid, last, ln
+
+
+class GradLayout:
+    """Slab -> parameter-gradient reduction table (include/sgnn.h slab layouts),
+    uploaded once per (slab arena, gradient buffers)."""
+
+    def __init__(self, H: int, nl: int, feat: int, dim: int, arena: torch.Tensor,
+                 slab_off: Dict[tuple, int], slab_floats: Dict[int, int], nslab_of: Dict[int, int]):
+        self.H, self.nl, self.feat, self.dim = H, nl, feat, dim
+        self.arena, self.slab_off, self.slab_floats, self.nslab_of = arena, slab_off, slab_floats, nslab_of
+        self.descs: List[SgnnReduceDesc] = []
+
+    def add(self, kind, k, offset, dst, nrows, ncols, src_ld, dst_ld=None, nrep=1, rep_stride=0,
+            scale=1.0, dst_off=0):
+        d = SgnnReduceDesc()
+        d.src = self.arena.data_ptr() + 4 * self.slab_off[(kind, k)]
+        d.dst = dst.data_ptr() + 4 * dst_off
+        d.slab_stride = self.slab_floats[kind]
+        d.offset = offset
+        d.rep_stride = rep_stride
+        d.nslab, d.nrep, d.src_ld = self.nslab_of[kind], nrep, src_ld
+        d.nrows, d.ncols = nrows, ncols
+        d.dst_ld = dst_ld if dst_ld is not None else ncols
+        d.accumulate = 0
+        d.scale = scale
+        self.descs.append(d)
+
+    def vec(self, kind, k, off, dst, n=None, width=None):
+        """A [W][width] per-wave partial vector -> dst[:n]."""
+        H = self.H
+        width = width or H
+        self.add(kind, k, off, dst, 1, n or width, width, nrep=W_PARTIALS, rep_stride=width)
+
+    def nmat(self, kind: int) -> int:
+        H, nl = self.H, self.nl
+        mid = H * H if nl == 3 else 0
+        fpad = 32 * ((self.feat + 31) // 32)
+        return {_hip.SLAB_EDGE: 2 * H * H + mid, _hip.SLAB_NODE: 3 * H * H + mid,
+                _hip.SLAB_UV: 2 * H * H, _hip.SLAB_DECODER: 32 * H + H * H + mid,
+                _hip.SLAB_ENC_NODE: H * H + H * fpad + mid,
+                _hip.SLAB_ENC_EDGE: H * H + H * 32 + mid}[kind]
+
+    # -- one reference MLP per call -------------------------------------------------
+    def enc_node(self, g, prefix):
+        H, nl, W = self.H, self.nl, W_PARTIALS
+        K = _hip.SLAB_ENC_NODE
+        fpad = 32 * ((self.feat + 31) // 32)
+        first, mid, last, ln = _lin(prefix, nl, True)
+        vb = self.nmat(K)
+        self.add(K, 0, H * H, g(first + "weight"), H, self.feat, fpad)
+        self.add(K, 0, 0, g(last + "weight"), H, H, H)
+        if mid:
+            self.add(K, 0, H * H + H * fpad, g(mid + "weight"), H, H, H)
+        self._vecs5(K, 0, vb, g, first, last, ln, mid)
+
+    def enc_edge(self, g, prefix, k=0):
+        H, nl = self.H, self.nl
+        K = _hip.SLAB_ENC_EDGE
+        first, mid, last, ln = _lin(prefix, nl, True)
+        vb = self.nmat(K)
+        self.add(K, k, H * H, g(first + "weight"), H, self.dim + 1, 32)
+        self.add(K, k, 0, g(last + "weight"), H, H, H)
+        if mid:
+            self.add(K, k, H * H + H * 32, g(mid + "weight"), H, H, H)
+        self._vecs5(K, k, vb, g, first, last, ln, mid)
+
+    def _vecs5(self, K, k, vb, g, first, last, ln, mid):
+        H, W = self.H, W_PARTIALS
+        self.vec(K, k, vb, g(first + "bias"))
+        self.vec(K, k, vb + W * H, g(last + "bias"))
+        self.vec(K, k, vb + 2 * W * H, g(ln + "weight"))
+        self.vec(K, k, vb + 3 * W * H, g(ln + "bias"))
+        if mid:
+            self.vec(K, k, vb + 4 * W * H, g(mid + "bias"))
+
+    def interaction(self, g, prefix, k, e_scale, slot=None):
+        """edge_fn (EDGE + UV slabs of layer slot) and node_fn (NODE slab)."""
+        H, nl, W = self.H, self.nl, W_PARTIALS
+        slot = k if slot is None else slot
+        first, mid, last, ln = _lin(prefix + "edge_fn.", nl, True)
+        E, U, N = _hip.SLAB_EDGE, _hip.SLAB_UV, _hip.SLAB_NODE
+        # edge MLP first Linear: [x_i | x_j] from UV, [e] from EDGE (x 2^k)
+        self.add(U, slot, 0, g(first + "weight"), H, 2 * H, 2 * H, dst_ld=3 * H)
+        self.add(E, slot, H * H, g(first + "weight"), H, H, H, dst_ld=3 * H, scale=float(e_scale),
+                 dst_off=2 * H)
+        self.vec(U, slot, 2 * H * H, g(first + "bias"))
+        self.add(E, slot, 0, g(last + "weight"), H, H, H)
+        vb = self.nmat(E)
+        self.vec(E, slot, vb, g(last + "bias"))
+        self.vec(E, slot, vb + W * H, g(ln + "weight"))
+        self.vec(E, slot, vb + 2 * W * H, g(ln + "bias"))
+        if mid:
+            self.add(E, slot, 2 * H * H, g(mid + "weight"), H, H, H)
+            self.vec(E, slot, vb + 3 * W * H, g(mid + "bias"))
+        first, mid, last, ln = _lin(prefix + "node_fn.", nl, True)
+        self.add(N, slot, H * H, g(first + "weight"), H, 2 * H, 2 * H)
+        self.add(N, slot, 0, g(last + "weight"), H, H, H)
+        if mid:
+            self.add(N, slot, 3 * H * H, g(mid + "weight"), H, H, H)
+        self._vecs5(N, slot, self.nmat(N), g, first, last, ln, mid)
+
+    def decoder(self, g, prefix, loss_out):
+        H, nl, W = self.H, self.nl, W_PARTIALS
+        D = _hip.SLAB_DECODER
+        first, mid, last, _ = _lin(prefix, nl, False)
+        d1 = self.dim + 1
+        vb = self.nmat(D)
+        self.add(D, 0, 32 * H, g(first + "weight"), H, H, H)
+        self.add(D, 0, 0, g(last + "weight"), d1, H, H)
+        if mid:
+            self.add(D, 0, 32 * H + H * H, g(mid + "weight"), H, H, H)
+        self.vec(D, 0, vb, g(last + "bias"), n=d1, width=32)
+        self.vec(D, 0, vb + W * 32, g(first + "bias"))
+        self.vec(D, 0, vb + W * 32 + W * H, loss_out, n=5, width=8)
+        if mid:
+            self.vec(D, 0, vb + W * 32 + W * H + W * 8, g(mid + "bias"))
+
+    def upload(self, device):
+        descs = self.descs
+        arr = (SgnnReduceDesc * len(descs))(*descs)
+        raw = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
+                               dtype=torch.uint8)
+        starts, nb = [], 0
+        for d in descs:
+            starts.append(nb)
+            nb += (d.nrows * d.ncols + 31) // 32
+        return raw.to(device), torch.tensor(starts, dtype=torch.int32).to(device), len(descs), nb
+
+
+class SlabArena:
+    """One fp32 arena holding every backward kernel's per-workgroup partial slabs."""
+
+    def __init__(self, H: int, nl: int, feat: int, keys: List[tuple], nslab_of: Dict[int, int],
+                 device: torch.device):
+        L = lib()
+        self.slab_floats = {k: int(L.sgnn_bwd_slab_floats(k, H, feat, nl)) for k in range(6)}
+        self.nslab_of = nslab_of
+        self.slab_off: Dict[Tuple[int, int], int] = {}
+        off = 0
+        for key in keys:
+            self.slab_off[key] = off
+            off += nslab_of[key[0]] * self.slab_floats[key[0]]
+        self.arena = torch.empty(max(off, 1), dtype=torch.float32, device=device)
+
+    def ptr(self, kind: int, k: int = 0) -> int:
+        return self.arena.data_ptr() + 4 * self.slab_off[(kind, k)]
+
+    def layout(self, H, nl, feat, dim) -> GradLayout:
+        return GradLayout(H, nl, feat, dim, self.arena, self.slab_off, self.slab_floats, self.nslab_of)
+
+
+def nslab_table(nslab: int) -> Dict[int, int]:
+    node_ns = max(1, min(nslab, NODE_NSLAB))
+    return {_hip.SLAB_EDGE: nslab, _hip.SLAB_ENC_EDGE: nslab, _hip.SLAB_NODE: node_ns,
+            _hip.SLAB_UV: node_ns, _hip.SLAB_DECODER: node_ns, _hip.SLAB_ENC_NODE: node_ns}
+
+
 class TrainWorkspace:
     """Forward saves + backward buffers + weight-gradient slabs for one shape."""
 
@@ -54,27 +223,32 @@ class TrainWorkspace:
                  device: torch.device, nslab: int = DEFAULT_NSLAB):
         L = lib()
         H, nl = epd.latent_dim, epd.nlayers
+        self.nlin = epd.nmlp_layers + 1
         self.H, self.L, self.n, self.T, self.dim, self.nslab = H, nl, n, T, dim, nslab
-        node_ns = max(1, min(nslab, NODE_NSLAB))
-        self.nslab_of = {_hip.SLAB_EDGE: nslab, _hip.SLAB_ENC_EDGE: nslab, _hip.SLAB_NODE: node_ns,
-                         _hip.SLAB_UV: node_ns, _hip.SLAB_DECODER: node_ns, _hip.SLAB_ENC_NODE: node_ns}
+        self.nslab_of = nslab_table(nslab)
         self.feat = epd.nnode_in
         self.f = engine.StepWorkspace(n, T, dim, H, K, loop, device)
         cap = self.f.edge_cap
         tl = int(L.sgnn_edge_latent_floats(cap, H))
         f32 = dict(dtype=torch.float32, device=device)
         e = lambda *s: torch.empty(*s, **f32)
+        two = self.nlin == 3
         self.enc_h, self.enc_yh, self.enc_rstd = e(n, H), e(n, H), e(n)
+        self.enc_h2 = e(n, H) if two else None
         self.ee_yh, self.ee_rstd = e(tl), e(cap)
+        self.ee_h2 = e(tl) if two else None
         self.e_h = [e(tl) for _ in range(nl)]
+        self.e_h2 = [e(tl) if two else None for _ in range(nl)]
         self.e_yh = [e(tl) for _ in range(nl)]
         self.e_rstd = [e(cap) for _ in range(nl)]
         self.n_agg = [e(n, H) for _ in range(nl)]
         self.n_h = [e(n, H) for _ in range(nl)]
+        self.n_h2 = [e(n, H) if two else None for _ in range(nl)]
         self.n_yh = [e(n, H) for _ in range(nl)]
         self.n_rstd = [e(n) for _ in range(nl)]
         self.xs = [e(n, H) for _ in range(nl + 1)]
         self.hd = e(n, H)
+        self.hd2 = e(n, H) if two else None
         self.pred = e(n, dim + 1)
         self.next_scratch = e(n, dim)
         self.g, self.dxp, self.dagg, self.du = e(n, H), e(n, H), e(n, H), e(n, H)
@@ -85,132 +259,47 @@ class TrainWorkspace:
         self.tperm = torch.empty(cap, **i32)
         self.tws = torch.empty(int(L.sgnn_transpose_workspace_bytes(n, cap)) + 256, dtype=torch.uint8,
                                device=device)
-        # slab arena
-        self.slab_floats = {k: int(L.sgnn_bwd_slab_floats(k, H, self.feat)) for k in range(6)}
-        self.slab_off: Dict[Tuple[int, int], int] = {}
-        off = 0
         keys = [(_hip.SLAB_DECODER, 0)] + [(_hip.SLAB_NODE, k) for k in range(nl)] + \
                [(_hip.SLAB_EDGE, k) for k in range(nl)] + [(_hip.SLAB_UV, k) for k in range(nl)] + \
                [(_hip.SLAB_ENC_NODE, 0), (_hip.SLAB_ENC_EDGE, 0)]
-        for key in keys:
-            self.slab_off[key] = off
-            off += self.nslab_of[key[0]] * self.slab_floats[key[0]]
-        self.arena = torch.empty(off, **f32)
+        self.slabs = SlabArena(H, self.nlin, self.feat, keys, self.nslab_of, device)
+        self.arena = self.slabs.arena
         self.loss_out = torch.zeros(8, **f32)
         self._descs_key = None
-        self._descs_dev = None
-        self._ndesc = 0
-        self._max_elems = 1
 
     def slab(self, kind: int, k: int = 0) -> int:
-        return self.arena.data_ptr() + 4 * self.slab_off[(kind, k)]
+        return self.slabs.ptr(kind, k)
 
     def tws_ptr(self) -> int:
         return (self.tws.data_ptr() + 255) & ~255
 
-    # ---------------------------------------------------------------- reduce
     def descriptors(self, epd: nn.Module, grads: Dict[str, torch.Tensor]) -> None:
         """Build the slab -> parameter-gradient reduction table (device copy)."""
         key = tuple(g.data_ptr() for g in grads.values())
         if key == self._descs_key:
             return
-        H, nl, ns = self.H, self.L, self.nslab
-        W = 4
-        descs: List[SgnnReduceDesc] = []
-
-        def add(kind, k, offset, dst, nrows, ncols, src_ld, dst_ld=None, nrep=1, rep_stride=0,
-                scale=1.0, dst_off=0):
-            d = SgnnReduceDesc()
-            d.src = self.arena.data_ptr() + 4 * self.slab_off[(kind, k)]
-            d.dst = dst.data_ptr() + 4 * dst_off
-            d.slab_stride = self.slab_floats[kind]
-            d.offset = offset
-            d.rep_stride = rep_stride
-            d.nslab, d.nrep, d.src_ld = self.nslab_of[kind], nrep, src_ld
-            d.nrows, d.ncols = nrows, ncols
-            d.dst_ld = dst_ld if dst_ld is not None else ncols
-            d.accumulate = 0
-            d.scale = scale
-            descs.append(d)
-
         pre = "_encode_process_decode."
         g = lambda name: grads[pre + name]
-        # encoder node MLP  (slab ENC_NODE: dW2 | dW1[H][fpad] | db1 db2 dg db)
-        fpad = 32 * ((self.feat + 31) // 32)
-        vb = H * H + H * fpad
-        e = "_encoder.node_fn."
-        add(_hip.SLAB_ENC_NODE, 0, H * H, g(e + "0.NN-0.weight"), H, self.feat, fpad)
-        add(_hip.SLAB_ENC_NODE, 0, vb, g(e + "0.NN-0.bias"), 1, H, H, nrep=W, rep_stride=H)
-        add(_hip.SLAB_ENC_NODE, 0, 0, g(e + "0.NN-1.weight"), H, H, H)
-        add(_hip.SLAB_ENC_NODE, 0, vb + W * H, g(e + "0.NN-1.bias"), 1, H, H, nrep=W, rep_stride=H)
-        add(_hip.SLAB_ENC_NODE, 0, vb + 2 * W * H, g(e + "1.weight"), 1, H, H, nrep=W, rep_stride=H)
-        add(_hip.SLAB_ENC_NODE, 0, vb + 3 * W * H, g(e + "1.bias"), 1, H, H, nrep=W, rep_stride=H)
-        # encoder edge MLP
-        vb = H * H + H * 32
-        e = "_encoder.edge_fn."
-        add(_hip.SLAB_ENC_EDGE, 0, H * H, g(e + "0.NN-0.weight"), H, self.dim + 1, 32)
-        add(_hip.SLAB_ENC_EDGE, 0, vb, g(e + "0.NN-0.bias"), 1, H, H, nrep=W, rep_stride=H)
-        add(_hip.SLAB_ENC_EDGE, 0, 0, g(e + "0.NN-1.weight"), H, H, H)
-        add(_hip.SLAB_ENC_EDGE, 0, vb + W * H, g(e + "0.NN-1.bias"), 1, H, H, nrep=W, rep_stride=H)
-        add(_hip.SLAB_ENC_EDGE, 0, vb + 2 * W * H, g(e + "1.weight"), 1, H, H, nrep=W, rep_stride=H)
-        add(_hip.SLAB_ENC_EDGE, 0, vb + 3 * W * H, g(e + "1.bias"), 1, H, H, nrep=W, rep_stride=H)
-        for k in range(nl):
-            p = f"_processor.gnn_stacks.{k}."
-            # edge MLP first Linear: [x_i | x_j] from UV slab, [e] from EDGE slab (x 2^k)
-            add(_hip.SLAB_UV, k, 0, g(p + "edge_fn.0.NN-0.weight"), H, 2 * H, 2 * H, dst_ld=3 * H)
-            add(_hip.SLAB_EDGE, k, H * H, g(p + "edge_fn.0.NN-0.weight"), H, H, H, dst_ld=3 * H,
-                scale=float(2.0 ** k), dst_off=2 * H)
-            add(_hip.SLAB_UV, k, 2 * H * H, g(p + "edge_fn.0.NN-0.bias"), 1, H, H, nrep=W, rep_stride=H)
-            add(_hip.SLAB_EDGE, k, 0, g(p + "edge_fn.0.NN-1.weight"), H, H, H)
-            vb = 2 * H * H
-            add(_hip.SLAB_EDGE, k, vb, g(p + "edge_fn.0.NN-1.bias"), 1, H, H, nrep=W, rep_stride=H)
-            add(_hip.SLAB_EDGE, k, vb + W * H, g(p + "edge_fn.1.weight"), 1, H, H, nrep=W, rep_stride=H)
-            add(_hip.SLAB_EDGE, k, vb + 2 * W * H, g(p + "edge_fn.1.bias"), 1, H, H, nrep=W,
-                rep_stride=H)
-            vb = 3 * H * H
-            add(_hip.SLAB_NODE, k, H * H, g(p + "node_fn.0.NN-0.weight"), H, 2 * H, 2 * H)
-            add(_hip.SLAB_NODE, k, vb, g(p + "node_fn.0.NN-0.bias"), 1, H, H, nrep=W, rep_stride=H)
-            add(_hip.SLAB_NODE, k, 0, g(p + "node_fn.0.NN-1.weight"), H, H, H)
-            add(_hip.SLAB_NODE, k, vb + W * H, g(p + "node_fn.0.NN-1.bias"), 1, H, H, nrep=W,
-                rep_stride=H)
-            add(_hip.SLAB_NODE, k, vb + 2 * W * H, g(p + "node_fn.1.weight"), 1, H, H, nrep=W,
-                rep_stride=H)
-            add(_hip.SLAB_NODE, k, vb + 3 * W * H, g(p + "node_fn.1.bias"), 1, H, H, nrep=W,
-                rep_stride=H)
-        # decoder (slab DECODER: dW2[32][H] | dW1[H][H] | db2[W][32] | db1[W][H] | loss[W][8])
-        d1 = self.dim + 1
-        vb = 32 * H + H * H
-        add(_hip.SLAB_DECODER, 0, 32 * H, g("_decoder.node_fn.NN-0.weight"), H, H, H)
-        add(_hip.SLAB_DECODER, 0, vb + W * 32, g("_decoder.node_fn.NN-0.bias"), 1, H, H, nrep=W,
-            rep_stride=H)
-        add(_hip.SLAB_DECODER, 0, 0, g("_decoder.node_fn.NN-1.weight"), d1, H, H)
-        add(_hip.SLAB_DECODER, 0, vb, g("_decoder.node_fn.NN-1.bias"), 1, d1, 32, nrep=W,
-            rep_stride=32)
-        add(_hip.SLAB_DECODER, 0, vb + W * 32 + W * H, self.loss_out, 1, 5, 8, nrep=W, rep_stride=8)
-        arr = (SgnnReduceDesc * len(descs))(*descs)
-        raw = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(arr), ctypes.sizeof(arr))),
-                               dtype=torch.uint8)
-        self._descs_dev = raw.to(self.arena.device)
-        self._ndesc = len(descs)
-        starts, nb = [], 0
-        for d in descs:
-            starts.append(nb)
-            nb += (d.nrows * d.ncols + 31) // 32
-        self._block_start = torch.tensor(starts, dtype=torch.int32).to(self.arena.device)
-        self._nblocks = nb
+        lay = self.slabs.layout(self.H, self.nlin, self.feat, self.dim)
+        lay.enc_node(g, "_encoder.node_fn.")
+        lay.enc_edge(g, "_encoder.edge_fn.")
+        for k in range(self.L):
+            lay.interaction(g, f"_processor.gnn_stacks.{k}.", k, 2.0 ** k)
+        lay.decoder(g, "_decoder.node_fn.", self.loss_out)
+        self._descs_dev, self._block_start, self._ndesc, self._nblocks = lay.upload(self.arena.device)
         self._descs_key = key
 
 
-def _saves(h=None, yhat=None, rstd=None, agg=None, hd=None) -> SgnnSaves:
+def _saves(h=None, yhat=None, rstd=None, agg=None, hd=None, h2=None, hd2=None) -> SgnnSaves:
     p = engine._ptr
-    return SgnnSaves(h=p(h), yhat=p(yhat), rstd=p(rstd), agg=p(agg), hd=p(hd))
+    return SgnnSaves(h=p(h), yhat=p(yhat), rstd=p(rstd), agg=p(agg), hd=p(hd), h2=p(h2), hd2=p(hd2))
 
 
 def check_trainable(epd: nn.Module, nparticle_types: int) -> None:
-    if epd.latent_dim != 64:
-        raise NotImplementedError("HIP training path: latent_dim must be 64 in this build")
-    if epd.nmlp_layers != 1:
-        raise NotImplementedError("HIP training path: nmlp_layers must be 1")
+    if epd.latent_dim not in (64, 128):
+        raise NotImplementedError("HIP training path: latent_dim must be 64 or 128")
+    if epd.nmlp_layers not in (1, 2):
+        raise NotImplementedError("HIP training path: nmlp_layers must be 1 or 2")
     if nparticle_types > 1:
         raise NotImplementedError("HIP training path: particle-type embeddings (nparticle_types > 1)")
 
@@ -243,19 +332,19 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
     s = stream_ptr(inp.pos_seq.device)
     pos = inp.pos_seq
     engine.radius_graph(ws, pos, (T - 1) * d, T * d, inp.ex_ptr, inp.n_ex, radius)
-    sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd)
+    sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2)
     check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, 0, 0, 0, 0, inp.vel_mean.data_ptr(),
                               inp.vel_std.data_ptr(), float(radius), 1.0, ctypes.byref(pk.enc_node),
                               ctypes.byref(pk.edge[0]), tw.xs[0].data_ptr(), ws.u.data_ptr(),
                               ws.v.data_ptr(), ctypes.byref(sv), s), "sgnn_encode_nodes")
-    sv = _saves(yhat=tw.ee_yh, rstd=tw.ee_rstd)
+    sv = _saves(yhat=tw.ee_yh, rstd=tw.ee_rstd, h2=tw.ee_h2)
     check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius),
                               ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
                               ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(),
                               ctypes.byref(sv), s), "sgnn_encode_edges")
     nl = len(pk.edge)
     for k in range(nl):
-        sv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k])
+        sv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k], h2=tw.e_h2[k])
         with _Timer(timers, "k_edge_layer(train)"):
           check(L.sgnn_edge_layer(ws.u.data_ptr(), ws.v.data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
                                 ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
@@ -263,14 +352,15 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
                                 ws.cin.data_ptr(), ws.cout.data_ptr(), ctypes.byref(sv), s),
               "sgnn_edge_layer")
         if k < nl - 1:
-            sv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k])
+            sv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], h2=tw.n_h2[k])
             check(L.sgnn_node_layer(tw.xs[k].data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
                                     ws.cout.data_ptr(), ws.rowptr.data_ptr(), n,
                                     ctypes.byref(pk.node[k]), ctypes.byref(pk.edge[k + 1]),
                                     tw.xs[k + 1].data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(),
                                     ctypes.byref(sv), s), "sgnn_node_layer")
         else:
-            sv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], hd=tw.hd)
+            sv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], hd=tw.hd,
+                        h2=tw.n_h2[k], hd2=tw.hd2)
             check(L.sgnn_node_layer_decode(tw.xs[k].data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
                                            ws.cout.data_ptr(), ws.rowptr.data_ptr(), n,
                                            ctypes.byref(pk.node[k]), ctypes.byref(pk.dec),
@@ -302,19 +392,20 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
     check(L.sgnn_decoder_loss_bwd(tw.pred.data_ptr(), inp.pos_seq.data_ptr(), p(next_pos), p(noise),
                                   p(next_strain), inp.acc_mean.data_ptr(), inp.acc_std.data_ptr(), n, T,
                                   d, float(w_pos), float(w_strain), float(inv_count), p(dpred),
-                                  tw.hd.data_ptr(), tw.xs[tw.L].data_ptr(), ctypes.byref(pk.dec),
+                                  ctypes.byref(_saves(hd=tw.hd, hd2=tw.hd2)), tw.xs[tw.L].data_ptr(),
+                                  ctypes.byref(pk.dec),
                                   tw.g.data_ptr(), tw.slab(_hip.SLAB_DECODER), tw.nslab_of[_hip.SLAB_DECODER], s),
           "sgnn_decoder_loss_bwd")
     for k in range(tw.L - 1, -1, -1):
-        check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, tw.n_yh[k].data_ptr(), tw.n_rstd[k].data_ptr(),
-                                    tw.n_h[k].data_ptr(), tw.n_agg[k].data_ptr(), tw.xs[k].data_ptr(),
+        nsv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], h2=tw.n_h2[k])
+        check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, ctypes.byref(nsv), tw.xs[k].data_ptr(),
                                     ctypes.byref(pk.node[k]), tw.dagg.data_ptr(), tw.dxp.data_ptr(),
                                     tw.slab(_hip.SLAB_NODE, k), tw.nslab_of[_hip.SLAB_NODE], s),
               "sgnn_node_layer_bwd")
         with _Timer(timers, "k_edge_bwd"):
+          esv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k], h2=tw.e_h2[k])
           check(L.sgnn_edge_layer_bwd(tw.dagg.data_ptr(), ws.rowptr.data_ptr(), ws.send.data_ptr(),
-                                    ws.recv.data_ptr(), n, tw.e_h[k].data_ptr(), tw.e_yh[k].data_ptr(),
-                                    tw.e_rstd[k].data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
+                                    ws.recv.data_ptr(), n, ctypes.byref(esv), ws.e0t.data_ptr(), float(2.0 ** k),
                                     ctypes.byref(pk.edge[k]), tw.du.data_ptr(), ws.cin.data_ptr(),
                                     ws.cout.data_ptr(), tw.dh_rows.data_ptr(), tw.de0t.data_ptr(),
                                     int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), tw.nslab_of[_hip.SLAB_EDGE], s),
@@ -325,14 +416,16 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                             tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV], s),
               "sgnn_uv_bwd")
     check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d,
-                                  inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius),
-                                  tw.enc_h.data_ptr(), tw.enc_yh.data_ptr(), tw.enc_rstd.data_ptr(),
+                                  inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius), 1.0,
+                                  ctypes.byref(_saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd,
+                                                      h2=tw.enc_h2)),
                                   ctypes.byref(pk.enc_node), tw.slab(_hip.SLAB_ENC_NODE),
                                   tw.nslab_of[_hip.SLAB_ENC_NODE], s),
           "sgnn_encode_nodes_bwd")
     check(L.sgnn_encode_edges_bwd(tw.de0t.data_ptr(), inp.pos_seq.data_ptr() + 4 * (T - 1) * d, T * d,
                                   d, float(radius), ws.rowptr.data_ptr(), ws.send.data_ptr(),
-                                  ws.recv.data_ptr(), n, tw.ee_yh.data_ptr(), tw.ee_rstd.data_ptr(),
+                                  ws.recv.data_ptr(), n,
+                                  ctypes.byref(_saves(yhat=tw.ee_yh, rstd=tw.ee_rstd, h2=tw.ee_h2)),
                                   ctypes.byref(pk.enc_edge), tw.slab(_hip.SLAB_ENC_EDGE),
                                   tw.nslab_of[_hip.SLAB_ENC_EDGE], s),
           "sgnn_encode_edges_bwd")

@@ -119,3 +119,39 @@ def test_gradients_against_oracle_autograd(nx, ny, radius, n_ex):
         if state[k].grad is not None:
             worst = max(worst, _grad_close(p.grad.cpu().numpy(), state[k].grad.numpy(), k, rel=5e-4))
     print(f"{nx}x{ny} r={radius}: worst relative grad error {worst:.3e}")
+
+
+@pytest.mark.parametrize("dim,H,nmlp", [(2, 64, 2), (2, 128, 1), (3, 128, 2)])
+def test_wide_and_deep_mlp_gradients_against_oracle(dim, H, nmlp):
+    """H = 128 (weights read from L2) and nmlp_layers = 2 (3-Linear MLPs, middle
+    Linear backward) through the fused backward, vs oracle autograd."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import synthetic
+    from sgnn_amd.learned_simulator import LearnedSimulator
+    from sgnn_amd.train import Trainer
+    T, L, R = 6, 3, 0.75
+    base = synthetic.lattice_2d(30, 20) if dim == 2 else synthetic.lattice_3d(10, 8, 6)
+    seq = synthetic.trajectory(base, T + 1, seed=5)
+    n = seq.shape[0]
+    st = synthetic.normalization_stats(dim, noise_std=0.02)
+    stats = {k: {kk: torch.from_numpy(vv) for kk, vv in v.items()} for k, v in st.items()}
+    torch.manual_seed(11)
+    sim = LearnedSimulator(dim, (T - 1) * dim + 1, dim + 1, H, L, nmlp, H, R, stats, 1, 9)
+    state = {k: v.detach().clone().requires_grad_(True) for k, v in sim.state_dict().items()}
+    pos, nxt = torch.from_numpy(seq[:, :T]), torch.from_numpy(seq[:, T])
+    strain = torch.from_numpy(np.random.default_rng(2).normal(0, 1, n).astype(np.float32))
+    noise = O.random_walk_noise(pos, 0.02, generator=torch.Generator().manual_seed(3))
+    osim = O.OracleSimulator(state, dim, L, R, stats, 1, nmlp_layers=nmlp)
+    pa, ta, ps = osim.predict_accelerations(nxt, noise, pos, [n], torch.zeros(n, dtype=torch.long))
+    ref_loss = O.training_loss(pa, ta, ps, strain)
+    ref_loss.backward()
+    sim = sim.cuda()
+    tr = Trainer(sim, lr_init=1e-3)
+    out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), [n], noise=noise.cuda())
+    torch.cuda.synchronize()
+    assert abs(float(out["loss"]) - ref_loss.item()) <= 2e-5 * abs(ref_loss.item())
+    worst = 0.0
+    for k, p in sim.named_parameters():
+        if state[k].grad is not None:
+            worst = max(worst, _grad_close(p.grad.cpu().numpy(), state[k].grad.numpy(), k, rel=5e-4))
+    print(f"dim={dim} H={H} nmlp={nmlp}: worst relative grad error {worst:.3e}")
