@@ -1,0 +1,302 @@
+"""Multi-scale training step on the HIP kernels (multi_scale_train.py:140-186:
+noise -> MultiScaleSimulator.predict_accelerations -> loss -> backward ->
+Adam -> LR decay), whole-graph data parallel over RCCL like the
+single-scale Trainer (sgnn_amd/train.py).
+
+Backward order (reverse of ms_engine.forward_step):
+  prediction head + loss        -> g = dL/dx_{B}
+  block b = B-1 .. 0 (M2G, M2M L-1 .. 0, G2M):
+     node_bwd(b) -> dagg, dx' ; edge_bwd(b) -> dU, dh rows, dE0[kind] ;
+     uv_bwd(b) -> g = dL/dx_b
+  grid encoder backward, three edge-encoder backwards (one per edge type)
+  slab reduction -> flat gradient
+The edge latent of M2M block k is 2^k e0_m2m, so dE0_m2m accumulates
+2^k W1e^T dh over the M2M blocks; g2m / m2g latents feed one block each.
+Sender-sorted transposes of the three static graphs are built once.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import torch
+
+from .. import _hip, engine
+from .._hip import check, lib, stream_ptr
+from ..train import DataParallel, random_walk_noise
+from ..training import (DEFAULT_NSLAB, Adam, FlatParams, SlabArena, _saves, _Timer, nslab_table)
+from . import ms_engine
+from .ms_engine import EDGE_TYPES
+
+KIND_SLOT = {"g2m": 0, "m2m": 1, "m2g": 2}
+
+
+def check_trainable(sim) -> None:
+    gnn = sim._multi_scale_gnn
+    if gnn.latent_dim not in (64, 128):
+        raise NotImplementedError("HIP multi-scale training: latent_dim must be 64 or 128")
+    if gnn.nmlp_layers not in (1, 2):
+        raise NotImplementedError("HIP multi-scale training: nmlp_layers must be 1 or 2")
+    if sim._nparticle_types > 1:
+        raise NotImplementedError("HIP multi-scale training: particle-type embeddings (nparticle_types > 1)")
+
+
+class MSTrainWorkspace:
+    """Saved activations, backward buffers and slabs for one (n, T, static graph)."""
+
+    def __init__(self, gnn, n: int, T: int, dim: int, graphs: Dict[str, engine.CsrGraph],
+                 device: torch.device, nslab: int = DEFAULT_NSLAB):
+        L = lib()
+        H = gnn.latent_dim
+        self.H, self.n, self.T, self.dim = H, n, T, dim
+        self.nlin = gnn.nmlp_layers + 1
+        self.nb = len(gnn.chain())
+        self.kinds = ["g2m"] + ["m2m"] * (self.nb - 2) + ["m2g"]
+        self.scales = [1.0] + [float(2.0 ** k) for k in range(self.nb - 2)] + [1.0]
+        self.graphs = graphs
+        self.f = ms_engine.MSWorkspace(n, T, dim, H, graphs, device)
+        f32 = dict(dtype=torch.float32, device=device)
+        e = lambda *s: torch.empty(*s, **f32)
+        two = self.nlin == 3
+        tl = {k: int(L.sgnn_edge_latent_floats(g.edge_cap, H)) for k, g in graphs.items()}
+        cap = {k: g.edge_cap for k, g in graphs.items()}
+        self.enc_h, self.enc_yh, self.enc_rstd = e(n, H), e(n, H), e(n)
+        self.enc_h2 = e(n, H) if two else None
+        self.ee_yh = {k: e(tl[k]) for k in EDGE_TYPES}
+        self.ee_rstd = {k: e(cap[k]) for k in EDGE_TYPES}
+        self.ee_h2 = {k: (e(tl[k]) if two else None) for k in EDGE_TYPES}
+        kb = self.kinds
+        self.e_h = [e(tl[kb[b]]) for b in range(self.nb)]
+        self.e_h2 = [e(tl[kb[b]]) if two else None for b in range(self.nb)]
+        self.e_yh = [e(tl[kb[b]]) for b in range(self.nb)]
+        self.e_rstd = [e(cap[kb[b]]) for b in range(self.nb)]
+        self.n_agg = [e(n, H) for _ in range(self.nb)]
+        self.n_h = [e(n, H) for _ in range(self.nb)]
+        self.n_h2 = [e(n, H) if two else None for _ in range(self.nb)]
+        self.n_yh = [e(n, H) for _ in range(self.nb)]
+        self.n_rstd = [e(n) for _ in range(self.nb)]
+        self.xs = [e(n, H) for _ in range(self.nb + 1)]
+        self.hd = e(n, H)
+        self.hd2 = e(n, H) if two else None
+        self.pred = e(n, dim + 1)
+        self.next_scratch = e(n, dim)
+        self.g, self.dxp, self.dagg, self.du = e(n, H), e(n, H), e(n, H), e(n, H)
+        self.dh_rows = e(max(cap.values()), H)
+        self.de0t = {k: e(tl[k]) for k in EDGE_TYPES}
+        # sender-sorted transposes of the static graphs (for dV), built once
+        i32 = dict(dtype=torch.int32, device=device)
+        self.tptr, self.tperm = {}, {}
+        s = stream_ptr(device)
+        for k, g in graphs.items():
+            self.tptr[k] = torch.empty(n + 1, **i32)
+            self.tperm[k] = torch.empty(g.edge_cap, **i32)
+            tws = torch.empty(int(L.sgnn_transpose_workspace_bytes(n, g.edge_cap)) + 256,
+                              dtype=torch.uint8, device=device)
+            check(L.sgnn_transpose_csr(g.rowptr.data_ptr(), g.send.data_ptr(), n, g.edge_cap,
+                                       (tws.data_ptr() + 255) & ~255, self.tptr[k].data_ptr(),
+                                       self.tperm[k].data_ptr(), s), "sgnn_transpose_csr")
+        self.nslab_of = nslab_table(nslab)
+        keys = [(_hip.SLAB_DECODER, 0)] + [(_hip.SLAB_NODE, b) for b in range(self.nb)] + \
+               [(_hip.SLAB_EDGE, b) for b in range(self.nb)] + [(_hip.SLAB_UV, b) for b in range(self.nb)] + \
+               [(_hip.SLAB_ENC_NODE, 0)] + [(_hip.SLAB_ENC_EDGE, KIND_SLOT[k]) for k in EDGE_TYPES]
+        self.feat = gnn.nnode_in
+        self.slabs = SlabArena(H, self.nlin, self.feat, keys, self.nslab_of, device)
+        self.loss_out = torch.zeros(8, **f32)
+        self._descs_key = None
+
+    def slab(self, kind: int, k: int = 0) -> int:
+        return self.slabs.ptr(kind, k)
+
+    def descriptors(self, grads: Dict[str, torch.Tensor]) -> None:
+        key = tuple(g.data_ptr() for g in grads.values())
+        if key == self._descs_key:
+            return
+        pre = "_multi_scale_gnn."
+        g = lambda name: grads[pre + name]
+        lay = self.slabs.layout(self.H, self.nlin, self.feat, self.dim)
+        lay.enc_node(g, "grid_node_encoder.")
+        for k in EDGE_TYPES:
+            lay.enc_edge(g, f"{k}_edge_encoder.", KIND_SLOT[k])
+        prefixes = ["g2m_block."] + [f"m2m_blocks.{k}." for k in range(self.nb - 2)] + ["m2g_block."]
+        for b, p in enumerate(prefixes):
+            lay.interaction(g, p, b, self.scales[b], slot=b)
+        lay.decoder(g, "prediction_head.", self.loss_out)
+        self._descs_dev, self._block_start, self._ndesc, self._nblocks = lay.upload(self.slabs.arena.device)
+        self._descs_key = key
+
+
+def train_forward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grid_radius: float,
+                  mesh_radius: float, timers: Optional[dict] = None) -> None:
+    """ms_engine.forward_step with every activation the backward needs saved."""
+    L = lib()
+    pk = ms_engine.ParamPack.get(gnn)
+    ws, graphs = tw.f, tw.graphs
+    n, T, d = tw.n, tw.T, tw.dim
+    s = stream_ptr(inp.pos_seq.device)
+    pos = inp.pos_seq
+    sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2)
+    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, 0, 0, 0, 0, inp.vel_mean.data_ptr(),
+                              inp.vel_std.data_ptr(), float(grid_radius), float(grid_radius),
+                              ctypes.byref(pk.enc), ctypes.byref(pk.edge[0]), tw.xs[0].data_ptr(),
+                              ws.u.data_ptr(), ws.v.data_ptr(), ctypes.byref(sv), s), "sgnn_encode_nodes")
+    radii = {"g2m": grid_radius, "m2m": mesh_radius, "m2g": grid_radius}
+    for k in EDGE_TYPES:
+        g = graphs[k]
+        sv = _saves(yhat=tw.ee_yh[k], rstd=tw.ee_rstd[k], h2=tw.ee_h2[k])
+        check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radii[k]),
+                                  g.rowptr.data_ptr(), g.send.data_ptr(), g.recv.data_ptr(), n, g.edge_cap,
+                                  ctypes.byref(pk.enc_edge[k]), ws.e0t[k].data_ptr(), ctypes.byref(sv), s),
+              "sgnn_encode_edges")
+    for b in range(tw.nb):
+        kind = tw.kinds[b]
+        g = graphs[kind]
+        sv = _saves(h=tw.e_h[b], yhat=tw.e_yh[b], rstd=tw.e_rstd[b], h2=tw.e_h2[b])
+        with _Timer(timers, "k_edge_layer(train)"):
+            check(L.sgnn_edge_layer(ws.u.data_ptr(), ws.v.data_ptr(), ws.e0t[kind].data_ptr(), tw.scales[b],
+                                    g.rowptr.data_ptr(), g.send.data_ptr(), g.recv.data_ptr(), n,
+                                    g.edge_cap, ctypes.byref(pk.edge[b]), ws.agg.data_ptr(),
+                                    ws.cin.data_ptr(), ws.cout.data_ptr(), ctypes.byref(sv), s),
+                  "sgnn_edge_layer")
+        if b < tw.nb - 1:
+            sv = _saves(h=tw.n_h[b], yhat=tw.n_yh[b], rstd=tw.n_rstd[b], agg=tw.n_agg[b], h2=tw.n_h2[b])
+            check(L.sgnn_node_layer(tw.xs[b].data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
+                                    ws.cout.data_ptr(), g.rowptr.data_ptr(), n, ctypes.byref(pk.node[b]),
+                                    ctypes.byref(pk.edge[b + 1]), tw.xs[b + 1].data_ptr(), ws.u.data_ptr(),
+                                    ws.v.data_ptr(), ctypes.byref(sv), s), "sgnn_node_layer")
+        else:
+            sv = _saves(h=tw.n_h[b], yhat=tw.n_yh[b], rstd=tw.n_rstd[b], agg=tw.n_agg[b], hd=tw.hd,
+                        h2=tw.n_h2[b], hd2=tw.hd2)
+            check(L.sgnn_node_layer_decode(tw.xs[b].data_ptr(), ws.agg.data_ptr(), ws.cin.data_ptr(),
+                                           ws.cout.data_ptr(), g.rowptr.data_ptr(), n,
+                                           ctypes.byref(pk.node[b]), ctypes.byref(pk.head), pos.data_ptr(),
+                                           T, d, inp.acc_mean.data_ptr(), inp.acc_std.data_ptr(),
+                                           tw.xs[b + 1].data_ptr(), tw.pred.data_ptr(),
+                                           tw.next_scratch.data_ptr(), 0, ctypes.byref(sv), s),
+                  "sgnn_node_layer_decode")
+
+
+def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dict[str, torch.Tensor],
+                   grid_radius: float, mesh_radius: float, dpred: Optional[torch.Tensor] = None,
+                   next_pos: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
+                   next_strain: Optional[torch.Tensor] = None, w_pos: float = 1.0, w_strain: float = 1.0,
+                   inv_count: float = 1.0, timers: Optional[dict] = None) -> None:
+    L = lib()
+    pk = ms_engine.ParamPack.get(gnn)
+    tw.descriptors(grads)
+    ws, graphs = tw.f, tw.graphs
+    n, T, d = tw.n, tw.T, tw.dim
+    s = stream_ptr(inp.pos_seq.device)
+    p = engine._ptr
+    ns = tw.nslab_of
+    check(L.sgnn_decoder_loss_bwd(tw.pred.data_ptr(), inp.pos_seq.data_ptr(), p(next_pos), p(noise),
+                                  p(next_strain), inp.acc_mean.data_ptr(), inp.acc_std.data_ptr(), n, T, d,
+                                  float(w_pos), float(w_strain), float(inv_count), p(dpred),
+                                  ctypes.byref(_saves(hd=tw.hd, hd2=tw.hd2)), tw.xs[tw.nb].data_ptr(),
+                                  ctypes.byref(pk.head), tw.g.data_ptr(), tw.slab(_hip.SLAB_DECODER),
+                                  ns[_hip.SLAB_DECODER], s), "sgnn_decoder_loss_bwd")
+    seen = set()
+    for b in range(tw.nb - 1, -1, -1):
+        kind = tw.kinds[b]
+        g = graphs[kind]
+        nsv = _saves(h=tw.n_h[b], yhat=tw.n_yh[b], rstd=tw.n_rstd[b], agg=tw.n_agg[b], h2=tw.n_h2[b])
+        check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, ctypes.byref(nsv), tw.xs[b].data_ptr(),
+                                    ctypes.byref(pk.node[b]), tw.dagg.data_ptr(), tw.dxp.data_ptr(),
+                                    tw.slab(_hip.SLAB_NODE, b), ns[_hip.SLAB_NODE], s), "sgnn_node_layer_bwd")
+        esv = _saves(h=tw.e_h[b], yhat=tw.e_yh[b], rstd=tw.e_rstd[b], h2=tw.e_h2[b])
+        with _Timer(timers, "k_edge_bwd"):
+            check(L.sgnn_edge_layer_bwd(tw.dagg.data_ptr(), g.rowptr.data_ptr(), g.send.data_ptr(),
+                                        g.recv.data_ptr(), n, ctypes.byref(esv), ws.e0t[kind].data_ptr(),
+                                        tw.scales[b], ctypes.byref(pk.edge[b]), tw.du.data_ptr(),
+                                        ws.cin.data_ptr(), ws.cout.data_ptr(), tw.dh_rows.data_ptr(),
+                                        tw.de0t[kind].data_ptr(), int(kind in seen),
+                                        tw.slab(_hip.SLAB_EDGE, b), ns[_hip.SLAB_EDGE], s),
+                  "sgnn_edge_layer_bwd")
+        seen.add(kind)
+        check(L.sgnn_uv_bwd(tw.dxp.data_ptr(), tw.du.data_ptr(), ws.cin.data_ptr(), ws.cout.data_ptr(),
+                            g.rowptr.data_ptr(), tw.dh_rows.data_ptr(), tw.tptr[kind].data_ptr(),
+                            tw.tperm[kind].data_ptr(), tw.xs[b].data_ptr(), n, ctypes.byref(pk.edge[b]),
+                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, b), ns[_hip.SLAB_UV], s), "sgnn_uv_bwd")
+    check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, inp.vel_mean.data_ptr(),
+                                  inp.vel_std.data_ptr(), float(grid_radius), float(grid_radius),
+                                  ctypes.byref(_saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd,
+                                                      h2=tw.enc_h2)),
+                                  ctypes.byref(pk.enc), tw.slab(_hip.SLAB_ENC_NODE), ns[_hip.SLAB_ENC_NODE], s),
+          "sgnn_encode_nodes_bwd")
+    radii = {"g2m": grid_radius, "m2m": mesh_radius, "m2g": grid_radius}
+    for k in EDGE_TYPES:
+        g = graphs[k]
+        if g.num_edges == 0:
+            continue
+        check(L.sgnn_encode_edges_bwd(tw.de0t[k].data_ptr(), inp.pos_seq.data_ptr() + 4 * (T - 1) * d, T * d,
+                                      d, float(radii[k]), g.rowptr.data_ptr(), g.send.data_ptr(),
+                                      g.recv.data_ptr(), n,
+                                      ctypes.byref(_saves(yhat=tw.ee_yh[k], rstd=tw.ee_rstd[k], h2=tw.ee_h2[k])),
+                                      ctypes.byref(pk.enc_edge[k]), tw.slab(_hip.SLAB_ENC_EDGE, KIND_SLOT[k]),
+                                      ns[_hip.SLAB_ENC_EDGE], s), "sgnn_encode_edges_bwd")
+    check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
+                              tw._nblocks, s), "sgnn_reduce_slabs")
+
+
+class MultiScaleTrainer:
+    """Drop-in body of the multi_scale_train.py:140-186 loop for a sgnn_amd
+    MultiScaleSimulator (static graph set with set_static_graph)."""
+
+    def __init__(self, simulator, lr_init: float = 1e-3, lr_decay: float = 0.1,
+                 lr_decay_steps: int = 15000, noise_std: float = 0.02,
+                 loss_weight_position: float = 1.0, loss_weight_strain: float = 1.0,
+                 group=None, nslab: int = DEFAULT_NSLAB):
+        check_trainable(simulator)
+        self.sim = simulator
+        self.gnn = simulator._multi_scale_gnn
+        self.flat = FlatParams(simulator)
+        self.opt = Adam(self.flat, lr_init)
+        self.grads = {k: p.grad for k, p in simulator.named_parameters()}
+        self.lr_init, self.lr_decay, self.lr_decay_steps = lr_init, lr_decay, lr_decay_steps
+        self.noise_std = noise_std
+        self.w_pos, self.w_strain = loss_weight_position, loss_weight_strain
+        self.dp = DataParallel(group)
+        self.nslab = nslab
+        self.step = 0
+        self._tw: Dict[tuple, MSTrainWorkspace] = {}
+        self._count_cache: Dict[int, int] = {}
+
+    def workspace(self, n: int, T: int, device) -> MSTrainWorkspace:
+        graphs = self.sim._csr(n, device)
+        key = (n, T, str(device), id(graphs))
+        tw = self._tw.get(key)
+        if tw is None:
+            if len(self._tw) > 2:
+                self._tw.clear()
+            tw = MSTrainWorkspace(self.gnn, n, T, self.sim._kinematic_dimensions, graphs, device, self.nslab)
+            self._tw[key] = tw
+        return tw
+
+    def train_step(self, position: torch.Tensor, next_position: torch.Tensor, next_strain: torch.Tensor,
+                   particle_types=None, noise: Optional[torch.Tensor] = None,
+                   n_global: Optional[int] = None, timers: Optional[dict] = None) -> dict:
+        pos = position.to(torch.float32).contiguous()
+        if noise is None:
+            noise = random_walk_noise(pos, self.noise_std)
+        noise = noise.to(pos.device, torch.float32).contiguous()
+        noisy = (pos + noise).contiguous()
+        inp, _ = self.sim._step_inputs(noisy, particle_types)
+        n, T, _ = noisy.shape
+        tw = self.workspace(n, T, pos.device)
+        if n_global is None:
+            n_global = self._count_cache.get(n)
+            if n_global is None:
+                n_global = self.dp.global_count(n, pos.device)
+                self._count_cache[n] = n_global
+        rg, rm = self.sim._grid_radius(), self.sim._mesh_radius()
+        train_forward(self.gnn, inp, tw, rg, rm, timers=timers)
+        train_backward(self.gnn, inp, tw, self.grads, rg, rm, next_pos=next_position.to(torch.float32).contiguous(),
+                       noise=noise, next_strain=next_strain.to(torch.float32).contiguous(), w_pos=self.w_pos,
+                       w_strain=self.w_strain, inv_count=1.0 / n_global, timers=timers)
+        self.dp.allreduce_(self.flat.grad, tw.loss_out)
+        self.opt.step()
+        self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6
+        self.step += 1
+        lo = tw.loss_out
+        return {"loss": lo[0] / n_global, "loss_position": (lo[1] + lo[2] + lo[3]) / n_global,
+                "loss_strain": lo[4] / n_global, "loss_xyz": lo[1:4] / n_global,
+                "n_global": n_global, "lr": self.opt.lr}

@@ -23,6 +23,36 @@ from .multi_scale_graph import MultiScaleConfig
 _KEYS = {"g2m": "grid2mesh_edges", "m2m": "mesh2mesh_edges", "m2g": "mesh2grid_edges"}
 
 
+class _TrainedGNN(torch.autograd.Function):
+    """pred = MultiScaleGNN(features(noisy window)) with the HIP backward
+    (multi_scale_train.py:176 loss.backward()).  One forward may be in flight
+    per workspace: a second forward before backward invalidates the first."""
+
+    @staticmethod
+    def forward(ctx, sim, inp, tw, *params):
+        from . import ms_training
+        ms_training.train_forward(sim._multi_scale_gnn, inp, tw, sim._grid_radius(), sim._mesh_radius())
+        tw.generation = getattr(tw, "generation", 0) + 1
+        ctx.sim, ctx.inp, ctx.tw, ctx.gen = sim, inp, tw, tw.generation
+        return tw.pred.clone()
+
+    @staticmethod
+    def backward(ctx, dpred):
+        from . import ms_training
+        sim, tw = ctx.sim, ctx.tw
+        if tw.generation != ctx.gen:
+            raise RuntimeError("sgnn_amd: a newer predict_accelerations overwrote the saved "
+                               "activations of this graph before backward")
+        gnn = sim._multi_scale_gnn
+        scratch = getattr(tw, "grad_scratch", None)
+        if scratch is None:
+            scratch = {k: torch.zeros_like(p) for k, p in gnn.named_parameters(prefix="_multi_scale_gnn")}
+            tw.grad_scratch = scratch
+        ms_training.train_backward(gnn, ctx.inp, tw, scratch, sim._grid_radius(), sim._mesh_radius(),
+                                   dpred=dpred.to(torch.float32).contiguous())
+        return (None, None, None, *[g.clone() for g in scratch.values()])
+
+
 class MultiScaleSimulator(nn.Module):
     """multi_scale_simulator.py:20-92"""
 
@@ -61,6 +91,7 @@ class MultiScaleSimulator(nn.Module):
         self._static_graph_data = graph_data
         self._csr_cache.clear()
         self._ws_cache.clear()
+        self.__dict__.get("_tw_cache", {}).clear()
 
     def _validate_static_graph(self):
         """:111-119"""
@@ -214,15 +245,34 @@ class MultiScaleSimulator(nn.Module):
                               particle_types: torch.Tensor):
         """:328-360 -> (predicted_normalized_acceleration, target_normalized_acceleration,
         predicted_strain)."""
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self._multi_scale_gnn.parameters()):
-            raise NotImplementedError("multi-scale training (HIP backward) is not implemented yet; "
-                                      "call under torch.no_grad() for evaluation")
         noisy = position_sequence + position_sequence_noise
-        inp, pred, _ = self._run(noisy, particle_types)
+        params = list(self._multi_scale_gnn.parameters())
         d = self._kinematic_dimensions
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            from . import ms_training
+            ms_training.check_trainable(self)
+            inp, _ = self._step_inputs(noisy, particle_types)
+            n, T, _ = inp.pos_seq.shape
+            tw = self._train_workspace(n, T, inp.pos_seq.device)
+            pred = _TrainedGNN.apply(self, inp, tw, *params)
+        else:
+            inp, pred, _ = self._run(noisy, particle_types)
         target = self._inverse_decoder_postprocessor(next_positions + position_sequence_noise[:, -1],
                                                      inp.pos_seq)
         return pred[:, :d], target, pred[:, -1]
+
+    def _train_workspace(self, n: int, T: int, device):
+        from . import ms_training
+        graphs = self._csr(n, device)
+        cache = self.__dict__.setdefault("_tw_cache", {})
+        key = (n, T, str(device), id(graphs))
+        tw = cache.get(key)
+        if tw is None:
+            cache.clear()
+            tw = ms_training.MSTrainWorkspace(self._multi_scale_gnn, n, T, self._kinematic_dimensions, graphs,
+                                              device)
+            cache[key] = tw
+        return tw
 
     def _inverse_decoder_postprocessor(self, next_position, position_sequence):
         """:362-373"""

@@ -309,6 +309,9 @@ def multi_scale_case(name, base, nframes, T, H, L, num_scales, window, mult, nty
 def main(only=None):
     if only == "ms":
         return main_ms()
+    if only == "ms_train":
+        return multi_scale_train_case("ms_train2d", synthetic.lattice_2d(16, 12, x0=-1.75), 6, 64, 2, 3, 2,
+                                      2.0, seed=6)
     T = 11
     # 1) tiny 2D, reference default radius 0.6, per-layer latents + 3-step rollout
     seq = synthetic.trajectory(synthetic.lattice_2d(10, 8), T + 3, seed=1)
@@ -337,6 +340,60 @@ def main(only=None):
     main_ms()
 
 
+def multi_scale_train_case(name, base, T, H, L, num_scales, window, mult, nmlp=2, seed=0):
+    """One step of the multi_scale_train.py:140-186 loop body (noise passed in,
+    lr_init 1e-3): loss, every gradient, Adam-updated weights."""
+    dim = base.shape[1]
+    noise_std = 0.02
+    seq = synthetic.trajectory(base, T + 1, seed=seed + 20)
+    st = synthetic.normalization_stats(dim, noise_std=noise_std)
+    norm = {k: {kk: torch.tensor(vv) for kk, vv in v.items()} for k, v in st.items()}
+    torch.manual_seed(seed)
+    sim = RefMSSim(kinematic_dimensions=dim, nnode_in=(T - 1) * dim + 1, nedge_in=dim + 1, nedge_out=H,
+                   latent_dim=H, nmessage_passing_steps=L, nmlp_layers=nmlp, normalization_stats=norm,
+                   nparticle_types=1, particle_type_embedding_size=9, num_scales=num_scales,
+                   window_size=window, radius_multiplier=mult, device="cpu")
+    sim.train()
+    graph = RefMSGraph(RefMSConfig(num_scales=num_scales, window_size=window, radius_multiplier=mult)
+                       ).create_all_edges(torch.tensor(seq[:, 0]))
+    sim.set_static_graph(graph)
+    n = seq.shape[0]
+    pos, next_pos = torch.tensor(seq[:, :T]), torch.tensor(seq[:, T])
+    next_strain = torch.tensor(np.random.default_rng(seed + 5).normal(0, 1, n).astype(np.float32))
+    types_ = torch.zeros(n, dtype=torch.long)
+    torch.manual_seed(seed + 100)
+    noise = ref_noise.get_random_walk_noise_for_position_sequence(pos, noise_std_last_step=noise_std)
+    init = sd_arrays(sim, "w0/")
+    opt = torch.optim.Adam(sim.parameters(), lr=1e-3)
+    opt.zero_grad()
+    pred_acc, target_acc, pred_strain = sim.predict_accelerations(
+        next_positions=next_pos, position_sequence_noise=noise, position_sequence=pos,
+        nparticles_per_example=torch.tensor([n]), particle_types=types_)
+    loss_pos = ((pred_acc - target_acc) ** 2).sum(dim=-1)          # multi_scale_train.py:162-166
+    loss_strain = (pred_strain - next_strain) ** 2                  # :169
+    loss = (1.0 * loss_pos + 1.0 * loss_strain).mean()              # :172-173
+    loss.backward()
+    grads = {"g/" + k: p.grad.detach().numpy().copy() for k, p in sim.named_parameters() if p.grad is not None}
+    opt.step()
+    out = {"hp_dim": np.int64(dim), "hp_T": np.int64(T), "hp_H": np.int64(H), "hp_L": np.int64(L),
+           "hp_ntypes": np.int64(1), "hp_emb": np.int64(9), "hp_nmlp": np.int64(nmlp),
+           "hp_num_scales": np.int64(num_scales), "hp_window": np.int64(window), "hp_mult": np.float32(mult),
+           **stats_arrays(st), **init, **grads, **sd_arrays(sim, "w1/"),
+           "positions": seq, "next_position": seq[:, T], "next_strain": next_strain.numpy(),
+           "noise": noise.numpy(), "particle_types": types_.numpy(),
+           "pred_acc": pred_acc.detach().numpy(), "target_acc": target_acc.detach().numpy(),
+           "pred_strain": pred_strain.detach().numpy(), "loss": np.float32(loss.item()),
+           "lr": np.float32(1e-3),
+           "g2m": graph["grid2mesh_edges"].numpy(), "m2m": graph["mesh2mesh_edges"].numpy(),
+           "m2g": graph["mesh2grid_edges"].numpy()}
+    for s_, d_ in graph["graph_hierarchy"].items():
+        out[f"scale{s_}_indices"] = d_["sampling_indices"].numpy()
+        out[f"scale{s_}_spacing"] = np.float32(d_["spacing"])
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: loss={loss.item():.6f} -> {os.path.getsize(path)/1e3:.0f} KB")
+
+
 def main_ms():
     # multi-scale 2D: 3 scales (grid + 2 meshes), nmlp_layers 2, wall feature active
     # (x starts at -1.75 so x+2 spans the clamp range)
@@ -346,6 +403,8 @@ def main_ms():
     # 27 lattice neighbours inside r, so the max_neighbors=24 truncation binds
     multi_scale_case("ms3d_h128", synthetic.lattice_3d(8, 6, 5, x0=-1.75), 6, 6, 128, 2, 2, 2, 2.0,
                      ntypes=2, seed=4, traj_seed=9)
+    # one multi-scale training step (2D, 3 scales, H=64, nmlp_layers 2)
+    multi_scale_train_case("ms_train2d", synthetic.lattice_2d(16, 12, x0=-1.75), 6, 64, 2, 3, 2, 2.0, seed=6)
 
 
 if __name__ == "__main__":
