@@ -42,11 +42,22 @@ from sgnn_amd import engine, synthetic  # noqa: E402
 from sgnn_amd.learned_simulator import LearnedSimulator  # noqa: E402
 
 WORKLOADS = {
-    # name: (lattice nx, ny, radius, hidden, layers)
-    "c2": (250, 200, 0.6, 64, 5),        # BASELINE configs[1]: ~50k particles, 5 layers, H=64, fp32
-    "c1_r15": (50, 40, 15.0, 64, 5),     # configs[0] shape at the BASELINE radius (cap binds)
-    "c1_r06": (50, 40, 0.6, 64, 5),      # configs[0] shape at the reference default radius
+    # name: (lattice dims, radius, hidden, layers)
+    "c2": ((250, 200), 0.6, 64, 5),        # BASELINE configs[1]: ~50k particles, 5 layers, H=64, fp32
+    "c1_r15": ((50, 40), 15.0, 64, 5),     # configs[0] shape at the BASELINE radius (cap binds)
+    "c1_r06": ((50, 40), 0.6, 64, 5),      # configs[0] shape at the reference default radius
+    "c4": ((100, 50, 40), 0.75, 128, 10),  # configs[3]: 3D 200k particles, 10 layers, H=128
 }
+MS_WORKLOADS = {
+    # name: (lattice dims, num_scales, window, radius_multiplier, hidden, layers, nmlp_layers)
+    "c5": ((100, 100, 100), 2, 2, 2.0, 128, 10, 2),   # configs[4]: multi-scale 3D ~1M per GPU
+    "c5_small": ((40, 40, 40), 2, 2, 2.0, 128, 10, 2),
+    "ms2d": ((240, 200), 2, 2, 2.0, 128, 10, 2),      # multi_scale_config.yaml widths, 2D
+}
+
+
+def lattice(dims):
+    return synthetic.lattice_2d(*dims) if len(dims) == 2 else synthetic.lattice_3d(*dims)
 T_SEQ = 11                # config.yaml:20 input_sequence_length
 MFMA_F32_PEAK = 157.3e12  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
 
@@ -56,8 +67,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["train", "rollout"], default="train")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--mode", choices=["train", "rollout", "ms-train", "ms-rollout"], default="train")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(MS_WORKLOADS), default=None)
     ap.add_argument("--cpu-steps", type=int, default=6, help="oracle steps for cpu_baseline (0: skip)")
     ap.add_argument("--no-rollout-extras", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
@@ -123,17 +134,18 @@ def max_over_ranks(x, world, device):
 
 # ----------------------------------------------------------------------------- rollout
 def rollout_setup(workload, device, seed, rank):
-    nx, ny, radius, H, L = WORKLOADS[workload]
-    sim = make_sim(H, L, radius, 2, device, seed)
-    seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny), T_SEQ, seed=1000 + rank)
+    dims, radius, H, L = WORKLOADS[workload]
+    dim = len(dims)
+    sim = make_sim(H, L, radius, dim, device, seed)
+    seq = synthetic.trajectory(lattice(dims), T_SEQ, seed=1000 + rank)
     n = seq.shape[0]
     window0 = torch.from_numpy(seq)
     types_ = torch.zeros(n, dtype=torch.long, device=device)
     inp, use_emb = sim._step_inputs(window0.to(device), [n], types_)
     ws = sim._workspace(n, T_SEQ, device)
     win = [inp.pos_seq, torch.empty_like(inp.pos_seq)]
-    pred = torch.empty(n, 3, device=device)
-    nxt = torch.empty(n, 2, device=device)
+    pred = torch.empty(n, dim + 1, device=device)
+    nxt = torch.empty(n, dim, device=device)
 
     def run(k0, nsteps, timers=None):
         for k in range(k0, k0 + nsteps):
@@ -143,10 +155,15 @@ def rollout_setup(workload, device, seed, rank):
     return sim, window0, ws, run, n, radius, H, L
 
 
-def cpu_rollout_baseline(sim, window, radius, L, steps):
+CPU_SAMPLE_DIMS = {"c4": (40, 25, 20)}   # bounded CPU sample (same spacing / radius / model)
+
+
+def cpu_rollout_baseline(sim, window, radius, L, steps, workload=None):
     """Oracle (test infrastructure: CPU restatement of the reference) rollout."""
     from oracle import sgnn_oracle as O
     state = {k: v.detach().cpu() for k, v in sim.state_dict().items()}
+    if workload in CPU_SAMPLE_DIMS:
+        window = torch.from_numpy(synthetic.trajectory(lattice(CPU_SAMPLE_DIMS[workload]), T_SEQ, seed=7))
     osim = O.OracleSimulator(state, window.shape[2], L, radius, sim._normalization_stats)
     cur, n = window.cpu(), window.shape[0]
     types_ = torch.zeros(n, dtype=torch.long)
@@ -180,13 +197,14 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps)
     E = ws.num_edges()
     edge_avg_s = float(np.mean([a.elapsed_time(b) for a, b in timers])) * 1e-3
     flops = E * 4 * H * H
-    out = {"workload": f"{workload}: {n} particles/GPU, r={radius}, L={L}, H={H}", "particles": n,
+    out = {"workload": f"{workload}: {'x'.join(map(str, WORKLOADS[workload][0]))} lattice = {n} particles/GPU, "
+                       f"r={radius}, L={L}, H={H}", "particles": n,
            "edges": E, "value": n * steps * world / dt, "unit": "particle-steps/s",
            "ms_per_step": dt / steps * 1e3,
            "M_edge_messages_per_s": E * L * steps * world / dt / 1e6,
            "edge_kernel_us": edge_avg_s * 1e6, "edge_kernel_mfma_frac": flops / edge_avg_s / MFMA_F32_PEAK}
     if cpu_steps > 0 and rank == 0 and world == 1:
-        out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps)
+        out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps, workload)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
     return out, timers, flops, edge_avg_s, E, n, radius, H, L
 
@@ -224,7 +242,8 @@ def cpu_train_baseline(state, seq, strain, radius, L, steps, stats):
 
 def bench_train(args, world, rank, device):
     from sgnn_amd.train import Trainer
-    nx, ny, radius, H, L = WORKLOADS[args.workload]
+    dims, radius, H, L = WORKLOADS[args.workload]
+    nx, ny = dims
     sim = make_sim(H, L, radius, 2, device, args.seed)
     state0 = {k: v.detach().cpu().clone() for k, v in sim.state_dict().items()}
     seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny), T_SEQ + 1, seed=2000 + rank)
@@ -290,12 +309,167 @@ def bench_train(args, world, rank, device):
     return res
 
 
+# ----------------------------------------------------------------------------- multi-scale
+def ms_setup(workload, device, seed, rank, nframes):
+    from sgnn_amd.multi_scale import MultiScaleSimulator, build_static_multi_scale_graph
+    dims, ns, win, mult, H, L, nmlp = MS_WORKLOADS[workload]
+    dim = len(dims)
+    torch.manual_seed(seed)
+    stats = synthetic.normalization_stats(dim, noise_std=0.02)
+    st = {k: {kk: torch.tensor(vv) for kk, vv in v.items()} for k, v in stats.items()}
+    sim = MultiScaleSimulator(dim, (T_SEQ - 1) * dim + 1, dim + 1, H, H, L, nmlp, st, 1, 9, ns, win, mult,
+                              device=str(device)).to(device)
+    base = lattice(dims)
+    base[:, 0] -= 2.0   # bar starts at the wall (x = -2): the wall feature is active
+    seq = synthetic.trajectory(base, nframes, seed=3000 + rank)
+    graph = build_static_multi_scale_graph(torch.from_numpy(seq[:, 0]).to(device), ns, win, mult)
+    sim.set_static_graph(graph)
+    edges = {k: int(graph[k].shape[1]) for k in ("grid2mesh_edges", "mesh2mesh_edges", "mesh2grid_edges")}
+    desc = (f"{workload}: multi-scale {'x'.join(map(str, dims))} lattice = {seq.shape[0]} particles/GPU, "
+            f"num_scales={ns}, window={win}, radius_multiplier={mult}, L={L} M2M blocks, H={H}, "
+            f"nmlp_layers={nmlp}, T={T_SEQ}; edges g2m/m2m/m2g = {edges['grid2mesh_edges']}/"
+            f"{edges['mesh2mesh_edges']}/{edges['mesh2grid_edges']}")
+    return sim, seq, edges, desc, (dims, ns, win, mult, H, L, nmlp)
+
+
+def ms_block_edges(edges, L):
+    return edges["grid2mesh_edges"] + L * edges["mesh2mesh_edges"] + edges["mesh2grid_edges"]
+
+
+def cpu_ms_train_baseline(sim, cfg, steps):
+    """Oracle multi-scale training step (forward + torch autograd + Adam) on a
+    bounded CPU sample of the same model (smaller lattice)."""
+    from oracle import multi_scale_oracle as MO
+    from oracle import sgnn_oracle as O
+    dims, ns, win, mult, H, L, nmlp = cfg
+    sdims = (16, 16, 12) if len(dims) == 3 else (60, 40)
+    base = lattice(sdims)
+    base[:, 0] -= 2.0
+    seq = synthetic.trajectory(base, T_SEQ + 1, seed=9)
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in sim.state_dict().items()}
+    graph = MO.create_all_edges(torch.from_numpy(seq[:, 0]), ns, win, mult)
+    osim = MO.MultiScaleOracle(params, len(dims), L, sim._normalization_stats, graph, ns, mult, 1, nmlp)
+    opt = torch.optim.Adam([p for k, p in params.items() if "embedding" not in k], lr=1e-3)
+    pos, nxt = torch.from_numpy(seq[:, :T_SEQ]), torch.from_numpy(seq[:, T_SEQ])
+    n = pos.shape[0]
+    strain = torch.zeros(n)
+
+    def step():
+        noise = O.random_walk_noise(pos, 0.02)
+        pa, ta, ps = osim.predict_accelerations(nxt, noise, pos)
+        loss = O.training_loss(pa, ta, ps, strain)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": torch.get_num_threads(),
+            "kind": "port", "cpu_model": cpu_model(), "seconds": dt,
+            "sample": f"{steps} oracle multi-scale training steps (forward + torch autograd + Adam, torch "
+                      f"CPU fp32 restatement of sgnn/multi_scale) on a {'x'.join(map(str, sdims))} lattice "
+                      f"= {n} particles, same model, after 1 warm-up"}
+
+
+def bench_ms_train(args, world, rank, device):
+    from sgnn_amd.multi_scale.ms_training import MultiScaleTrainer
+    sim, seq, edges, desc, cfg = ms_setup(args.workload, device, args.seed, rank, T_SEQ + 1)
+    n = seq.shape[0]
+    H, L = cfg[4], cfg[5]
+    pos = torch.from_numpy(seq[:, :T_SEQ]).to(device)
+    nxt = torch.from_numpy(seq[:, T_SEQ]).to(device)
+    strain = torch.from_numpy(np.random.default_rng(rank).normal(0, 1, n).astype(np.float32)).to(device)
+    tr = MultiScaleTrainer(sim, lr_init=1e-3)
+    for _ in range(args.warmup):
+        tr.train_step(pos, nxt, strain)
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = tr.train_step(pos, nxt, strain)
+    sync_barrier(world)
+    dt = time.perf_counter() - t0
+    timers = {}
+    for _ in range(min(args.steps, 3)):
+        tr.train_step(pos, nxt, strain, timers=timers)
+    torch.cuda.synchronize()
+    dt = max_over_ranks(dt, world, device)
+    kstats = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in timers.items()}
+    nmlp = cfg[6]
+    eb = ms_block_edges(edges, L)
+    # edge backward per edge: last (+ middle) Linear W^T dy and dW, W1e^T dh and dW1e
+    flops_bwd = eb / (L + 2) * (8 + (4 if nmlp == 2 else 0)) * H * H
+    dom = "k_edge_bwd"
+    achieved = flops_bwd / kstats[dom]
+    res = {
+        "metric": "particle-steps/sec (multi-scale training fwd+bwd+Adam)",
+        "value": n * args.steps * world / dt, "unit": "particle-steps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (0.5 mm lattice + random-walk frames; random-init weights)",
+        "config": {"workload": desc + ", training step (noise+fwd+bwd+Adam)", "particles_per_gpu": n,
+                   "edge_evaluations_per_step": eb, "global_batch_graphs": world,
+                   "parallelism": f"dp{world} (whole-graph, RCCL all-reduce)" if world > 1 else "single GPU"},
+        "M_edge_messages_per_s": eb * args.steps * world / dt / 1e6,
+        "final_loss": float(out["loss"]),
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved / 1e12, "peak": MFMA_F32_PEAK / 1e12,
+                     "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK, "traffic": None,
+                     "avg_launch_us": kstats[dom] * 1e6, "flops_per_launch": flops_bwd},
+        "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
+    }
+    if rank == 0 and world == 1 and args.cpu_steps > 0:
+        res["cpu_baseline"] = cpu_ms_train_baseline(sim, cfg, max(1, args.cpu_steps // 3))
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    return res
+
+
+def bench_ms_rollout(args, world, rank, device):
+    sim, seq, edges, desc, cfg = ms_setup(args.workload, device, args.seed, rank, T_SEQ)
+    n = seq.shape[0]
+    L = cfg[5]
+    cur = torch.from_numpy(seq).to(device).contiguous()
+    nxt_win = torch.empty_like(cur)
+    types_ = None
+
+    def run(k):
+        nonlocal cur, nxt_win
+        for _ in range(k):
+            sim._run(cur, types_, window_out=nxt_win)
+            cur, nxt_win = nxt_win, cur
+
+    with torch.no_grad():
+        run(args.warmup)
+        sync_barrier(world)
+        t0 = time.perf_counter()
+        run(args.steps)
+        sync_barrier(world)
+        dt = time.perf_counter() - t0
+    dt = max_over_ranks(dt, world, device)
+    eb = ms_block_edges(edges, L)
+    return {"metric": "particle-steps/sec (multi-scale rollout)", "value": n * args.steps * world / dt,
+            "unit": "particle-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (0.5 mm lattice + random-walk frames; random-init weights)",
+            "config": {"workload": desc + ", rollout", "particles": n,
+                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+            "M_edge_messages_per_s": eb * args.steps * world / dt / 1e6}
+
+
 def main():
     args = parse()
     world, rank, local = init_dist()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    if args.mode == "train":
+    if args.workload is None:
+        args.workload = "c5" if args.mode.startswith("ms") else "c2"
+    if args.mode == "ms-train":
+        res = bench_ms_train(args, world, rank, device)
+    elif args.mode == "ms-rollout":
+        res = bench_ms_rollout(args, world, rank, device)
+    elif args.mode == "train":
         res = bench_train(args, world, rank, device)
         if not args.no_rollout_extras:
             res["rollout"] = {}

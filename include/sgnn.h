@@ -187,6 +187,13 @@ int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin
 enum { SGNN_SLAB_EDGE = 0, SGNN_SLAB_NODE = 1, SGNN_SLAB_UV = 2, SGNN_SLAB_DECODER = 3,
        SGNN_SLAB_ENC_NODE = 4, SGNN_SLAB_ENC_EDGE = 5 };
 int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat, int32_t nlin);
+/* Hidden 128 runs each of the EDGE / NODE / UV / ENC_EDGE backwards as a
+ * per-item kernel that writes pre-activation gradients to `scratch` plus
+ * split-K MFMA GEMMs for the weight gradients (same slab layouts).  scratch
+ * must hold sgnn_bwd_scratch_floats(kind, hidden, nitems, nlin) floats, nitems
+ * = edge_cap (edge kinds) or n (node kinds); 0 (scratch unused) for hidden 64.
+ * One scratch buffer may serve every call on the same stream. */
+int64_t sgnn_bwd_scratch_floats(int32_t kind, int32_t hidden, int64_t nitems, int32_t nlin);
 
 /* out[r*dst_ld + c] (+)= scale * sum_{g<nslab} sum_{q<nrep}
  *                         src[g*slab_stride + offset + q*rep_stride + r*src_ld + c] */
@@ -217,17 +224,18 @@ int sgnn_decoder_loss_bwd(const float* pred, const float* pos_seq, const float* 
 /* saves: yhat, rstd, h, agg (+ h2) as node_layer wrote them. */
 int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* saves, const float* x_in,
                         const sgnn_mlp* node_fn, float* dagg, float* dxp, float* slab,
-                        int32_t nslab, void* stream);
+                        int32_t nslab, float* scratch, void* stream);
 /* saves: h, yhat, rstd (+ h2) as edge_layer wrote them. */
 int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t* send,
                         const int32_t* recv, int64_t n, const sgnn_saves* saves, const float* e0t,
                         float e_scale, const sgnn_mlp* edge_fn, float* du, float* cin,
                         float* cout, float* dh_rows, float* de0t, int32_t de0_accumulate,
-                        float* slab, int32_t nslab, void* stream);
+                        float* slab, int32_t nslab, float* scratch, int64_t edge_cap,
+                        void* stream);
 int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, const float* cout,
                 const int32_t* rowptr, const float* dh_rows, const int32_t* tptr,
                 const int32_t* tperm, const float* x_in, int64_t n, const sgnn_mlp* edge_fn,
-                float* g, float* slab, int32_t nslab, void* stream);
+                float* g, float* slab, int32_t nslab, float* scratch, void* stream);
 /* Wall feature as sgnn_encode_nodes: clamp(x + 2, 0, wall_max) / wall_div.
  * saves: h, yhat, rstd (+ h2). */
 int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
@@ -238,7 +246,8 @@ int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32
 int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_stride, int32_t dim,
                           float radius, const int32_t* rowptr, const int32_t* send,
                           const int32_t* recv, int64_t n, const sgnn_saves* saves,
-                          const sgnn_mlp* enc, float* slab, int32_t nslab, void* stream);
+                          const sgnn_mlp* enc, float* slab, int32_t nslab, float* scratch,
+                          int64_t edge_cap, void* stream);
 
 /* Fused Adam over a flat fp32 buffer; same update as torch.optim.Adam
  * (amsgrad=False, weight_decay=0) used by train.py:199,271-273. step >= 1. */

@@ -77,6 +77,7 @@ SIGNATURES = {
     "sgnn_coo_to_csr": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p]),
     "sgnn_bwd_slab_floats": (c_int64, [c_int32, c_int32, c_int32, c_int32]),
+    "sgnn_bwd_scratch_floats": (c_int64, [c_int32, c_int32, c_int64, c_int32]),
     "sgnn_reduce_slabs": (ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "sgnn_transpose_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64]),
     "sgnn_transpose_csr": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
@@ -86,20 +87,20 @@ SIGNATURES = {
                                              c_float, c_float, c_void_p, P_SAVES, c_void_p, P_MLP,
                                              c_void_p, c_void_p, c_int32, c_void_p]),
     "sgnn_node_layer_bwd": (ctypes.c_int, [c_void_p, c_int64, P_SAVES, c_void_p, P_MLP, c_void_p,
-                                           c_void_p, c_void_p, c_int32, c_void_p]),
+                                           c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "sgnn_edge_layer_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                            P_SAVES, c_void_p, c_float, P_MLP,
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                           c_int32, c_void_p, c_int32, c_void_p]),
+                                           c_int32, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
     "sgnn_uv_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_int64, P_MLP, c_void_p,
-                                   c_void_p, c_int32, c_void_p]),
+                                   c_void_p, c_int32, c_void_p, c_void_p]),
     "sgnn_encode_nodes_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                              c_void_p, c_void_p, c_float, c_float, P_SAVES,
                                              P_MLP, c_void_p, c_int32, c_void_p]),
     "sgnn_encode_edges_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_float,
                                              c_void_p, c_void_p, c_void_p, c_int64, P_SAVES,
-                                             P_MLP, c_void_p, c_int32, c_void_p]),
+                                             P_MLP, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
     "sgnn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,
                                       c_float, c_float, c_float, c_int64, c_void_p]),
 }

@@ -62,19 +62,57 @@ SGNN_DEV void mfma_step(f32x16 (&acc)[TH], const float* wl, int ld, int koff, fl
   for (int t = 0; t < TH; ++t) acc[t] = mfma32(wl[(32 * t + l) * ld + koff], b, acc[t]);
 }
 
+// Buffer resource over a global weight matrix: loads take the per-lane part
+// of the address in one VGPR, the uniform part in a scalar offset and the
+// immediate (plain pointers make the compiler hoist one 64-bit address per
+// unrolled load out of the item loop and spill them).
+SGNN_DEV __amdgpu_buffer_rsrc_t weight_rsrc(const float* w) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(w), (short)0, 0x7ffffff0, 0x00020000);
+}
+
+SGNN_DEV f32x4 buf_ld4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 v = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+  return __builtin_bit_cast(f32x4, v);
+}
+
+// W rows for one (t, k-group) product step: LDS image or global (G) matrix.
+template <int TH, bool G>
+struct WRows {
+  const float* w;
+  int ld;
+  __amdgpu_buffer_rsrc_t rs;
+  int voff;
+  SGNN_DEV WRows(const float* w_, int ld_) : w(w_), ld(ld_) {
+    const int l = lane_id() & 31, h = lane_id() >> 5;
+    if constexpr (G) {
+      rs = weight_rsrc(w_);
+      voff = 4 * (l * ld_ + 4 * h);
+    } else {
+      voff = l * ld_ + 4 * h;
+    }
+  }
+  // units 32t + lane, k = kb .. kb+3 (+4h)
+  SGNN_DEV f32x4 get(int t, int kb) const {
+    if constexpr (G) return buf_ld4(rs, voff, 4 * (32 * t * ld + kb));
+    else return ld4(w + voff + 32 * t * ld + kb);
+  }
+};
+
 // Product with the B operand in C layout (a previous accumulator X, TK
 // tiles): acc[t] += sum_{k} W[32t+lane][k] X[k][item] over K = 32*TK units.
-template <int TH, int TK>
+// G: W is a global (L2-resident) matrix, otherwise an LDS image.
+template <int TH, int TK, bool G = false>
 SGNN_DEV void mfma_from_acc(f32x16 (&acc)[TH], const float* wl, int ld, int kbase,
                             const f32x16 (&x)[TK]) {
-  const int l = lane_id() & 31, h = lane_id() >> 5;
+  const WRows<TH, G> W(wl, ld);
 #pragma unroll
   for (int tk = 0; tk < TK; ++tk) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       f32x4 w[TH];
 #pragma unroll
-      for (int t = 0; t < TH; ++t) w[t] = ld4(wl + (32 * t + l) * ld + kbase + 32 * tk + 8 * g + 4 * h);
+      for (int t = 0; t < TH; ++t) w[t] = W.get(t, kbase + 32 * tk + 8 * g);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
 #pragma unroll
@@ -86,17 +124,17 @@ SGNN_DEV void mfma_from_acc(f32x16 (&acc)[TH], const float* wl, int ld, int kbas
 
 // Same, but the B operand comes as float4 groups in the C-layout order that
 // the caller loads from memory: xg[tk*4+g] holds units 32tk+8g+4h+(0..3).
-template <int TH, int TK>
+template <int TH, int TK, bool G = false>
 SGNN_DEV void mfma_from_groups(f32x16 (&acc)[TH], const float* wl, int ld, int kbase,
                                const f32x4 (&xg)[TK * 4], float scale) {
-  const int l = lane_id() & 31, h = lane_id() >> 5;
+  const WRows<TH, G> W(wl, ld);
 #pragma unroll
   for (int tk = 0; tk < TK; ++tk) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       f32x4 w[TH];
 #pragma unroll
-      for (int t = 0; t < TH; ++t) w[t] = ld4(wl + (32 * t + l) * ld + kbase + 32 * tk + 8 * g + 4 * h);
+      for (int t = 0; t < TH; ++t) w[t] = W.get(t, kbase + 32 * tk + 8 * g);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const float b = xg[tk * 4 + g][c] * scale;
@@ -347,24 +385,25 @@ SGNN_DEV void stage_matrix_t(float* lds, int ld, const float* g, int ldg, int ro
 // layers (nmlp_layers = 2), y = LAST(h) for 2 (nmlp_layers = 1).
 // h2 receives the second hidden (NL = 3; untouched for NL = 2) for the
 // training saves.
-template <int TH, int NL, int TO>
+// The middle weights Wm are always global; Wl is global when GL.
+template <int TH, int NL, int TO, bool GL = false>
 SGNN_DEV void mlp_tail(f32x16 (&y)[TO], f32x16 (&h2)[TH], const f32x16 (&h)[TH], const float* Wm,
                        int ldm, const float* bm_lds, const float* Wl, int ldl, const float* bl_lds) {
   if constexpr (NL == 3) {
     acc_bias<TH>(h2, bm_lds);
-    mfma_from_acc<TH, TH>(h2, Wm, ldm, 0, h);
+    mfma_from_acc<TH, TH, true>(h2, Wm, ldm, 0, h);
     acc_relu<TH>(h2);
     acc_bias<TO>(y, bl_lds);
-    mfma_from_acc<TO, TH>(y, Wl, ldl, 0, h2);
+    mfma_from_acc<TO, TH, GL>(y, Wl, ldl, 0, h2);
   } else {
     acc_bias<TO>(y, bl_lds);
-    mfma_from_acc<TO, TH>(y, Wl, ldl, 0, h);
+    mfma_from_acc<TO, TH, GL>(y, Wl, ldl, 0, h);
   }
 }
 
-template <int TH, int NL, int TO>
+template <int TH, int NL, int TO, bool GL = false>
 SGNN_DEV void mlp_tail(f32x16 (&y)[TO], const f32x16 (&h)[TH], const float* Wm, int ldm,
                        const float* bm_lds, const float* Wl, int ldl, const float* bl_lds) {
   f32x16 h2[TH];
-  mlp_tail<TH, NL, TO>(y, h2, h, Wm, ldm, bm_lds, Wl, ldl, bl_lds);
+  mlp_tail<TH, NL, TO, GL>(y, h2, h, Wm, ldm, bm_lds, Wl, ldl, bl_lds);
 }

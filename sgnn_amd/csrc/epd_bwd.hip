@@ -181,17 +181,24 @@ SGNN_DEV void matvec_t(f32x16 (&acc)[TH], const float* w, int ld, const f32x16 (
   if constexpr (!GW) {
     mfma_from_acc<TH, TK>(acc, w, ld, 0, x);
   } else {
+    // Buffer loads: per-lane part of the address in one VGPR, the row in a
+    // scalar offset, the 32-unit tile in the immediate.  (Plain pointers make
+    // the compiler hoist 32*TH*TK 64-bit addresses out of the item loop.)
     const int l = lane_id() & 31, h = lane_id() >> 5;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(w), (short)0, 0x7ffffff0, 0x00020000);
+    const int voff = 4 * (4 * h * ld + l);
 #pragma unroll
     for (int tk = 0; tk < TK; ++tk)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const float* row = w + (int64_t)(32 * tk + 8 * g + 4 * h + c) * ld + l;
+          const int soff = 4 * (32 * tk + 8 * g + c) * ld;
           float wv[TH];
 #pragma unroll
-          for (int t = 0; t < TH; ++t) wv[t] = row[32 * t];
+          for (int t = 0; t < TH; ++t)
+            wv[t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff + 128 * t, soff, 0));
 #pragma unroll
           for (int t = 0; t < TH; ++t) acc[t] = mfma32(wv[t], x[tk][4 * g + c], acc[t]);
         }
@@ -1020,6 +1027,396 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
 }
 
 // ===========================================================================
+// Hidden 128: per-item chains and weight-gradient GEMMs in separate launches.
+// In the fused form every wave would hold 3-4 [128 x 128] weight-gradient
+// accumulators (192-256 registers) next to the per-item state, which does not
+// fit the 512-entry register file without spilling.  At H = 128 the per-item
+// kernels (wave-independent, no workgroup barriers) therefore write the
+// pre-activation gradients (dy, d2, dh) to scratch, and k_wgrad forms every
+// dW = sum_items A (x) B (plus the bias sums = column sums of A) as a split-K
+// MFMA GEMM over LDS-staged 128-item chunks, into the same slab layouts.
+
+template <int TH>
+SGNN_DEV void wave_colsum(LaneVec<TH>& acc, float* slice, const f32x16 (&x)[TH], int nvalid) {
+  constexpr int ldh = 32 * TH + 4;
+  lds_store_items<TH>(slice, ldh, lane_id() & 31, x);
+  wave_lds_sync();
+  lane_sums<TH>(acc, slice, ldh, nvalid);
+  wave_lds_sync();
+}
+
+struct WgradOp {
+  const float *A, *B;
+  int a_tiled, b_tiled;  // 1: 32-item tiled layout; 0: row-major with leading dim a_ld / b_ld
+  int a_ld, b_ld;
+  float* dst;            // workgroup-0 slab + matrix offset
+  int dst_ld;
+  float* colsum;         // workgroup-0 slab + [W][32*TU] vector offset, or null
+  int64_t slab_stride, nitems;
+  const int32_t* nitems_dev;  // if set: nitems = *nitems_dev (edge count = rowptr[n])
+};
+
+// Stage items [item0, item0 + kChunk) x U units of a tiled or row-major
+// operand as an LDS image [item][unit] (ld U + 4); items >= nitems are zero.
+template <int U>
+SGNN_DEV void stage_items(float* img, const float* src, int tiled, int ld, int64_t item0,
+                          int64_t nitems) {
+  constexpr int ldi = U + 4, Q = U / 4;
+  if (tiled) {
+    constexpr int per_tile = (U / 32) * 4 * 64;  // f32x4 groups per 32-item tile
+    for (int idx = threadIdx.x; idx < 4 * per_tile; idx += blockDim.x) {
+      const int q = idx / per_tile, rem = idx - q * per_tile;
+      const int grp = rem >> 6, lane = rem & 63;
+      const int item = q * 32 + (lane & 31);
+      const int unit = 32 * (grp >> 2) + 8 * (grp & 3) + 4 * (lane >> 5);
+      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+      const int64_t t0 = item0 + q * 32;
+      if (t0 < nitems) {
+        v = ld4(src + (t0 / 32) * (32 * U) + grp * 256 + lane * 4);
+        if (item0 + item >= nitems) v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+      st4(img + item * ldi + unit, v);
+    }
+  } else {
+    for (int idx = threadIdx.x; idx < kChunk * Q; idx += blockDim.x) {
+      const int item = idx / Q, quad = idx - item * Q;
+      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (item0 + item < nitems) v = ld4(src + (item0 + item) * ld + 4 * quad);
+      st4(img + item * ldi + 4 * quad, v);
+    }
+  }
+}
+
+template <int TU, int TV>
+__global__ __launch_bounds__(kBlock) void k_wgrad(WgradOp op) {
+  constexpr int AU = 32 * TU, BU = 32 * TV, lda = AU + 4, ldb = BU + 4;
+  constexpr int NT = (TU * TV + kWaves - 1) / kWaves;
+  constexpr int CPL = AU >= 64 ? AU / 64 : 1;  // column-sum units per lane
+  extern __shared__ float lds[];
+  float* imA = lds;
+  float* imB = imA + kChunk * lda;
+  const int l = lane_id(), w = threadIdx.x >> 6;
+  f32x16 acc[NT];
+  zero_acc<NT>(acc);
+  float cs[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) cs[q] = 0.0f;
+  const int64_t nitems = op.nitems_dev ? (int64_t)*op.nitems_dev : op.nitems;
+  const int64_t nch = (nitems + kChunk - 1) / kChunk;
+  const int64_t c0 = nch * blockIdx.x / gridDim.x, c1 = nch * (blockIdx.x + 1) / gridDim.x;
+  for (int64_t c = c0; c < c1; ++c) {
+    const int64_t item0 = c * kChunk;
+    stage_items<AU>(imA, op.A, op.a_tiled, op.a_ld, item0, nitems);
+    stage_items<BU>(imB, op.B, op.b_tiled, op.b_ld, item0, nitems);
+    __syncthreads();
+    outer_tiles<NT>(acc, TU, TV, imA, lda, 0, imB, ldb, 0);
+    if (op.colsum) {
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        const int u = l + 64 * q;
+        if (u < AU) cs[q] += lane_sum(imA + w * 32 * lda, lda, 32, u);
+      }
+    }
+    __syncthreads();
+  }
+  store_outer<NT>(op.dst + blockIdx.x * op.slab_stride, op.dst_ld, TU, TV, acc);
+  if (op.colsum) {
+    float* v = op.colsum + blockIdx.x * op.slab_stride + w * AU;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q)
+      if (l + 64 * q < AU) v[l + 64 * q] = cs[q];
+  }
+}
+
+// ---- edge layer, H = 128 ---------------------------------------------------
+struct EdgeItemsArgs {
+  EdgeBwdArgs b;
+  float *dy_out, *d2_out;  // tiled scratch
+};
+
+template <int NL>
+__global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
+  constexpr int TH = 4, H = 128, ldh = H + 4;
+  const EdgeBwdArgs& a = p.b;
+  extern __shared__ float lds[];
+  float* gam = lds;
+  stage_vec(gam, a.gamma, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
+  float* sl = gam + H + w * 32 * ldh;
+  LANEVEC(s_dg);
+  LANEVEC(s_db);
+  const int64_t E = a.rowptr[a.n];
+  const int64_t ntiles = (E + 31) / 32;
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t tile = (int64_t)blockIdx.x * kWaves + w; tile < ntiles; tile += nw) {
+    const int64_t base = tile * 32, e = base + j;
+    const int nvalid = clamp_items(E - base);
+    const bool valid = e < E;
+    const int64_t ec = valid ? e : E - 1;
+    const int rv = a.recv[ec];
+    f32x16 dy[TH];
+    {
+      f32x16 dm[TH], yh[TH];
+      load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
+      zero_if<TH>(dm, !valid);
+      load_tiled<TH>(yh, a.yh + tile * (32 * H));
+      acc_layernorm_bwd<TH>(dm, yh, a.rstd[ec], gam, dy);
+      zero_if<TH>(dy, !valid);
+      wave_colsum<TH>(s_db, sl, dm, nvalid);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yh[t][r] = valid ? yh[t][r] * dm[t][r] : 0.0f;
+      wave_colsum<TH>(s_dg, sl, yh, nvalid);
+    }
+    store_tiled<TH>(p.dy_out + tile * (32 * H), dy);
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    if constexpr (NL == 3) {
+      f32x16 d2[TH], act[TH];
+      zero<TH>(d2);
+      matvec_t<TH, TH, true>(d2, a.wl, H, dy);
+      load_tiled<TH>(act, a.hs2 + tile * (32 * H));
+      relu_mask<TH>(d2, act, valid);
+      store_tiled<TH>(p.d2_out + tile * (32 * H), d2);
+      matvec_t<TH, TH, true>(dh, a.wm, H, d2);
+    } else {
+      matvec_t<TH, TH, true>(dh, a.wl, H, dy);
+    }
+    {
+      f32x16 act[TH];
+      load_tiled<TH>(act, a.hs + tile * (32 * H));
+      relu_mask<TH>(dh, act, valid);
+    }
+    {
+      f32x16 de[TH];
+      zero<TH>(de);
+      matvec_t<TH, TH, true>(de, a.we, 3 * H, dh);
+      float* dtile = a.de0t + tile * (32 * H);
+      if (a.de0_accumulate) {
+        f32x16 old[TH];
+        load_tiled<TH>(old, dtile);
+#pragma unroll
+        for (int t = 0; t < TH; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) de[t][r] = old[t][r] + de[t][r] * a.e_scale;
+      } else {
+#pragma unroll
+        for (int t = 0; t < TH; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) de[t][r] *= a.e_scale;
+      }
+      store_tiled<TH>(dtile, de);
+    }
+    if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
+    lds_store_items<TH>(sl, ldh, j, dh);
+    wave_lds_sync();
+    segment_sum_store<TH>(sl, ldh, rv, nvalid, base, tile, a.rowptr, a.du, a.cin, a.cout);
+    wave_lds_sync();
+  }
+  float* v = a.slab + blockIdx.x * a.slab_stride + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, NL);
+  store_lane_vec<TH>(v + kWaves * H, s_dg);
+  store_lane_vec<TH>(v + 2 * kWaves * H, s_db);
+}
+
+// ---- node layer, H = 128 ---------------------------------------------------
+struct NodeItemsArgs {
+  NodeBwdArgs b;
+  float *dy_out, *d2_out, *dh_out;  // row-major [n][H] scratch
+};
+
+template <int NL>
+__global__ __launch_bounds__(kBlock) void k_node_items(NodeItemsArgs p) {
+  constexpr int TH = 4, H = 128, ldh = H + 4;
+  const NodeBwdArgs& a = p.b;
+  extern __shared__ float lds[];
+  float* gam = lds;
+  stage_vec(gam, a.gamma, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
+  float* sl = gam + H + w * 32 * ldh;
+  LANEVEC(s_dg);
+  LANEVEC(s_db);
+  const int64_t ntiles = (a.n + 31) / 32;
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t tile = (int64_t)blockIdx.x * kWaves + w; tile < ntiles; tile += nw) {
+    const int64_t i = tile * 32 + j;
+    const int nvalid = clamp_items(a.n - tile * 32);
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    f32x16 gi[TH], dy[TH];
+    load_row_clayout<TH>(gi, a.g + ic * H);
+    zero_if<TH>(gi, !valid);
+    {
+      f32x16 yh[TH];
+      load_row_clayout<TH>(yh, a.yh + ic * H);
+      acc_layernorm_bwd<TH>(gi, yh, a.rstd[ic], gam, dy);
+      zero_if<TH>(dy, !valid);
+      wave_colsum<TH>(s_db, sl, gi, nvalid);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yh[t][r] = valid ? yh[t][r] * gi[t][r] : 0.0f;
+      wave_colsum<TH>(s_dg, sl, yh, nvalid);
+    }
+    if (valid) store_row_clayout<TH>(p.dy_out + i * H, dy);
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    if constexpr (NL == 3) {
+      f32x16 d2[TH], act[TH];
+      zero<TH>(d2);
+      matvec_t<TH, TH, true>(d2, a.wl, H, dy);
+      load_row_clayout<TH>(act, a.hn2 + ic * H);
+      relu_mask<TH>(d2, act, valid);
+      if (valid) store_row_clayout<TH>(p.d2_out + i * H, d2);
+      matvec_t<TH, TH, true>(dh, a.wm, H, d2);
+    } else {
+      matvec_t<TH, TH, true>(dh, a.wl, H, dy);
+    }
+    {
+      f32x16 act[TH];
+      load_row_clayout<TH>(act, a.hn + ic * H);
+      relu_mask<TH>(dh, act, valid);
+    }
+    if (valid) store_row_clayout<TH>(p.dh_out + i * H, dh);
+    f32x16 o[TH];
+    zero<TH>(o);
+    matvec_t<TH, TH, true>(o, a.w1, 2 * H, dh);
+    if (valid) store_row_clayout<TH>(a.dagg + i * H, o);
+    matvec_t<TH, TH, true>(gi, a.w1 + H, 2 * H, dh);
+    if (valid) store_row_clayout<TH>(a.dxp + i * H, gi);
+  }
+  float* v = a.slab + blockIdx.x * a.slab_stride + slab_nmat_floats(SGNN_SLAB_NODE, H, 0, NL);
+  store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
+  store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
+}
+
+// ---- u/v projections, H = 128 ------------------------------------------------
+struct UvItemsArgs {
+  UvBwdArgs b;
+  float *du_out, *dv_out;  // row-major [n][H]
+};
+
+__global__ __launch_bounds__(kBlock) void k_uv_items(UvItemsArgs p) {
+  constexpr int TH = 4, H = 128;
+  const UvBwdArgs& a = p.b;
+  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
+  const int64_t ntiles = (a.n + 31) / 32;
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t tile = (int64_t)blockIdx.x * kWaves + w; tile < ntiles; tile += nw) {
+    const int64_t i = tile * 32 + j;
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    f32x16 du[TH], dv[TH], gg[TH];
+    load_resolved<TH>(du, a.du, a.cin, a.cout, a.rowptr, ic);
+    zero<TH>(dv);
+    for (int32_t t = a.tptr[ic], t1 = a.tptr[ic + 1]; t < t1; ++t)
+      add_row_clayout<TH>(dv, a.dh_rows + (int64_t)a.tperm[t] * H);
+    load_row_clayout<TH>(gg, a.dxp + ic * H);
+    matvec_t<TH, TH, true>(gg, a.w1, 3 * H, du);
+    matvec_t<TH, TH, true>(gg, a.w1 + H, 3 * H, dv);
+    if (valid) {
+      store_row_clayout<TH>(a.g + i * H, gg);
+      store_row_clayout<TH>(p.du_out + i * H, du);
+      store_row_clayout<TH>(p.dv_out + i * H, dv);
+    }
+  }
+}
+
+// ---- edge encoder, H = 128 ---------------------------------------------------
+struct EncEdgeItemsArgs {
+  EncEdgeBwdArgs b;
+  float *dy_out, *d2_out, *dh_out, *h1_out;  // tiled scratch
+  float* f_out;                              // [E][32] edge features (units >= dim+1 zero)
+};
+
+template <int NL>
+__global__ __launch_bounds__(kBlock) void k_enc_edge_items(EncEdgeItemsArgs p) {
+  constexpr int TH = 4, H = 128, ldh = H + 4, ld1 = 5;
+  const EncEdgeBwdArgs& a = p.b;
+  extern __shared__ float lds[];
+  float* W1 = lds;
+  float* b1 = W1 + H * ld1;
+  float* gam = b1 + H;
+  stage_matrix(W1, ld1, a.w1, a.dim + 1, H, a.dim + 1, H, 4);
+  stage_vec(b1, a.b1, H, H);
+  stage_vec(gam, a.gamma, H, H);
+  __syncthreads();
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  float* sl = gam + H + w * 32 * ldh;
+  LANEVEC(s_dg);
+  LANEVEC(s_db);
+  const int64_t E = a.rowptr[a.n];
+  const int64_t ntiles = (E + 31) / 32;
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t tile = (int64_t)blockIdx.x * kWaves + w; tile < ntiles; tile += nw) {
+    const int64_t base = tile * 32, e = base + j;
+    const int nvalid = clamp_items(E - base);
+    const bool valid = e < E;
+    const int64_t ec = valid ? e : E - 1;
+    f32x16 dy[TH];
+    {
+      f32x16 dm[TH], yh[TH];
+      load_tiled<TH>(dm, a.de0t + tile * (32 * H));
+      zero_if<TH>(dm, !valid);
+      load_tiled<TH>(yh, a.yh + tile * (32 * H));
+      acc_layernorm_bwd<TH>(dm, yh, a.rstd[ec], gam, dy);
+      zero_if<TH>(dy, !valid);
+      wave_colsum<TH>(s_db, sl, dm, nvalid);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yh[t][r] = valid ? yh[t][r] * dm[t][r] : 0.0f;
+      wave_colsum<TH>(s_dg, sl, yh, nvalid);
+    }
+    store_tiled<TH>(p.dy_out + tile * (32 * H), dy);
+    // recompute edge features and the first hidden layer (K = dim+1)
+    const int64_t s = a.send[ec], r = a.recv[ec];
+    float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float ss = 0.0f;
+    for (int cc = 0; cc < a.dim; ++cc) {
+      const float d = __fdiv_rn(__fsub_rn(a.pos[s * a.stride + cc], a.pos[r * a.stride + cc]), a.radius);
+      f[cc] = d;
+      ss = __fadd_rn(ss, __fmul_rn(d, d));
+    }
+    f[a.dim] = sqrtf(ss);
+    if (valid && h == 0) {
+      f32x4 v = {f[0], f[1], f[2], f[3]};
+      st4(p.f_out + e * 32, v);
+      const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int q = 1; q < 8; ++q) st4(p.f_out + e * 32 + 4 * q, z);
+    }
+    f32x16 h1[TH];
+    acc_bias<TH>(h1, b1);
+    mfma_step<TH>(h1, W1, ld1, h, h ? f[1] : f[0]);
+    mfma_step<TH>(h1, W1, ld1, 2 + h, h ? f[3] : f[2]);
+    acc_relu<TH>(h1);
+    zero_if<TH>(h1, !valid);
+    store_tiled<TH>(p.h1_out + tile * (32 * H), h1);
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    if constexpr (NL == 3) {
+      f32x16 d2[TH], act[TH];
+      zero<TH>(d2);
+      matvec_t<TH, TH, true>(d2, a.wl, H, dy);
+      load_tiled<TH>(act, a.h2 + tile * (32 * H));
+      relu_mask<TH>(d2, act, valid);
+      store_tiled<TH>(p.d2_out + tile * (32 * H), d2);
+      matvec_t<TH, TH, true>(dh, a.wm, H, d2);
+    } else {
+      matvec_t<TH, TH, true>(dh, a.wl, H, dy);
+    }
+    relu_mask<TH>(dh, h1, valid);
+    store_tiled<TH>(p.dh_out + tile * (32 * H), dh);
+  }
+  float* v = a.slab + blockIdx.x * a.slab_stride + slab_nmat_floats(SGNN_SLAB_ENC_EDGE, H, 0, NL);
+  store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
+  store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
+}
+
+// ===========================================================================
 // Slab reduction: out[r][c] = scale * sum_g sum_q slab_g[off + q*rep + r*ld + c].
 // Block = 32 consecutive output elements x 8 slab groups; thread q sums slabs
 // g = q, q+8, ... with 4 independent accumulators (coalesced 128-B rows per
@@ -1115,6 +1512,21 @@ void launch_bwd(K kernel, int nslab, size_t lds, void* stream, const A& a) {
                      static_cast<hipStream_t>(stream), a);
 }
 
+template <int TU, int TV>
+void run_wgrad(const WgradOp& op, int nslab, void* stream) {
+  const size_t lds = 4 * (size_t)kChunk * ((32 * TU + 4) + (32 * TV + 4));
+  launch_bwd(k_wgrad<TU, TV>, nslab, lds, stream, op);
+}
+
+WgradOp wg(const float* A, int a_tiled, int a_ld, const float* B, int b_tiled, int b_ld,
+           float* slab, int64_t mat_off, int dst_ld, int64_t vec_off, int64_t slab_stride,
+           int64_t nitems, const int32_t* nitems_dev) {
+  return WgradOp{A, B, a_tiled, b_tiled, a_ld, b_ld, slab + mat_off, dst_ld,
+                 vec_off >= 0 ? slab + vec_off : nullptr, slab_stride, nitems, nitems_dev};
+}
+
+constexpr size_t kItemsLds = 4 * (128 + (size_t)kWaves * 32 * (128 + 4));  // gamma + wave slices
+
 // LDS bytes per kind: weight images (H = 64 only) + vectors + the two
 // [128 items][H+4] operand images of the outer products.
 size_t bwd_lds(int kind, int H, int tkf, int nl) {
@@ -1167,12 +1579,25 @@ extern "C" int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t fe
   return slab_nmat_floats(kind, hidden, fpad, nlin) + slab_nvec_floats(kind, hidden, nlin);
 }
 
+extern "C" int64_t sgnn_bwd_scratch_floats(int32_t kind, int32_t hidden, int64_t nitems, int32_t nlin) {
+  if (hidden != 128) return 0;
+  const int64_t H = hidden, pad = 32 * ((nitems + 31) / 32);
+  (void)nlin;
+  switch (kind) {
+    case SGNN_SLAB_EDGE: return 2 * pad * H;                // dy, d2 (tiled)
+    case SGNN_SLAB_NODE: return 3 * nitems * H;             // dy, d2, dh
+    case SGNN_SLAB_UV: return 2 * nitems * H;               // dU, dV
+    case SGNN_SLAB_ENC_EDGE: return 4 * pad * H + pad * 32; // dy, d2, dh, h1 (tiled) + features
+    default: return 0;
+  }
+}
+
 extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t* send,
                                    const int32_t* recv, int64_t n, const sgnn_saves* saves,
                                    const float* e0t, float e_scale, const sgnn_mlp* edge_fn,
                                    float* du, float* cin, float* cout, float* dh_rows, float* de0t,
                                    int32_t de0_accumulate, float* slab, int32_t nslab,
-                                   void* stream) {
+                                   float* scratch, int64_t edge_cap, void* stream) {
   using namespace sgnn;
   if (!edge_fn || !dagg || !rowptr || !send || !recv || !saves || !saves->h || !saves->yhat ||
       !saves->rstd || !e0t || !du || !cin || !cout || !dh_rows || !de0t || !slab || nslab < 1 ||
@@ -1186,6 +1611,23 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
                 e_scale, last_w(edge_fn), mid_w(edge_fn), edge_fn->w1 + 2 * H, edge_fn->ln_g, du,
                 cin, cout, dh_rows, de0t, de0_accumulate, slab,
                 sgnn_bwd_slab_floats(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin)};
+  if (H == 128) {
+    if (!scratch || edge_cap < 1) return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: H=128 needs scratch");
+    const int nl = edge_fn->nlin;
+    const int64_t pad = 32 * ((edge_cap + 31) / 32);
+    EdgeItemsArgs p{a, scratch, scratch + pad * H};
+    if (nl == 3) launch_bwd(k_edge_items<3>, nslab, kItemsLds, stream, p);
+    else launch_bwd(k_edge_items<2>, nslab, kItemsLds, stream, p);
+    const int64_t vb = slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, nl), W = kWaves, ss = a.slab_stride;
+    const int32_t* Edev = rowptr + n;
+    const float* hl = nl == 3 ? saves->h2 : saves->h;
+    run_wgrad<4, 4>(wg(p.dy_out, 1, 0, hl, 1, 0, slab, 0, H, vb, ss, 0, Edev), nslab, stream);
+    run_wgrad<4, 4>(wg(dh_rows, 0, H, e0t, 1, 0, slab, H * H, H, -1, ss, 0, Edev), nslab, stream);
+    if (nl == 3)
+      run_wgrad<4, 4>(wg(p.d2_out, 1, 0, saves->h, 1, 0, slab, 2 * H * H, H, vb + 3 * W * H, ss, 0, Edev),
+                      nslab, stream);
+    return check_launch("edge_layer_bwd");
+  }
   const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin);
   SGNN_BWD_DISPATCH(H, edge_fn->nlin, (launch_bwd(k_edge_bwd<TH_, NL_>, nslab, lds, stream, a)));
   return check_launch("edge_layer_bwd");
@@ -1193,7 +1635,8 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
 
 extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* saves,
                                    const float* x_in, const sgnn_mlp* node_fn, float* dagg,
-                                   float* dxp, float* slab, int32_t nslab, void* stream) {
+                                   float* dxp, float* slab, int32_t nslab, float* scratch,
+                                   void* stream) {
   using namespace sgnn;
   if (!node_fn || !g || !saves || !saves->yhat || !saves->rstd || !saves->h || !saves->agg ||
       !x_in || !dagg || !dxp || !slab || nslab < 1 || n <= 0)
@@ -1205,6 +1648,24 @@ extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* 
   NodeBwdArgs a{g, n, saves->yhat, saves->rstd, saves->h, saves->h2, saves->agg, x_in, node_fn->w1,
                 last_w(node_fn), mid_w(node_fn), node_fn->ln_g, dagg, dxp, slab,
                 sgnn_bwd_slab_floats(SGNN_SLAB_NODE, H, 0, node_fn->nlin)};
+  if (H == 128) {
+    if (!scratch) return set_error(SGNN_ERR_INVALID, "node_layer_bwd: H=128 needs scratch");
+    const int nl = node_fn->nlin;
+    NodeItemsArgs p{a, scratch, scratch + n * H, scratch + 2 * n * H};
+    if (nl == 3) launch_bwd(k_node_items<3>, nslab, kItemsLds, stream, p);
+    else launch_bwd(k_node_items<2>, nslab, kItemsLds, stream, p);
+    const int64_t vb = slab_nmat_floats(SGNN_SLAB_NODE, H, 0, nl), W = kWaves, ss = a.slab_stride;
+    const float* hl = nl == 3 ? saves->h2 : saves->h;
+    run_wgrad<4, 4>(wg(p.dy_out, 0, H, hl, 0, H, slab, 0, H, vb + W * H, ss, n, nullptr), nslab, stream);
+    run_wgrad<4, 4>(wg(p.dh_out, 0, H, saves->agg, 0, H, slab, H * H, 2 * H, vb, ss, n, nullptr), nslab,
+                    stream);
+    run_wgrad<4, 4>(wg(p.dh_out, 0, H, x_in, 0, H, slab, H * H + H, 2 * H, -1, ss, n, nullptr), nslab,
+                    stream);
+    if (nl == 3)
+      run_wgrad<4, 4>(wg(p.d2_out, 0, H, saves->h, 0, H, slab, 3 * H * H, H, vb + 4 * W * H, ss, n, nullptr),
+                      nslab, stream);
+    return check_launch("node_layer_bwd");
+  }
   const size_t lds = bwd_lds(SGNN_SLAB_NODE, H, 0, node_fn->nlin);
   SGNN_BWD_DISPATCH(H, node_fn->nlin, (launch_bwd(k_node_bwd<TH_, NL_>, nslab, lds, stream, a)));
   return check_launch("node_layer_bwd");
@@ -1214,7 +1675,7 @@ extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, 
                            const int32_t* rowptr, const float* dh_rows, const int32_t* tptr,
                            const int32_t* tperm, const float* x_in, int64_t n,
                            const sgnn_mlp* edge_fn, float* g, float* slab, int32_t nslab,
-                           void* stream) {
+                           float* scratch, void* stream) {
   using namespace sgnn;
   if (!edge_fn || !dxp || !du || !cin || !cout || !rowptr || !dh_rows || !tptr || !tperm ||
       !x_in || !g || !slab || nslab < 1 || n <= 0)
@@ -1224,9 +1685,17 @@ extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, 
   const int H = edge_fn->hidden;
   UvBwdArgs a{dxp, du, cin, cout, rowptr, dh_rows, tptr, tperm, x_in, n, edge_fn->w1, g, slab,
               sgnn_bwd_slab_floats(SGNN_SLAB_UV, H, 0, edge_fn->nlin)};
+  if (H == 128) {
+    if (!scratch) return set_error(SGNN_ERR_INVALID, "uv_bwd: H=128 needs scratch");
+    UvItemsArgs p{a, scratch, scratch + n * H};
+    launch_bwd(k_uv_items, nslab, 0, stream, p);
+    const int64_t ss = a.slab_stride;
+    run_wgrad<4, 4>(wg(p.du_out, 0, H, x_in, 0, H, slab, 0, 2 * H, 2 * H * H, ss, n, nullptr), nslab, stream);
+    run_wgrad<4, 4>(wg(p.dv_out, 0, H, x_in, 0, H, slab, H, 2 * H, -1, ss, n, nullptr), nslab, stream);
+    return check_launch("uv_bwd");
+  }
   const size_t lds = bwd_lds(SGNN_SLAB_UV, H, 0, 2);
-  if (H == 64) launch_bwd(k_uv_bwd<2>, nslab, lds, stream, a);
-  else launch_bwd(k_uv_bwd<4>, nslab, lds, stream, a);
+  launch_bwd(k_uv_bwd<2>, nslab, lds, stream, a);
   return check_launch("uv_bwd");
 }
 
@@ -1292,7 +1761,8 @@ extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_
                                      int32_t dim, float radius, const int32_t* rowptr,
                                      const int32_t* send, const int32_t* recv, int64_t n,
                                      const sgnn_saves* saves, const sgnn_mlp* enc, float* slab,
-                                     int32_t nslab, void* stream) {
+                                     int32_t nslab, float* scratch, int64_t edge_cap,
+                                     void* stream) {
   using namespace sgnn;
   if (!enc || !de0t || !pos || !rowptr || !send || !recv || !saves || !saves->yhat ||
       !saves->rstd || !slab || nslab < 1 || n <= 0)
@@ -1304,6 +1774,25 @@ extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_
   EncEdgeBwdArgs a{de0t, pos, pos_stride, dim, radius, rowptr, send, recv, n, saves->h2,
                    saves->yhat, saves->rstd, enc->w1, enc->b1, last_w(enc), mid_w(enc), enc->ln_g,
                    slab, sgnn_bwd_slab_floats(SGNN_SLAB_ENC_EDGE, H, 0, enc->nlin)};
+  if (H == 128) {
+    if (!scratch || edge_cap < 1) return set_error(SGNN_ERR_INVALID, "encode_edges_bwd: H=128 needs scratch");
+    const int nl = enc->nlin;
+    const int64_t pad = 32 * ((edge_cap + 31) / 32);
+    EncEdgeItemsArgs p{a, scratch, scratch + pad * H, scratch + 2 * pad * H, scratch + 3 * pad * H,
+                       scratch + 4 * pad * H};
+    const size_t lds = kItemsLds + 4 * (size_t)(128 * 5 + 128);
+    if (nl == 3) launch_bwd(k_enc_edge_items<3>, nslab, lds, stream, p);
+    else launch_bwd(k_enc_edge_items<2>, nslab, lds, stream, p);
+    const int64_t vb = slab_nmat_floats(SGNN_SLAB_ENC_EDGE, H, 0, nl), W = kWaves, ss = a.slab_stride;
+    const int32_t* Edev = rowptr + n;
+    const float* hl = nl == 3 ? saves->h2 : p.h1_out;
+    run_wgrad<4, 4>(wg(p.dy_out, 1, 0, hl, 1, 0, slab, 0, H, vb + W * H, ss, 0, Edev), nslab, stream);
+    run_wgrad<4, 1>(wg(p.dh_out, 1, 0, p.f_out, 0, 32, slab, H * H, 32, vb, ss, 0, Edev), nslab, stream);
+    if (nl == 3)
+      run_wgrad<4, 4>(wg(p.d2_out, 1, 0, p.h1_out, 1, 0, slab, H * H + H * 32, H, vb + 4 * W * H, ss, 0, Edev),
+                      nslab, stream);
+    return check_launch("encode_edges_bwd");
+  }
   const size_t lds = bwd_lds(SGNN_SLAB_ENC_EDGE, H, 0, enc->nlin);
   SGNN_BWD_DISPATCH(H, enc->nlin, (launch_bwd(k_enc_edge_bwd<TH_, NL_>, nslab, lds, stream, a)));
   return check_launch("encode_edges_bwd");

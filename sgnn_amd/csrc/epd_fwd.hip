@@ -46,27 +46,27 @@ struct EncNodeArgs {
   sgnn_saves sv;
 };
 
-template <int TH>
+template <int TH, bool G = false>
 SGNN_DEV void store_uv(const float* Wi, const float* Wj, const float* b1e, int ldh,
                        const f32x16 (&x)[TH], float* u_row, float* v_row, bool valid) {
   f32x16 acc[TH];
   acc_bias<TH>(acc, b1e);
-  mfma_from_acc<TH, TH>(acc, Wi, ldh, 0, x);
+  mfma_from_acc<TH, TH, G>(acc, Wi, ldh, 0, x);
   if (valid) store_row_clayout<TH>(u_row, acc);
   acc_bias<TH>(acc, nullptr);
-  mfma_from_acc<TH, TH>(acc, Wj, ldh, 0, x);
+  mfma_from_acc<TH, TH, G>(acc, Wj, ldh, 0, x);
   if (valid) store_row_clayout<TH>(v_row, acc);
 }
 
-template <int TH>
+template <int TH, bool G = false>
 SGNN_DEV void store_uv2(const float* Wi, int ldi, const float* Wj, int ldj, const float* b1e,
                         const f32x16 (&x)[TH], float* u_row, float* v_row, bool valid) {
   f32x16 acc[TH];
   acc_bias<TH>(acc, b1e);
-  mfma_from_acc<TH, TH>(acc, Wi, ldi, 0, x);
+  mfma_from_acc<TH, TH, G>(acc, Wi, ldi, 0, x);
   if (valid) store_row_clayout<TH>(u_row, acc);
   acc_bias<TH>(acc, nullptr);
-  mfma_from_acc<TH, TH>(acc, Wj, ldj, 0, x);
+  mfma_from_acc<TH, TH, G>(acc, Wj, ldj, 0, x);
   if (valid) store_row_clayout<TH>(v_row, acc);
 }
 
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
     acc_relu<TH>(hacc);
     if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
     f32x16 y[TH], h2[TH];
-    mlp_tail<TH, NL, TH>(y, h2, hacc, a.wm, H, bm, W2, ldh, b2);
+    mlp_tail<TH, NL, TH, GW>(y, h2, hacc, a.wm, H, bm, W2, ldh, b2);
     if (TRAIN && NL == 3 && valid) store_row_clayout<TH>(a.sv.h2 + i * H, h2);
     if (TRAIN) {
       f32x16 yh[TH];
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
       acc_layernorm<TH>(y, g, bb);
     }
     if (valid) store_row_clayout<TH>(a.x0 + i * H, y);
-    store_uv<TH>(Wi, Wj, b1e, ldwe, y, a.u + i * H, a.v + i * H, valid);
+    store_uv<TH, GW>(Wi, Wj, b1e, ldwe, y, a.u + i * H, a.v + i * H, valid);
   }
 }
 
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
     mfma_step<TH>(hacc, W1, ld1, 2 + h, h ? f[3] : f[2]);
     acc_relu<TH>(hacc);
     f32x16 y[TH], h2[TH];
-    mlp_tail<TH, NL, TH>(y, h2, hacc, a.wm, H, bm, W2, ldh, b2);
+    mlp_tail<TH, NL, TH, GW>(y, h2, hacc, a.wm, H, bm, W2, ldh, b2);
     if (TRAIN && NL == 3) store_tiled<TH>(a.sv.h2 + tile * (32 * H), h2);
     if (TRAIN) {
       f32x16 yh[TH];
@@ -289,11 +289,11 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     const float* src = a.e0t + tile * (32 * H) + l * 4;
 #pragma unroll
     for (int q = 0; q < TH * 4; ++q) xg[q] = ld4(src + q * 256);
-    mfma_from_groups<TH, TH>(hacc, We, lde, 0, xg, a.e_scale);
+    mfma_from_groups<TH, TH, GW>(hacc, We, lde, 0, xg, a.e_scale);
     acc_relu<TH>(hacc);
     if (TRAIN) store_tiled<TH>(a.sv.h + tile * (32 * H), hacc);
     f32x16 y[TH], h2[TH];
-    mlp_tail<TH, NL, TH>(y, h2, hacc, a.wm, H, bm, W2, ldw2, b2);
+    mlp_tail<TH, NL, TH, GW>(y, h2, hacc, a.wm, H, bm, W2, ldw2, b2);
     if (TRAIN && NL == 3) store_tiled<TH>(a.sv.h2 + tile * (32 * H), h2);
     if (TRAIN) {
       f32x16 yh[TH];
@@ -448,12 +448,12 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
     load_row_clayout<TH>(x, a.x_in + ic * H);
     f32x16 hacc[TH];
     acc_bias<TH>(hacc, b1);
-    mfma_from_acc<TH, TH>(hacc, W1, ld2, 0, ag);   // graph_network.py:220 cat([aggr, x])
-    mfma_from_acc<TH, TH>(hacc, W1, ld2, H, x);
+    mfma_from_acc<TH, TH, GW>(hacc, W1, ld2, 0, ag);   // graph_network.py:220 cat([aggr, x])
+    mfma_from_acc<TH, TH, GW>(hacc, W1, ld2, H, x);
     acc_relu<TH>(hacc);
     if (TRAIN && valid) store_row_clayout<TH>(a.sv.h + i * H, hacc);
     f32x16 y[TH], h2[TH];
-    mlp_tail<TH, NL, TH>(y, h2, hacc, a.wm, H, bm, W2, ldw2, b2);
+    mlp_tail<TH, NL, TH, GW>(y, h2, hacc, a.wm, H, bm, W2, ldw2, b2);
     if (TRAIN && NL == 3 && valid) store_row_clayout<TH>(a.sv.h2 + i * H, h2);
     if (TRAIN) {
       f32x16 yh[TH];
@@ -472,11 +472,11 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
       for (int r = 0; r < 16; ++r) x[t][r] = y[t][r] + x[t][r];  // :176 residual
     if (valid && a.x_out) store_row_clayout<TH>(a.x_out + i * H, x);
     if (MODE == 0) {
-      store_uv2<TH>(Wa, lda, Wb, ldb, ba, x, a.u + i * H, a.v + i * H, valid);
+      store_uv2<TH, GW>(Wa, lda, Wb, ldb, ba, x, a.u + i * H, a.v + i * H, valid);
     } else {
       f32x16 hd[TH];
       acc_bias<TH>(hd, ba);
-      mfma_from_acc<TH, TH>(hd, Wa, lda, 0, x);
+      mfma_from_acc<TH, TH, GW>(hd, Wa, lda, 0, x);
       acc_relu<TH>(hd);
       if (TRAIN && valid) store_row_clayout<TH>(a.sv.hd + i * H, hd);
       f32x16 o[1], hd2[TH];

@@ -102,6 +102,9 @@ class MSTrainWorkspace:
         self.feat = gnn.nnode_in
         self.slabs = SlabArena(H, self.nlin, self.feat, keys, self.nslab_of, device)
         self.loss_out = torch.zeros(8, **f32)
+        sc = lambda kind, items: int(L.sgnn_bwd_scratch_floats(kind, H, items, self.nlin))
+        self.scratch = e(max(1, sc(_hip.SLAB_EDGE, max(cap.values())), sc(_hip.SLAB_ENC_EDGE, max(cap.values())),
+                             sc(_hip.SLAB_NODE, n), sc(_hip.SLAB_UV, n)))
         self._descs_key = None
 
     def slab(self, kind: int, k: int = 0) -> int:
@@ -201,7 +204,8 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
         nsv = _saves(h=tw.n_h[b], yhat=tw.n_yh[b], rstd=tw.n_rstd[b], agg=tw.n_agg[b], h2=tw.n_h2[b])
         check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, ctypes.byref(nsv), tw.xs[b].data_ptr(),
                                     ctypes.byref(pk.node[b]), tw.dagg.data_ptr(), tw.dxp.data_ptr(),
-                                    tw.slab(_hip.SLAB_NODE, b), ns[_hip.SLAB_NODE], s), "sgnn_node_layer_bwd")
+                                    tw.slab(_hip.SLAB_NODE, b), ns[_hip.SLAB_NODE],
+                                    tw.scratch.data_ptr(), s), "sgnn_node_layer_bwd")
         esv = _saves(h=tw.e_h[b], yhat=tw.e_yh[b], rstd=tw.e_rstd[b], h2=tw.e_h2[b])
         with _Timer(timers, "k_edge_bwd"):
             check(L.sgnn_edge_layer_bwd(tw.dagg.data_ptr(), g.rowptr.data_ptr(), g.send.data_ptr(),
@@ -209,13 +213,15 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                                         tw.scales[b], ctypes.byref(pk.edge[b]), tw.du.data_ptr(),
                                         ws.cin.data_ptr(), ws.cout.data_ptr(), tw.dh_rows.data_ptr(),
                                         tw.de0t[kind].data_ptr(), int(kind in seen),
-                                        tw.slab(_hip.SLAB_EDGE, b), ns[_hip.SLAB_EDGE], s),
+                                        tw.slab(_hip.SLAB_EDGE, b), ns[_hip.SLAB_EDGE],
+                                        tw.scratch.data_ptr(), g.edge_cap, s),
                   "sgnn_edge_layer_bwd")
         seen.add(kind)
         check(L.sgnn_uv_bwd(tw.dxp.data_ptr(), tw.du.data_ptr(), ws.cin.data_ptr(), ws.cout.data_ptr(),
                             g.rowptr.data_ptr(), tw.dh_rows.data_ptr(), tw.tptr[kind].data_ptr(),
                             tw.tperm[kind].data_ptr(), tw.xs[b].data_ptr(), n, ctypes.byref(pk.edge[b]),
-                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, b), ns[_hip.SLAB_UV], s), "sgnn_uv_bwd")
+                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, b), ns[_hip.SLAB_UV],
+                            tw.scratch.data_ptr(), s), "sgnn_uv_bwd")
     check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, inp.vel_mean.data_ptr(),
                                   inp.vel_std.data_ptr(), float(grid_radius), float(grid_radius),
                                   ctypes.byref(_saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd,
@@ -232,7 +238,8 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                                       g.recv.data_ptr(), n,
                                       ctypes.byref(_saves(yhat=tw.ee_yh[k], rstd=tw.ee_rstd[k], h2=tw.ee_h2[k])),
                                       ctypes.byref(pk.enc_edge[k]), tw.slab(_hip.SLAB_ENC_EDGE, KIND_SLOT[k]),
-                                      ns[_hip.SLAB_ENC_EDGE], s), "sgnn_encode_edges_bwd")
+                                      ns[_hip.SLAB_ENC_EDGE], tw.scratch.data_ptr(), g.edge_cap, s),
+                  "sgnn_encode_edges_bwd")
     check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
                               tw._nblocks, s), "sgnn_reduce_slabs")
 

@@ -265,6 +265,9 @@ class TrainWorkspace:
         self.slabs = SlabArena(H, self.nlin, self.feat, keys, self.nslab_of, device)
         self.arena = self.slabs.arena
         self.loss_out = torch.zeros(8, **f32)
+        sc = lambda kind, items: int(L.sgnn_bwd_scratch_floats(kind, H, items, self.nlin))
+        self.scratch = e(max(1, sc(_hip.SLAB_EDGE, cap), sc(_hip.SLAB_ENC_EDGE, cap),
+                             sc(_hip.SLAB_NODE, n), sc(_hip.SLAB_UV, n)))
         self._descs_key = None
 
     def slab(self, kind: int, k: int = 0) -> int:
@@ -400,7 +403,8 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
         nsv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], h2=tw.n_h2[k])
         check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, ctypes.byref(nsv), tw.xs[k].data_ptr(),
                                     ctypes.byref(pk.node[k]), tw.dagg.data_ptr(), tw.dxp.data_ptr(),
-                                    tw.slab(_hip.SLAB_NODE, k), tw.nslab_of[_hip.SLAB_NODE], s),
+                                    tw.slab(_hip.SLAB_NODE, k), tw.nslab_of[_hip.SLAB_NODE],
+                                    tw.scratch.data_ptr(), s),
               "sgnn_node_layer_bwd")
         with _Timer(timers, "k_edge_bwd"):
           esv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k], h2=tw.e_h2[k])
@@ -408,12 +412,14 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                     ws.recv.data_ptr(), n, ctypes.byref(esv), ws.e0t.data_ptr(), float(2.0 ** k),
                                     ctypes.byref(pk.edge[k]), tw.du.data_ptr(), ws.cin.data_ptr(),
                                     ws.cout.data_ptr(), tw.dh_rows.data_ptr(), tw.de0t.data_ptr(),
-                                    int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), tw.nslab_of[_hip.SLAB_EDGE], s),
+                                    int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), tw.nslab_of[_hip.SLAB_EDGE],
+                                    tw.scratch.data_ptr(), ws.edge_cap, s),
               "sgnn_edge_layer_bwd")
         check(L.sgnn_uv_bwd(tw.dxp.data_ptr(), tw.du.data_ptr(), ws.cin.data_ptr(), ws.cout.data_ptr(),
                             ws.rowptr.data_ptr(), tw.dh_rows.data_ptr(), tw.tptr.data_ptr(),
                             tw.tperm.data_ptr(), tw.xs[k].data_ptr(), n, ctypes.byref(pk.edge[k]),
-                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV], s),
+                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV],
+                            tw.scratch.data_ptr(), s),
               "sgnn_uv_bwd")
     check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d,
                                   inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius), 1.0,
@@ -427,7 +433,7 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                   ws.recv.data_ptr(), n,
                                   ctypes.byref(_saves(yhat=tw.ee_yh, rstd=tw.ee_rstd, h2=tw.ee_h2)),
                                   ctypes.byref(pk.enc_edge), tw.slab(_hip.SLAB_ENC_EDGE),
-                                  tw.nslab_of[_hip.SLAB_ENC_EDGE], s),
+                                  tw.nslab_of[_hip.SLAB_ENC_EDGE], tw.scratch.data_ptr(), ws.edge_cap, s),
           "sgnn_encode_edges_bwd")
     check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
                               tw._nblocks, s), "sgnn_reduce_slabs")
