@@ -414,6 +414,7 @@ def bench_ms_train(args, world, rank, device):
                    "parallelism": f"dp{world} (whole-graph, RCCL all-reduce)" if world > 1 else "single GPU"},
         "M_edge_messages_per_s": eb * args.steps * world / dt / 1e6,
         "final_loss": float(out["loss"]),
+        "hbm_peak_gib": torch.cuda.max_memory_allocated(device) / 2 ** 30,
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved / 1e12, "peak": MFMA_F32_PEAK / 1e12,
                      "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK, "traffic": None,
                      "avg_launch_us": kstats[dom] * 1e6, "flops_per_launch": flops_bwd},
