@@ -87,7 +87,21 @@ int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n, int32_t d
  * rowptr [n+1], send/recv [E]. */
 size_t sgnn_coo_workspace_bytes(int64_t n, int64_t E);
 int sgnn_coo_to_csr(const int64_t* src, const int64_t* dst, int64_t E, int64_t n, void* workspace,
-                    int32_t* rowptr, int32_t* send, int32_t* recv, void* stream);
+                    int32_t* rowptr, int32_t* send, int32_t* recv, int32_t* perm, void* stream);
+/* perm (optional, [E]): CSR position -> original COO edge id. */
+
+/* EncodeProcessDecode.forward(x, edge_index, edge_features) on explicit
+ * features (graph_network.py:388-406; MultiScaleGNN.forward
+ * multi_scale_gnn.py:262-326): the encoders read given rows instead of
+ * deriving features from positions.  x: [n][feat] row-major; e: [E][fe] in the
+ * COO order of edge_index, read through perm from sgnn_coo_to_csr.  The rest
+ * of the chain is unchanged (sgnn_edge_layer / sgnn_node_layer /
+ * sgnn_node_layer_decode with pos_seq = NULL: decoder output only). */
+int sgnn_encode_node_features(const float* x, int64_t n, int32_t feat, const sgnn_mlp* enc,
+                              const sgnn_mlp* edge0, float* x0, float* u, float* v, void* stream);
+int sgnn_encode_edge_features(const float* e, int32_t fe, const int32_t* perm,
+                              const int32_t* rowptr, int64_t n, int64_t edge_cap,
+                              const sgnn_mlp* enc, float* e0t, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Encoder, node side: node features of LearnedSimulator._encoder_preprocessor

@@ -75,7 +75,11 @@ SIGNATURES = {
                                               c_void_p, P_SAVES, c_void_p]),
     "sgnn_coo_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64]),
     "sgnn_coo_to_csr": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
-                                       c_void_p, c_void_p, c_void_p]),
+                                       c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sgnn_encode_node_features": (ctypes.c_int, [c_void_p, c_int64, c_int32, P_MLP, P_MLP, c_void_p,
+                                                 c_void_p, c_void_p, c_void_p]),
+    "sgnn_encode_edge_features": (ctypes.c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_int64,
+                                                 P_MLP, c_void_p, c_void_p]),
     "sgnn_bwd_slab_floats": (c_int64, [c_int32, c_int32, c_int32, c_int32]),
     "sgnn_bwd_scratch_floats": (c_int64, [c_int32, c_int32, c_int64, c_int32]),
     "sgnn_reduce_slabs": (ctypes.c_int, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),

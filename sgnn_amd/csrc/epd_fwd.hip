@@ -44,6 +44,7 @@ struct EncNodeArgs {
   const float *we, *be;                     // edge0 W1 [H][3H], b1
   float *x0, *u, *v;
   sgnn_saves sv;
+  const float* feat_in;  // explicit node features [n][feat] (EncodeProcessDecode.forward) or null
 };
 
 template <int TH, bool G = false>
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
     const int64_t i = node0 + j;
     const bool valid = i < a.n;
     const int64_t ic = valid ? i : a.n - 1;
-    const float* p = a.pos_seq + ic * a.T * a.dim;
+    const float* p = a.feat_in ? nullptr : a.pos_seq + ic * a.T * a.dim;
     f32x16 xf[TKF];
 #pragma unroll
     for (int tk = 0; tk < TKF; ++tk)
@@ -116,7 +117,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
       for (int r = 0; r < 16; ++r) {
         const int f = 32 * tk + crow(r, h);
         float val = 0.0f;
-        if (f < nvel) {  // learned_simulator.py:258,272-278
+        if (a.feat_in) {  // explicit features (graph_network.py:403 Encoder input)
+          if (f < a.feat) val = a.feat_in[ic * a.feat + f];
+        } else if (f < nvel) {  // learned_simulator.py:258,272-278
           const int t = f / a.dim, c = f - t * a.dim;
           const float vel = __fsub_rn(p[(t + 1) * a.dim + c], p[t * a.dim + c]);
           val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[c]), a.vel_std[c]);
@@ -163,6 +166,9 @@ struct EncEdgeArgs {
   float* e0t;
   sgnn_saves sv;
   const float *wm, *bm;
+  const float* efeat_in;  // explicit edge features [E][fe] in COO order, or null
+  const int32_t* perm;    // CSR position -> COO edge id (with efeat_in)
+  int fe;
 };
 
 template <int TH, bool TRAIN, int NL>
@@ -194,15 +200,20 @@ __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
   for (int64_t tile = gw; tile < ntiles; tile += nw) {
     const int64_t e = tile * 32 + j;
     const int64_t ec = e < E ? e : E - 1;
-    const int64_t s = a.send[ec], r = a.recv[ec];
     float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    float ss = 0.0f;
-    for (int c = 0; c < a.dim; ++c) {  // learned_simulator.py:299-312
-      const float d = __fdiv_rn(__fsub_rn(a.pos[s * a.stride + c], a.pos[r * a.stride + c]), a.radius);
-      f[c] = d;
-      ss = __fadd_rn(ss, __fmul_rn(d, d));
+    if (a.efeat_in) {  // explicit features (graph_network.py:403 Encoder input)
+      const int64_t src = a.perm[ec];
+      for (int c = 0; c < a.fe; ++c) f[c] = a.efeat_in[src * a.fe + c];
+    } else {
+      const int64_t s = a.send[ec], r = a.recv[ec];
+      float ss = 0.0f;
+      for (int c = 0; c < a.dim; ++c) {  // learned_simulator.py:299-312
+        const float d = __fdiv_rn(__fsub_rn(a.pos[s * a.stride + c], a.pos[r * a.stride + c]), a.radius);
+        f[c] = d;
+        ss = __fadd_rn(ss, __fmul_rn(d, d));
+      }
+      f[a.dim] = sqrtf(ss);
     }
-    f[a.dim] = sqrtf(ss);
     f32x16 hacc[TH];
     acc_bias<TH>(hacc, b1);
     mfma_step<TH>(hacc, W1, ld1, h, h ? f[1] : f[0]);
@@ -482,7 +493,9 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
       f32x16 o[1], hd2[TH];
       mlp_tail<TH, NL, 1>(o, hd2, hd, a.wdm, H, bdm, Wb, ldh, bd2);
       if (TRAIN && NL == 3 && valid) store_row_clayout<TH>(a.sv.hd2 + i * H, hd2);
-      if (valid && h == 0) {  // lanes with h == 0 hold units 0..3 in registers 0..3
+      if (valid && h == 0 && !a.pos_seq) {  // decoder output only (EncodeProcessDecode.forward)
+        for (int c = 0; c <= a.dim; ++c) a.pred[i * (a.dim + 1) + c] = o[0][c];
+      } else if (valid && h == 0) {  // lanes with h == 0 hold units 0..3 in registers 0..3
         const int D = a.dim;
         for (int c = 0; c <= D; ++c) a.pred[i * (D + 1) + c] = o[0][c];
         const float* p = a.pos_seq + i * a.T * D;
@@ -736,8 +749,8 @@ extern "C" int sgnn_node_layer_decode(const float* x_in, const float* agg, const
                                       const sgnn_saves* saves, void* stream) {
   using namespace sgnn;
   if (n <= 0) return SGNN_OK;
-  if (!x_in || !agg || !cin || !cout || !rowptr || !pos_seq || !acc_mean || !acc_std || !pred ||
-      !next_pos || T < 2 || dim < 1 || dim > 3)
+  if (!x_in || !agg || !cin || !cout || !rowptr || !pred || dim < 1 || dim > 3 ||
+      (pos_seq && (!acc_mean || !acc_std || !next_pos || T < 2)))
     return set_error(SGNN_ERR_INVALID, "node_layer_decode: bad arguments");
   const int H = node_fn ? node_fn->hidden : 0;
   int st = check_mlp(decoder, H, H, dim + 1, false, "node_layer_decode: decoder MLP shape");
@@ -748,6 +761,59 @@ extern "C" int sgnn_node_layer_decode(const float* x_in, const float* agg, const
   a.wdm = mid_w(decoder); a.bdm = mid_b(decoder);
   a.pos_seq = pos_seq; a.T = T; a.dim = dim; a.acc_mean = acc_mean; a.acc_std = acc_std;
   a.pred = pred; a.next_pos = next_pos; a.window_out = window_out; a.x_out = x_out;
-  if (window_out == pos_seq) return set_error(SGNN_ERR_INVALID, "node_layer_decode: window_out aliases pos_seq");
+  if (window_out && window_out == pos_seq)
+    return set_error(SGNN_ERR_INVALID, "node_layer_decode: window_out aliases pos_seq");
   return node_layer_common(a, node_fn, 1, decoder->nlin, saves, stream);
+}
+
+// ---------------------------------------------------------------------------
+// EncodeProcessDecode.forward(x, edge_index, edge_features) on explicit
+// features (graph_network.py:388-406): the encoders read given feature rows
+// instead of deriving them from positions.
+extern "C" int sgnn_encode_node_features(const float* x, int64_t n, int32_t feat,
+                                         const sgnn_mlp* enc, const sgnn_mlp* edge0, float* x0,
+                                         float* u, float* v, void* stream) {
+  using namespace sgnn;
+  if (n <= 0) return SGNN_OK;
+  if (!x || !x0 || !u || !v || !enc || feat < 1) return set_error(SGNN_ERR_INVALID, "encode_node_features: bad arguments");
+  const int H = enc->hidden;
+  int st = check_mlp(enc, feat, H, H, true, "encode_node_features: encoder MLP shape");
+  if (!st) st = check_mlp(edge0, 3 * H, H, H, true, "encode_node_features: edge0 MLP shape");
+  if (st) return st;
+  if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "encode_node_features: hidden must be 64 or 128");
+  EncNodeArgs a{nullptr, n, 2, 1, nullptr, nullptr, 0, 0, nullptr, nullptr, 0.0f, feat, enc->w1,
+                enc->b1, last_w(enc), last_b(enc), enc->ln_g, enc->ln_b, mid_w(enc), mid_b(enc),
+                0.0f, 1.0f, edge0->w1, edge0->b1, x0, u, v, {}, x};
+  const unsigned grid = persistent_grid(n, 32 * kWaves, 2);
+  const int tkf = (feat + 31) / 32;
+  const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + (H == 64 ? 3 * H * (H + 4) : 0) + 6 * H);
+  if (tkf > 3 || (tkf == 3 && H != 64) || lds > kLdsMax)
+    return set_error(SGNN_ERR_UNSUPPORTED, "encode_node_features: too many node features");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (tkf == 1) SGNN_DISPATCH_H_NL(H, enc->nlin, (go_encode_nodes<TH_, 1, NL_>(false, grid, lds, s, a)));
+  else if (tkf == 2) SGNN_DISPATCH_H_NL(H, enc->nlin, (go_encode_nodes<TH_, 2, NL_>(false, grid, lds, s, a)));
+  else if (enc->nlin == 2) go_encode_nodes<2, 3, 2>(false, grid, lds, s, a);
+  else go_encode_nodes<2, 3, 3>(false, grid, lds, s, a);
+  return check_launch("encode_node_features");
+}
+
+extern "C" int sgnn_encode_edge_features(const float* e, int32_t fe, const int32_t* perm,
+                                         const int32_t* rowptr, int64_t n, int64_t edge_cap,
+                                         const sgnn_mlp* enc, float* e0t, void* stream) {
+  using namespace sgnn;
+  if (n <= 0 || edge_cap <= 0) return SGNN_OK;
+  if (!e || !perm || !rowptr || !e0t || !enc || fe < 1 || fe > 4)
+    return set_error(SGNN_ERR_INVALID, "encode_edge_features: bad arguments (1 <= fe <= 4)");
+  const int H = enc->hidden;
+  int st = check_mlp(enc, fe, H, H, true, "encode_edge_features: encoder MLP shape");
+  if (st) return st;
+  if (H != 64 && H != 128) return set_error(SGNN_ERR_UNSUPPORTED, "encode_edge_features: hidden must be 64 or 128");
+  EncEdgeArgs a{nullptr, 0, fe - 1, 1.0f, rowptr, nullptr, nullptr, n, enc->w1, enc->b1,
+                last_w(enc), last_b(enc), enc->ln_g, enc->ln_b, e0t, {}, mid_w(enc), mid_b(enc),
+                e, perm, fe};
+  const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 4);
+  const size_t lds = sizeof(float) * (size_t)(H * 5 + (H == 64 ? H * (H + 4) : 0) + 5 * H);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  SGNN_DISPATCH_H_NL(H, enc->nlin, (go_encode_edges<TH_, NL_>(false, grid, lds, s, a)));
+  return check_launch("encode_edge_features");
 }

@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256) void k_coo_fill(const int64_t* dst, int64_t E,
 // one wave per receiver: rank = number of smaller edge ids in its segment
 __global__ __launch_bounds__(256) void k_coo_sort(const int32_t* ptr, int64_t n, const int32_t* raw,
                                                   const int64_t* src, const int64_t* dst,
-                                                  int32_t* send, int32_t* recv) {
+                                                  int32_t* send, int32_t* recv, int32_t* perm) {
   const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (i >= n) return;
   const int lane = threadIdx.x & 63;
@@ -507,6 +507,7 @@ __global__ __launch_bounds__(256) void k_coo_sort(const int32_t* ptr, int64_t n,
     for (int t = 0; t < len; ++t) rank += raw[b + t] < key;
     send[b + rank] = (int32_t)src[key];
     recv[b + rank] = (int32_t)dst[key];
+    if (perm) perm[b + rank] = key;
   }
 }
 
@@ -518,7 +519,7 @@ extern "C" size_t sgnn_coo_workspace_bytes(int64_t n, int64_t E) {
 
 extern "C" int sgnn_coo_to_csr(const int64_t* src, const int64_t* dst, int64_t E, int64_t n,
                                void* workspace, int32_t* rowptr, int32_t* send, int32_t* recv,
-                               void* stream_) {
+                               int32_t* perm, void* stream_) {
   using namespace sgnn;
   hipStream_t s = static_cast<hipStream_t>(stream_);
   if (n <= 0 || E < 0 || !rowptr || !workspace || (E > 0 && (!src || !dst || !send || !recv)))
@@ -542,7 +543,7 @@ extern "C" int sgnn_coo_to_csr(const int64_t* src, const int64_t* dst, int64_t E
   if (E > 0) {
     hipLaunchKernelGGL(k_coo_fill, dim3(g), dim3(256), 0, s, dst, E, rowptr, fill, raw);
     hipLaunchKernelGGL(k_coo_sort, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, rowptr, n, raw,
-                       src, dst, send, recv);
+                       src, dst, send, recv, perm);
   }
   return check_launch("coo_to_csr");
 }

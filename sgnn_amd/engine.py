@@ -166,7 +166,7 @@ class CsrGraph:
         return torch.stack([self.send[:e], self.recv[:e]]).to(torch.int64)
 
 
-def coo_to_csr(edge_index: torch.Tensor, n: int) -> CsrGraph:
+def coo_to_csr(edge_index: torch.Tensor, n: int, with_perm: bool = False) -> CsrGraph:
     """edge_index [2, E] (row 0 senders, row 1 receivers, PyG source_to_target)
     -> stable receiver-sorted CSR through sgnn_coo_to_csr.  Index range is
     checked here (one host sync: static graphs are built once)."""
@@ -187,10 +187,13 @@ def coo_to_csr(edge_index: torch.Tensor, n: int) -> CsrGraph:
     send = torch.zeros(max(E, 1), dtype=torch.int32, device=dev)
     recv = torch.zeros(max(E, 1), dtype=torch.int32, device=dev)
     src, dst = ei[0].contiguous(), ei[1].contiguous()
+    perm = torch.zeros(max(E, 1), dtype=torch.int32, device=dev) if with_perm else None
     check(L.sgnn_coo_to_csr(src.data_ptr() if E else None, dst.data_ptr() if E else None, E, n,
                             (ws.data_ptr() + 255) & ~255, rowptr.data_ptr(), send.data_ptr(),
-                            recv.data_ptr(), stream_ptr(dev)), "sgnn_coo_to_csr")
-    return CsrGraph(rowptr, send, recv, n, E)
+                            recv.data_ptr(), _ptr(perm), stream_ptr(dev)), "sgnn_coo_to_csr")
+    g = CsrGraph(rowptr, send, recv, n, E)
+    g.perm = perm
+    return g
 
 
 def radius_graph_csr(pos: torch.Tensor, radius: float, K: int, loop: bool,
@@ -283,7 +286,83 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
                   "sgnn_node_layer_decode")
 
 
+class ChainBuffers:
+    """Node / edge buffers of one explicit-feature forward (n nodes, edge sets)."""
+
+    def __init__(self, n: int, hidden: int, graphs: Dict[str, "CsrGraph"], device):
+        L = lib()
+        f32 = dict(dtype=torch.float32, device=device)
+        self.x_a, self.x_b = torch.empty(n, hidden, **f32), torch.empty(n, hidden, **f32)
+        self.u, self.v = torch.empty(n, hidden, **f32), torch.empty(n, hidden, **f32)
+        self.agg = torch.empty(n, hidden, **f32)
+        nt = max(g.ntiles for g in graphs.values())
+        self.cin, self.cout = torch.empty(nt, hidden, **f32), torch.empty(nt, hidden, **f32)
+        self.e0t = {k: torch.empty(int(L.sgnn_edge_latent_floats(g.edge_cap, hidden)), **f32)
+                    for k, g in graphs.items()}
+
+
+def _feature_rows(t: torch.Tensor, name: str) -> torch.Tensor:
+    _hip.require_gpu_tensor(t, name)
+    if t.dim() != 2:
+        raise ValueError(f"{name} must be 2-D, got shape {tuple(t.shape)}")
+    return t.to(torch.float32).contiguous()
+
+
+def run_chain(enc_node, enc_edges: Dict[str, SgnnMlp], edges: List[SgnnMlp], nodes: List[SgnnMlp],
+              decoder: SgnnMlp, kinds: List[str], scales: List[float], x: torch.Tensor,
+              graphs: Dict[str, "CsrGraph"], efeats: Dict[str, torch.Tensor], out_dim: int) -> torch.Tensor:
+    """Encoder -> blocks -> decoder on explicit features (no integrator): the
+    operator boundary EncodeProcessDecode.forward / MultiScaleGNN.forward."""
+    L = lib()
+    n, feat = x.shape
+    H = edges[0].hidden
+    dev = x.device
+    s = stream_ptr(dev)
+    b = ChainBuffers(n, H, graphs, dev)
+    check(L.sgnn_encode_node_features(x.data_ptr(), n, feat, ctypes.byref(enc_node), ctypes.byref(edges[0]),
+                                      b.x_a.data_ptr(), b.u.data_ptr(), b.v.data_ptr(), s),
+          "sgnn_encode_node_features")
+    for k, g in graphs.items():
+        if g.num_edges == 0:
+            continue
+        ef = efeats[k]
+        if ef.shape[0] != g.num_edges:
+            raise ValueError(f"edge features of {k}: {ef.shape[0]} rows for {g.num_edges} edges")
+        check(L.sgnn_encode_edge_features(ef.data_ptr(), ef.shape[1], g.perm.data_ptr(), g.rowptr.data_ptr(), n,
+                                          g.edge_cap, ctypes.byref(enc_edges[k]), b.e0t[k].data_ptr(), s),
+              "sgnn_encode_edge_features")
+    pred = torch.empty(n, out_dim, dtype=torch.float32, device=dev)
+    x_in, x_out = b.x_a, b.x_b
+    nb = len(edges)
+    for i in range(nb):
+        g = graphs[kinds[i]]
+        check(L.sgnn_edge_layer(b.u.data_ptr(), b.v.data_ptr(), b.e0t[kinds[i]].data_ptr(), float(scales[i]),
+                                g.rowptr.data_ptr(), g.send.data_ptr(), g.recv.data_ptr(), n, g.edge_cap,
+                                ctypes.byref(edges[i]), b.agg.data_ptr(), b.cin.data_ptr(), b.cout.data_ptr(),
+                                None, s), "sgnn_edge_layer")
+        if i < nb - 1:
+            check(L.sgnn_node_layer(x_in.data_ptr(), b.agg.data_ptr(), b.cin.data_ptr(), b.cout.data_ptr(),
+                                    g.rowptr.data_ptr(), n, ctypes.byref(nodes[i]), ctypes.byref(edges[i + 1]),
+                                    x_out.data_ptr(), b.u.data_ptr(), b.v.data_ptr(), None, s),
+                  "sgnn_node_layer")
+            x_in, x_out = x_out, x_in
+        else:
+            check(L.sgnn_node_layer_decode(x_in.data_ptr(), b.agg.data_ptr(), b.cin.data_ptr(), b.cout.data_ptr(),
+                                           g.rowptr.data_ptr(), n, ctypes.byref(nodes[i]), ctypes.byref(decoder),
+                                           None, 0, out_dim - 1, None, None, 0, pred.data_ptr(), None, None,
+                                           None, s), "sgnn_node_layer_decode")
+    return pred
+
+
 def epd_forward(epd, x, edge_index, edge_features):
-    raise NotImplementedError(
-        "EncodeProcessDecode.forward on explicit (x, edge_index, edge_features) is not wired to the "
-        "HIP path yet; use LearnedSimulator.predict_positions / predict_accelerations")
+    """EncodeProcessDecode.forward(x, edge_index, edge_features)
+    (graph_network.py:388-406) on the HIP kernels: explicit node features
+    [N, F], edge_index [2, E] (senders; receivers), edge features [E, F_e] ->
+    decoder output [N, d+1]."""
+    x = _feature_rows(x, "x")
+    ef = _feature_rows(edge_features, "edge_features")
+    g = coo_to_csr(edge_index, x.shape[0], with_perm=True)
+    pk = ParamPack.get(epd)
+    nl = len(pk.edge)
+    return run_chain(pk.enc_node, {"e": pk.enc_edge}, pk.edge, pk.node, pk.dec, ["e"] * nl,
+                     [2.0 ** k for k in range(nl)], x, {"e": g}, {"e": ef}, pk.dec.out_dim)

@@ -118,3 +118,22 @@ def forward_step(gnn, emb_weight: Optional[torch.Tensor], use_emb: bool, inp: en
                                            d, inp.acc_mean.data_ptr(), inp.acc_std.data_ptr(), 0,
                                            pred.data_ptr(), next_pos.data_ptr(),
                                            engine._ptr(window_out), None, s), "sgnn_node_layer_decode")
+
+
+def gnn_forward(gnn, x, g2m_edge_index, g2m_edge_features, m2m_edge_index, m2m_edge_features,
+                m2g_edge_index, m2g_edge_features) -> torch.Tensor:
+    """MultiScaleGNN.forward (multi_scale_gnn.py:262-326) on explicit features:
+    grid node features [N, F], the three COO edge lists and their features ->
+    prediction head output [N, d+1]."""
+    x = engine._feature_rows(x, "x")
+    n = x.shape[0]
+    eis = {"g2m": g2m_edge_index, "m2m": m2m_edge_index, "m2g": m2g_edge_index}
+    efs = {"g2m": g2m_edge_features, "m2m": m2m_edge_features, "m2g": m2g_edge_features}
+    graphs = {k: engine.coo_to_csr(torch.as_tensor(eis[k]).to(x.device), n, with_perm=True) for k in EDGE_TYPES}
+    efeats = {k: engine._feature_rows(efs[k], f"{k}_edge_features") for k in EDGE_TYPES}
+    pk = ParamPack.get(gnn)
+    nb = len(gnn.chain())
+    kinds = ["g2m"] + ["m2m"] * (nb - 2) + ["m2g"]
+    scales = [1.0] + [float(2.0 ** k) for k in range(nb - 2)] + [1.0]
+    return engine.run_chain(pk.enc, pk.enc_edge, pk.edge, pk.node, pk.head, kinds, scales, x, graphs, efeats,
+                            pk.head.out_dim)

@@ -5,8 +5,8 @@ keys and random initialisation as the reference (a reference checkpoint loads
 unchanged; under one seed both draw identical weights).  The arithmetic of
 `MultiScaleGNN.forward` runs as the fused HIP chain in `ms_engine`
 (encoder -> G2M -> M2M x L -> M2G -> prediction head), driven by
-`MultiScaleSimulator`; calling the block modules on explicit tensors is not
-wired to the kernels (the encoder kernels build the features on the fly).
+`MultiScaleSimulator`; `MultiScaleGNN.forward` on explicit features runs the
+same kernels (the individual block modules are not callable on their own).
 
 Semantics the kernels implement (what PyG executes for these blocks):
   message  m = LN(MLP_e([x_i, x_j, e]))   (multi_scale_gnn.py:96-101)
@@ -86,6 +86,10 @@ class MultiScaleGNN(nn.Module):
         """Blocks in execution order (:301-319)."""
         return [self.g2m_block, *self.m2m_blocks, self.m2g_block]
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("MultiScaleGNN.forward on explicit features is not wired to the HIP "
-                                  "path; use MultiScaleSimulator.predict_positions / predict_accelerations")
+    def forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index, m2m_edge_features,
+                m2g_edge_index, m2g_edge_features, graph_hierarchy=None):
+        """multi_scale_gnn.py:262-326 on explicit features (HIP kernels);
+        graph_hierarchy is unused, as in the reference."""
+        from . import ms_engine
+        return ms_engine.gnn_forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index,
+                                     m2m_edge_features, m2g_edge_index, m2g_edge_features)

@@ -134,3 +134,16 @@ def test_high_degree_user_graph_against_oracle():
     _close(strain.cpu().numpy(), ref_strain.numpy(), what="high-degree strain")
     _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * float(np.max(z["acc_std"])), rtol=1e-6,
            what="high-degree next_pos")
+
+
+@pytest.mark.parametrize("case", MS_CASES)
+def test_multi_scale_gnn_on_explicit_features(case):
+    """MultiScaleGNN.forward(x, g2m_ei, g2m_e, m2m_ei, m2m_e, m2g_ei, m2g_e, h)
+    (multi_scale_gnn.py:262-326) on the reference's own features."""
+    z = golden(case)
+    sim = ms_product_sim(z)
+    t = lambda k: torch.from_numpy(z[k]).cuda()
+    pred = sim._multi_scale_gnn(t("node_features"), t("g2m"), t("ef_g2m"), t("m2m"), t("ef_m2m"), t("m2g"),
+                                t("ef_m2g"), None)
+    torch.cuda.synchronize()
+    _close(pred.cpu().numpy(), z["pred"], what=f"{case} MultiScaleGNN.forward")

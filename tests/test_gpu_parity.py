@@ -131,3 +131,35 @@ def test_3d_h128_against_oracle():
     _close(strain.cpu().numpy(), ref_strain.numpy(), what="3d h128 strain")
     scale = float(np.max(z["acc_std"]))
     _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * scale, rtol=1e-6, what="3d h128 next_pos")
+
+
+@pytest.mark.parametrize("case", FWD_H64 + ["tiny3d_h128"])
+def test_encode_process_decode_on_explicit_features(case):
+    """The operator boundary EncodeProcessDecode.forward(x, edge_index, e)
+    (graph_network.py:388-406) on the reference's own features."""
+    z = golden(case)
+    sim = product_sim(z)
+    t = lambda k: torch.from_numpy(z[k]).cuda()
+    pred = sim._encode_process_decode(t("node_features"), t("edge_index"), t("edge_features"))
+    torch.cuda.synchronize()
+    _close(pred.cpu().numpy(), z["pred"], what=f"{case} EPD.forward")
+
+
+def test_encode_process_decode_edgeless_and_shuffled():
+    """No edges at all (aggregates are zero) and a shuffled COO edge order
+    (the CSR conversion restores receiver order; sums are order-independent
+    up to fp32 rounding) against the oracle."""
+    from oracle import sgnn_oracle as O
+    from tests.helpers import state_of
+    z = golden("tiny2d_r06")
+    sim = product_sim(z)
+    state = state_of(z)
+    nf = torch.from_numpy(z["node_features"])
+    ei = torch.from_numpy(z["edge_index"])
+    ef = torch.from_numpy(z["edge_features"])
+    ref = O.encode_process_decode(state, nf, ei[:, :0], ef[:0], 5)
+    got = sim._encode_process_decode(nf.cuda(), ei[:, :0].cuda(), ef[:0].cuda())
+    _close(got.cpu().numpy(), ref.numpy(), what="edgeless EPD.forward")
+    perm = torch.randperm(ei.shape[1], generator=torch.Generator().manual_seed(0))
+    got = sim._encode_process_decode(nf.cuda(), ei[:, perm].cuda(), ef[perm].cuda())
+    _close(got.cpu().numpy(), z["pred"], what="shuffled EPD.forward")
