@@ -193,7 +193,8 @@ int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin
  *   DECODER : dWl[32][H] (rows > dim zero) | dW1[H][H] | dWm | dbl [W][32] |
  *             db1 [W][H] | loss [W][8] = (total, x, y, z, strain) sums of
  *             squared errors | dbm [W][H]
- *   ENC_NODE: dWl[H][H] | dW1[H][32*ceil(F/32)] | dWm | db1, dbl, dgamma, dbeta [W][H] | dbm
+ *   ENC_NODE: dWl[H][H] | dW1[H][32*ceil(F/32)] | dWm | db1, dbl, dgamma, dbeta [W][H] | dbm |
+ *             G[32][H] (per-particle-type sums of dh; zero without embeddings)
  *   ENC_EDGE: dWl[H][H] | dW1[H][32] | dWm | db1, dbl, dgamma, dbeta [W][H] | dbm
  * Hidden 64 or 128, nlin 2 or 3 (nmlp_layers 1 or 2).  Saved activations come
  * through struct sgnn_saves as the training forward wrote them.
@@ -253,9 +254,18 @@ int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, const float
 /* Wall feature as sgnn_encode_nodes: clamp(x + 2, 0, wall_max) / wall_div.
  * saves: h, yhat, rstd (+ h2). */
 int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
-                          int32_t dim, const float* vel_mean, const float* vel_std,
-                          float wall_max, float wall_div, const sgnn_saves* saves,
-                          const sgnn_mlp* enc, float* slab, int32_t nslab, void* stream);
+                          int32_t dim, const int64_t* types, const float* emb_w, int32_t emb_dim,
+                          int32_t ntypes, int32_t use_emb, const float* vel_mean,
+                          const float* vel_std, float wall_max, float wall_div,
+                          const sgnn_saves* saves, const sgnn_mlp* enc, float* slab,
+                          int32_t nslab, void* stream);
+/* Particle-type embedding gradient (learned_simulator.py:287-290 under
+ * autograd): the ENC_NODE slab's trailing G[32][H] block (per-type sums of the
+ * encoder's first-layer gradient, reduced) times the embedding columns of
+ * W1: dEmb[t][c] (+)= sum_u G[t][u] W1[u][col0 + c]. */
+int sgnn_embedding_grad(const float* G, int32_t ntypes, int32_t hidden, const float* w1,
+                        int32_t w1_ld, int32_t col0, int32_t emb_dim, float* demb,
+                        int32_t accumulate, void* stream);
 /* saves: yhat, rstd (+ h2); the first hidden is recomputed. */
 int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_stride, int32_t dim,
                           float radius, const int32_t* rowptr, const int32_t* send,

@@ -100,8 +100,11 @@ SIGNATURES = {
                                    c_void_p, c_void_p, c_void_p, c_int64, P_MLP, c_void_p,
                                    c_void_p, c_int32, c_void_p, c_void_p]),
     "sgnn_encode_nodes_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                             c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                              c_void_p, c_void_p, c_float, c_float, P_SAVES,
                                              P_MLP, c_void_p, c_int32, c_void_p]),
+    "sgnn_embedding_grad": (ctypes.c_int, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32,
+                                           c_int32, c_void_p, c_int32, c_void_p]),
     "sgnn_encode_edges_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_float,
                                              c_void_p, c_void_p, c_void_p, c_int64, P_SAVES,
                                              P_MLP, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),

@@ -309,7 +309,7 @@ SGNN_HOST_DEV inline int64_t slab_nvec_floats(int kind, int64_t H, int nl) {
     case SGNN_SLAB_NODE: return 4 * W * H + mid;                  // db1 dbl dg db | dbm
     case SGNN_SLAB_UV: return W * H;                              // db1
     case SGNN_SLAB_DECODER: return W * 32 + W * H + W * 8 + mid;  // dbl[32] db1 loss[8] | dbm
-    case SGNN_SLAB_ENC_NODE:
+    case SGNN_SLAB_ENC_NODE: return 4 * W * H + mid + 32 * H;     // db1 dbl dg db | dbm | G[32][H]
     case SGNN_SLAB_ENC_EDGE: return 4 * W * H + mid;              // db1 dbl dg db | dbm
     default: return -1;
   }
@@ -807,6 +807,9 @@ struct EncNodeBwdArgs {
   const float *wl, *wm, *gamma;
   float* slab;
   int64_t slab_stride;
+  const int64_t* types;  // particle types (use_emb) -> embedding features + per-type dh sums
+  const float* emb_w;
+  int emb_dim, use_emb;
 };
 
 template <int TH, int TKF, int NL>
@@ -838,10 +841,12 @@ __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
   const int l = lane_id(), j = im.j, h = l >> 5, w = threadIdx.x >> 6;
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   constexpr int NT1 = (TH * TKF + kWaves - 1) / kWaves;
-  f32x16 acc_wl[NT], acc_wm[NT], acc_w1[NT1];
+  constexpr int NTG = (TH + kWaves - 1) / kWaves;
+  f32x16 acc_wl[NT], acc_wm[NT], acc_w1[NT1], acc_g[NTG];
   zero_acc<NT>(acc_wl);
   zero_acc<NT>(acc_wm);
   zero_acc<NT1>(acc_w1);
+  zero_acc<NTG>(acc_g);
   LANEVEC(s_db1);
   LANEVEC(s_dbl);
   LANEVEC(s_dbm);
@@ -882,6 +887,8 @@ __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
         } else if (valid && f == nvel) {
           val = __fdiv_rn(fminf(fmaxf(__fadd_rn(pp[(a.T - 1) * a.dim], 2.0f), 0.0f), a.wall_max),
                           a.wall_div);
+        } else if (valid && a.use_emb && f < nvel + 1 + a.emb_dim) {  // :287-290
+          val = a.emb_w[a.types[ic] * a.emb_dim + (f - nvel - 1)];
         }
         xf[tk][r] = val;
       }
@@ -892,6 +899,18 @@ __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
     __syncthreads();
     outer_tiles<NT1>(acc_w1, TH, TKF, bufA, ldh, 0, bufB, ldb, 0);
     __syncthreads();
+    if (a.use_emb) {
+      // G[type][u] += dh[u] over this type's nodes (one-hot (x) dh); the
+      // embedding gradient is G . W1[:, emb columns] (sgnn_embedding_grad)
+      const int ty = valid ? (int)a.types[ic] : -1;
+      f32x16 oh[1];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oh[0][r] = crow(r, h) == ty ? 1.0f : 0.0f;
+      lds_store_items<1>(im.sB, ldb, j, oh);
+      __syncthreads();
+      outer_tiles<NTG>(acc_g, 1, TH, bufB, ldb, 0, bufA, ldh, 0);
+      __syncthreads();
+    }
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
   store_outer<NT>(slab, H, TH, TH, acc_wl);
@@ -903,6 +922,7 @@ __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
   store_lane_vec<TH>(v + 2 * kWaves * H, s_dg);
   store_lane_vec<TH>(v + 3 * kWaves * H, s_db);
   if (NL == 3) store_lane_vec<TH>(v + 4 * kWaves * H, s_dbm);
+  store_outer<NTG>(v + (NL == 3 ? 5 : 4) * kWaves * H, H, 1, TH, acc_g);  // G [32][H]
 }
 
 // ===========================================================================
@@ -1727,7 +1747,9 @@ extern "C" int sgnn_decoder_loss_bwd(const float* pred, const float* pos_seq,
 }
 
 extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
-                                     int32_t dim, const float* vel_mean, const float* vel_std,
+                                     int32_t dim, const int64_t* types, const float* emb_w,
+                                     int32_t emb_dim, int32_t ntypes, int32_t use_emb,
+                                     const float* vel_mean, const float* vel_std,
                                      float wall_max, float wall_div, const sgnn_saves* saves,
                                      const sgnn_mlp* enc, float* slab, int32_t nslab,
                                      void* stream) {
@@ -1739,13 +1761,15 @@ extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64
   if (st) return st;
   if (enc->nlin == 3 && !saves->h2) return set_error(SGNN_ERR_INVALID, "encode_nodes_bwd: saves->h2");
   const int H = enc->hidden;
-  const int feat = (T - 1) * dim + 1;
-  if (enc->in_dim != feat)
-    return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd: particle-type embeddings not supported");
+  const int feat = (T - 1) * dim + 1 + (use_emb ? emb_dim : 0);
+  if (enc->in_dim != feat) return set_error(SGNN_ERR_INVALID, "encode_nodes_bwd: encoder input width");
+  if (use_emb && (!types || !emb_w || ntypes < 1 || ntypes > 32))
+    return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd: embeddings need types, weights, ntypes <= 32");
   const int tkf = (feat + 31) / 32;
   EncNodeBwdArgs a{g, pos_seq, n, T, dim, feat, vel_mean, vel_std, wall_max, wall_div, saves->h,
                    saves->h2, saves->yhat, saves->rstd, last_w(enc), mid_w(enc), enc->ln_g, slab,
-                   sgnn_bwd_slab_floats(SGNN_SLAB_ENC_NODE, H, feat, enc->nlin)};
+                   sgnn_bwd_slab_floats(SGNN_SLAB_ENC_NODE, H, feat, enc->nlin), types, emb_w,
+                   use_emb ? emb_dim : 0, use_emb};
   const size_t lds = bwd_lds(SGNN_SLAB_ENC_NODE, H, tkf, enc->nlin);
   if (tkf == 1) {
     SGNN_BWD_DISPATCH(H, enc->nlin, (launch_bwd(k_enc_node_bwd<TH_, 1, NL_>, nslab, lds, stream, a)));
@@ -1838,4 +1862,31 @@ extern "C" int sgnn_transpose_csr(const int32_t* rowptr, const int32_t* send, in
   hipLaunchKernelGGL(k_tcsr_sort, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, tptr, n, raw,
                      tperm);
   return check_launch("transpose_csr");
+}
+
+namespace {
+// dEmb[t][c] (+)= sum_u G[t][u] W1[u][col0 + c]   (G = per-type sums of dh)
+__global__ __launch_bounds__(256) void k_embedding_grad(const float* G, int ntypes, int H,
+                                                        const float* w1, int ld, int col0,
+                                                        int emb_dim, float* demb, int accumulate) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < ntypes * emb_dim;
+       idx += gridDim.x * blockDim.x) {
+    const int t = idx / emb_dim, c = idx - t * emb_dim;
+    float s = 0.0f;
+    for (int u = 0; u < H; ++u) s += G[t * H + u] * w1[(int64_t)u * ld + col0 + c];
+    demb[idx] = accumulate ? demb[idx] + s : s;
+  }
+}
+}  // namespace
+
+extern "C" int sgnn_embedding_grad(const float* G, int32_t ntypes, int32_t hidden, const float* w1,
+                                   int32_t w1_ld, int32_t col0, int32_t emb_dim, float* demb,
+                                   int32_t accumulate, void* stream) {
+  using namespace sgnn;
+  if (!G || !w1 || !demb || ntypes < 1 || ntypes > 32 || hidden < 1 || emb_dim < 1)
+    return set_error(SGNN_ERR_INVALID, "embedding_grad: bad arguments");
+  hipLaunchKernelGGL(k_embedding_grad, dim3((ntypes * emb_dim + 255) / 256), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), G, ntypes, hidden, w1, w1_ld, col0, emb_dim,
+                     demb, accumulate);
+  return check_launch("embedding_grad");
 }

@@ -21,10 +21,10 @@ class _TrainedEPD(torch.autograd.Function):
     per workspace: a second forward before backward invalidates the first."""
 
     @staticmethod
-    def forward(ctx, sim, inp, tw, *params):
-        training.train_forward(sim._encode_process_decode, sim._connectivity_radius, inp, tw)
+    def forward(ctx, sim, inp, tw, emb, *params):
+        training.train_forward(sim._encode_process_decode, sim._connectivity_radius, inp, tw, emb_weight=emb)
         tw.generation = getattr(tw, "generation", 0) + 1
-        ctx.sim, ctx.inp, ctx.tw, ctx.gen = sim, inp, tw, tw.generation
+        ctx.sim, ctx.inp, ctx.tw, ctx.gen, ctx.emb = sim, inp, tw, tw.generation, emb
         return tw.pred.clone()
 
     @staticmethod
@@ -38,9 +38,16 @@ class _TrainedEPD(torch.autograd.Function):
         if scratch is None:
             scratch = {k: torch.zeros_like(p) for k, p in epd.named_parameters(prefix="_encode_process_decode")}
             tw.grad_scratch = scratch
+        demb = None
+        if ctx.emb is not None:
+            demb = getattr(tw, "emb_grad_scratch", None)
+            if demb is None or demb.shape != ctx.emb.shape:
+                demb = torch.zeros_like(ctx.emb)
+                tw.emb_grad_scratch = demb
         training.train_backward(epd, sim._connectivity_radius, ctx.inp, tw, scratch,
-                                dpred=dpred.to(torch.float32).contiguous())
-        return (None, None, None, *[g.clone() for g in scratch.values()])
+                                dpred=dpred.to(torch.float32).contiguous(), emb_weight=ctx.emb, emb_grad=demb)
+        return (None, None, None, demb.clone() if demb is not None else None,
+                *[g.clone() for g in scratch.values()])
 
 
 class LearnedSimulator(nn.Module):
@@ -193,13 +200,15 @@ class LearnedSimulator(nn.Module):
         noisy = position_sequence + position_sequence_noise
         epd = self._encode_process_decode
         params = list(epd.parameters())
-        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        need_grad = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or (
+            self._nparticle_types > 1 and self._particle_type_embedding.weight.requires_grad))
         inp, use_emb = self._step_inputs(noisy, nparticles_per_example, particle_types)
         n, T, d = inp.pos_seq.shape
         if need_grad:
             training.check_trainable(epd, self._nparticle_types)
             tw = self._train_workspace(n, T, inp.pos_seq.device)
-            pred = _TrainedEPD.apply(self, inp, tw, *params)
+            emb = self._particle_type_embedding.weight if use_emb else None
+            pred = _TrainedEPD.apply(self, inp, tw, emb, *params)
         else:
             ws = self._workspace(n, T, inp.pos_seq.device)
             pred = torch.empty(n, d + 1, dtype=torch.float32, device=inp.pos_seq.device)

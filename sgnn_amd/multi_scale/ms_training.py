@@ -24,7 +24,8 @@ import torch
 from .. import _hip, engine
 from .._hip import check, lib, stream_ptr
 from ..train import DataParallel, random_walk_noise
-from ..training import (DEFAULT_NSLAB, Adam, FlatParams, SlabArena, _saves, _Timer, nslab_table)
+from ..training import (DEFAULT_NSLAB, Adam, FlatParams, SlabArena, _saves, _Timer, emb_args,
+                        embedding_backward, nslab_table)
 from . import ms_engine
 from .ms_engine import EDGE_TYPES
 
@@ -37,8 +38,8 @@ def check_trainable(sim) -> None:
         raise NotImplementedError("HIP multi-scale training: latent_dim must be 64 or 128")
     if gnn.nmlp_layers not in (1, 2):
         raise NotImplementedError("HIP multi-scale training: nmlp_layers must be 1 or 2")
-    if sim._nparticle_types > 1:
-        raise NotImplementedError("HIP multi-scale training: particle-type embeddings (nparticle_types > 1)")
+    if sim._nparticle_types > 32:
+        raise NotImplementedError("HIP multi-scale training: at most 32 particle types")
 
 
 class MSTrainWorkspace:
@@ -102,6 +103,7 @@ class MSTrainWorkspace:
         self.feat = gnn.nnode_in
         self.slabs = SlabArena(H, self.nlin, self.feat, keys, self.nslab_of, device)
         self.loss_out = torch.zeros(8, **f32)
+        self.emb_g = torch.zeros(32, H, **f32)
         sc = lambda kind, items: int(L.sgnn_bwd_scratch_floats(kind, H, items, self.nlin))
         self.scratch = e(max(1, sc(_hip.SLAB_EDGE, max(cap.values())), sc(_hip.SLAB_ENC_EDGE, max(cap.values())),
                              sc(_hip.SLAB_NODE, n), sc(_hip.SLAB_UV, n)))
@@ -110,14 +112,14 @@ class MSTrainWorkspace:
     def slab(self, kind: int, k: int = 0) -> int:
         return self.slabs.ptr(kind, k)
 
-    def descriptors(self, grads: Dict[str, torch.Tensor]) -> None:
-        key = tuple(g.data_ptr() for g in grads.values())
+    def descriptors(self, grads: Dict[str, torch.Tensor], use_emb: bool = False) -> None:
+        key = tuple(g.data_ptr() for g in grads.values()) + (use_emb,)
         if key == self._descs_key:
             return
         pre = "_multi_scale_gnn."
         g = lambda name: grads[pre + name]
         lay = self.slabs.layout(self.H, self.nlin, self.feat, self.dim)
-        lay.enc_node(g, "grid_node_encoder.")
+        lay.enc_node(g, "grid_node_encoder.", self.emb_g if use_emb else None)
         for k in EDGE_TYPES:
             lay.enc_edge(g, f"{k}_edge_encoder.", KIND_SLOT[k])
         prefixes = ["g2m_block."] + [f"m2m_blocks.{k}." for k in range(self.nb - 2)] + ["m2g_block."]
@@ -129,7 +131,8 @@ class MSTrainWorkspace:
 
 
 def train_forward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grid_radius: float,
-                  mesh_radius: float, timers: Optional[dict] = None) -> None:
+                  mesh_radius: float, timers: Optional[dict] = None,
+                  emb_weight: Optional[torch.Tensor] = None) -> None:
     """ms_engine.forward_step with every activation the backward needs saved."""
     L = lib()
     pk = ms_engine.ParamPack.get(gnn)
@@ -138,7 +141,7 @@ def train_forward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grid_radius
     s = stream_ptr(inp.pos_seq.device)
     pos = inp.pos_seq
     sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2)
-    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, 0, 0, 0, 0, inp.vel_mean.data_ptr(),
+    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, *emb_args(inp, emb_weight), inp.vel_mean.data_ptr(),
                               inp.vel_std.data_ptr(), float(grid_radius), float(grid_radius),
                               ctypes.byref(pk.enc), ctypes.byref(pk.edge[0]), tw.xs[0].data_ptr(),
                               ws.u.data_ptr(), ws.v.data_ptr(), ctypes.byref(sv), s), "sgnn_encode_nodes")
@@ -182,10 +185,12 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                    grid_radius: float, mesh_radius: float, dpred: Optional[torch.Tensor] = None,
                    next_pos: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
                    next_strain: Optional[torch.Tensor] = None, w_pos: float = 1.0, w_strain: float = 1.0,
-                   inv_count: float = 1.0, timers: Optional[dict] = None) -> None:
+                   inv_count: float = 1.0, timers: Optional[dict] = None,
+                   emb_weight: Optional[torch.Tensor] = None, emb_grad: Optional[torch.Tensor] = None) -> None:
     L = lib()
     pk = ms_engine.ParamPack.get(gnn)
-    tw.descriptors(grads)
+    use_emb = emb_weight is not None and inp.types is not None
+    tw.descriptors(grads, use_emb)
     ws, graphs = tw.f, tw.graphs
     n, T, d = tw.n, tw.T, tw.dim
     s = stream_ptr(inp.pos_seq.device)
@@ -222,7 +227,9 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                             tw.tperm[kind].data_ptr(), tw.xs[b].data_ptr(), n, ctypes.byref(pk.edge[b]),
                             tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, b), ns[_hip.SLAB_UV],
                             tw.scratch.data_ptr(), s), "sgnn_uv_bwd")
-    check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, inp.vel_mean.data_ptr(),
+    ty, ew, ed, ue = emb_args(inp, emb_weight)
+    check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, ty, ew, ed,
+                                  int(emb_weight.shape[0]) if ue else 0, ue, inp.vel_mean.data_ptr(),
                                   inp.vel_std.data_ptr(), float(grid_radius), float(grid_radius),
                                   ctypes.byref(_saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd,
                                                       h2=tw.enc_h2)),
@@ -242,6 +249,8 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                   "sgnn_encode_edges_bwd")
     check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
                               tw._nblocks, s), "sgnn_reduce_slabs")
+    if use_emb:
+        embedding_backward(tw, gnn.grid_node_encoder[0][0].weight, emb_weight, emb_grad, (T - 1) * d, s)
 
 
 class MultiScaleTrainer:
@@ -295,10 +304,12 @@ class MultiScaleTrainer:
                 n_global = self.dp.global_count(n, pos.device)
                 self._count_cache[n] = n_global
         rg, rm = self.sim._grid_radius(), self.sim._mesh_radius()
-        train_forward(self.gnn, inp, tw, rg, rm, timers=timers)
+        emb = self.sim._particle_type_embedding.weight if self.sim._nparticle_types > 1 else None
+        train_forward(self.gnn, inp, tw, rg, rm, timers=timers, emb_weight=emb)
         train_backward(self.gnn, inp, tw, self.grads, rg, rm, next_pos=next_position.to(torch.float32).contiguous(),
                        noise=noise, next_strain=next_strain.to(torch.float32).contiguous(), w_pos=self.w_pos,
-                       w_strain=self.w_strain, inv_count=1.0 / n_global, timers=timers)
+                       w_strain=self.w_strain, inv_count=1.0 / n_global, timers=timers, emb_weight=emb,
+                       emb_grad=self.grads.get("_particle_type_embedding.weight"))
         self.dp.allreduce_(self.flat.grad, tw.loss_out)
         self.opt.step()
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6

@@ -29,11 +29,12 @@ class _TrainedGNN(torch.autograd.Function):
     per workspace: a second forward before backward invalidates the first."""
 
     @staticmethod
-    def forward(ctx, sim, inp, tw, *params):
+    def forward(ctx, sim, inp, tw, emb, *params):
         from . import ms_training
-        ms_training.train_forward(sim._multi_scale_gnn, inp, tw, sim._grid_radius(), sim._mesh_radius())
+        ms_training.train_forward(sim._multi_scale_gnn, inp, tw, sim._grid_radius(), sim._mesh_radius(),
+                                  emb_weight=emb)
         tw.generation = getattr(tw, "generation", 0) + 1
-        ctx.sim, ctx.inp, ctx.tw, ctx.gen = sim, inp, tw, tw.generation
+        ctx.sim, ctx.inp, ctx.tw, ctx.gen, ctx.emb = sim, inp, tw, tw.generation, emb
         return tw.pred.clone()
 
     @staticmethod
@@ -48,9 +49,11 @@ class _TrainedGNN(torch.autograd.Function):
         if scratch is None:
             scratch = {k: torch.zeros_like(p) for k, p in gnn.named_parameters(prefix="_multi_scale_gnn")}
             tw.grad_scratch = scratch
+        demb = torch.zeros_like(ctx.emb) if ctx.emb is not None else None
         ms_training.train_backward(gnn, ctx.inp, tw, scratch, sim._grid_radius(), sim._mesh_radius(),
-                                   dpred=dpred.to(torch.float32).contiguous())
-        return (None, None, None, *[g.clone() for g in scratch.values()])
+                                   dpred=dpred.to(torch.float32).contiguous(), emb_weight=ctx.emb,
+                                   emb_grad=demb)
+        return (None, None, None, demb, *[g.clone() for g in scratch.values()])
 
 
 class MultiScaleSimulator(nn.Module):
@@ -254,7 +257,8 @@ class MultiScaleSimulator(nn.Module):
             inp, _ = self._step_inputs(noisy, particle_types)
             n, T, _ = inp.pos_seq.shape
             tw = self._train_workspace(n, T, inp.pos_seq.device)
-            pred = _TrainedGNN.apply(self, inp, tw, *params)
+            emb = self._particle_type_embedding.weight if self._nparticle_types > 1 else None
+            pred = _TrainedGNN.apply(self, inp, tw, emb, *params)
         else:
             inp, pred, _ = self._run(noisy, particle_types)
         target = self._inverse_decoder_postprocessor(next_positions + position_sequence_noise[:, -1],

@@ -112,11 +112,13 @@ class Trainer:
                 n_global = self.dp.global_count(n, pos.device)
                 self._count_cache[n] = n_global
         radius = self.sim._connectivity_radius
-        training.train_forward(self.epd, radius, inp, tw, timers=timers)
+        emb = self.sim._particle_type_embedding.weight if self.sim._nparticle_types > 1 else None
+        training.train_forward(self.epd, radius, inp, tw, timers=timers, emb_weight=emb)
         training.train_backward(self.epd, radius, inp, tw, self.grads, timers=timers,
                                 next_pos=next_position.to(torch.float32).contiguous(), noise=noise,
                                 next_strain=next_strain.to(torch.float32).contiguous(),
-                                w_pos=self.w_pos, w_strain=self.w_strain, inv_count=1.0 / n_global)
+                                w_pos=self.w_pos, w_strain=self.w_strain, inv_count=1.0 / n_global,
+                                emb_weight=emb, emb_grad=self.grads.get("_particle_type_embedding.weight"))
         self.dp.allreduce_(self.flat.grad, tw.loss_out)
         self.opt.step()
         # train.py:276-278: LR for the NEXT step, computed from the pre-increment step

@@ -102,7 +102,8 @@ class GradLayout:
                 _hip.SLAB_ENC_EDGE: H * H + H * 32 + mid}[kind]
 
     # -- one reference MLP per call -------------------------------------------------
-    def enc_node(self, g, prefix):
+    def enc_node(self, g, prefix, emb_g: Optional[torch.Tensor] = None):
+        """emb_g: [32][H] destination of the per-type dh sums (embeddings)."""
         H, nl, W = self.H, self.nl, W_PARTIALS
         K = _hip.SLAB_ENC_NODE
         fpad = 32 * ((self.feat + 31) // 32)
@@ -113,6 +114,8 @@ class GradLayout:
         if mid:
             self.add(K, 0, H * H + H * fpad, g(mid + "weight"), H, H, H)
         self._vecs5(K, 0, vb, g, first, last, ln, mid)
+        if emb_g is not None:
+            self.add(K, 0, vb + (5 if mid else 4) * W * H, emb_g, 32, H, H)
 
     def enc_edge(self, g, prefix, k=0):
         H, nl = self.H, self.nl
@@ -265,6 +268,7 @@ class TrainWorkspace:
         self.slabs = SlabArena(H, self.nlin, self.feat, keys, self.nslab_of, device)
         self.arena = self.slabs.arena
         self.loss_out = torch.zeros(8, **f32)
+        self.emb_g = torch.zeros(32, H, **f32)   # per-type dh sums (particle-type embeddings)
         sc = lambda kind, items: int(L.sgnn_bwd_scratch_floats(kind, H, items, self.nlin))
         self.scratch = e(max(1, sc(_hip.SLAB_EDGE, cap), sc(_hip.SLAB_ENC_EDGE, cap),
                              sc(_hip.SLAB_NODE, n), sc(_hip.SLAB_UV, n)))
@@ -276,15 +280,15 @@ class TrainWorkspace:
     def tws_ptr(self) -> int:
         return (self.tws.data_ptr() + 255) & ~255
 
-    def descriptors(self, epd: nn.Module, grads: Dict[str, torch.Tensor]) -> None:
+    def descriptors(self, epd: nn.Module, grads: Dict[str, torch.Tensor], use_emb: bool = False) -> None:
         """Build the slab -> parameter-gradient reduction table (device copy)."""
-        key = tuple(g.data_ptr() for g in grads.values())
+        key = tuple(g.data_ptr() for g in grads.values()) + (use_emb,)
         if key == self._descs_key:
             return
         pre = "_encode_process_decode."
         g = lambda name: grads[pre + name]
         lay = self.slabs.layout(self.H, self.nlin, self.feat, self.dim)
-        lay.enc_node(g, "_encoder.node_fn.")
+        lay.enc_node(g, "_encoder.node_fn.", self.emb_g if use_emb else None)
         lay.enc_edge(g, "_encoder.edge_fn.")
         for k in range(self.L):
             lay.interaction(g, f"_processor.gnn_stacks.{k}.", k, 2.0 ** k)
@@ -303,8 +307,8 @@ def check_trainable(epd: nn.Module, nparticle_types: int) -> None:
         raise NotImplementedError("HIP training path: latent_dim must be 64 or 128")
     if epd.nmlp_layers not in (1, 2):
         raise NotImplementedError("HIP training path: nmlp_layers must be 1 or 2")
-    if nparticle_types > 1:
-        raise NotImplementedError("HIP training path: particle-type embeddings (nparticle_types > 1)")
+    if nparticle_types > 32:
+        raise NotImplementedError("HIP training path: at most 32 particle types")
 
 
 class _Timer:
@@ -325,8 +329,23 @@ class _Timer:
             self.timers.setdefault(self.name, []).append((self.ev0, ev1))
 
 
+def emb_args(inp: engine.StepInputs, emb_weight: Optional[torch.Tensor]):
+    """(types, emb_w, emb_dim, use_emb) for the encoder kernels."""
+    if emb_weight is None or inp.types is None:
+        return 0, 0, 0, 0
+    return inp.types.data_ptr(), emb_weight.data_ptr(), int(emb_weight.shape[1]), 1
+
+
+def embedding_backward(tw, enc_w1: torch.Tensor, emb_weight: torch.Tensor, demb: torch.Tensor,
+                       nvel: int, stream: int) -> None:
+    """dEmb = G . W1[:, emb columns] after the slab reduction filled tw.emb_g."""
+    check(lib().sgnn_embedding_grad(tw.emb_g.data_ptr(), int(emb_weight.shape[0]), tw.H, enc_w1.data_ptr(),
+                                    int(enc_w1.shape[1]), nvel + 1, int(emb_weight.shape[1]),
+                                    demb.data_ptr(), 0, stream), "sgnn_embedding_grad")
+
+
 def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: TrainWorkspace,
-                  timers: Optional[dict] = None) -> None:
+                  timers: Optional[dict] = None, emb_weight: Optional[torch.Tensor] = None) -> None:
     """predict_accelerations' forward with every activation the backward needs saved."""
     L = lib()
     pk = engine.ParamPack.get(epd)
@@ -336,7 +355,7 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
     pos = inp.pos_seq
     engine.radius_graph(ws, pos, (T - 1) * d, T * d, inp.ex_ptr, inp.n_ex, radius)
     sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2)
-    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, 0, 0, 0, 0, inp.vel_mean.data_ptr(),
+    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, *emb_args(inp, emb_weight), inp.vel_mean.data_ptr(),
                               inp.vel_std.data_ptr(), float(radius), 1.0, ctypes.byref(pk.enc_node),
                               ctypes.byref(pk.edge[0]), tw.xs[0].data_ptr(), ws.u.data_ptr(),
                               ws.v.data_ptr(), ctypes.byref(sv), s), "sgnn_encode_nodes")
@@ -380,13 +399,17 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                    grads: Dict[str, torch.Tensor], dpred: Optional[torch.Tensor] = None,
                    next_pos: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
                    next_strain: Optional[torch.Tensor] = None, w_pos: float = 1.0,
-                   w_strain: float = 1.0, inv_count: float = 1.0, timers: Optional[dict] = None) -> None:
-    """Gradients of every parameter into `grads` (name -> tensor views).
+                   w_strain: float = 1.0, inv_count: float = 1.0, timers: Optional[dict] = None,
+                   emb_weight: Optional[torch.Tensor] = None,
+                   emb_grad: Optional[torch.Tensor] = None) -> None:
+    """Gradients of every parameter into `grads` (name -> tensor views);
+    with emb_weight, the particle-type embedding gradient into emb_grad.
     With dpred: dL/dpred is given (autograd path); otherwise the loss of
     train.py:257-268 is differentiated in-kernel (its sums land in tw.loss_out)."""
     L = lib()
     pk = engine.ParamPack.get(epd)
-    tw.descriptors(epd, grads)
+    use_emb = emb_weight is not None and inp.types is not None
+    tw.descriptors(epd, grads, use_emb)
     ws = tw.f
     n, T, d = ws.n, ws.T, ws.dim
     s = stream_ptr(inp.pos_seq.device)
@@ -421,7 +444,9 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                             tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV],
                             tw.scratch.data_ptr(), s),
               "sgnn_uv_bwd")
-    check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d,
+    ty, ew, ed, ue = emb_args(inp, emb_weight)
+    check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, ty, ew, ed,
+                                  int(emb_weight.shape[0]) if ue else 0, ue,
                                   inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius), 1.0,
                                   ctypes.byref(_saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd,
                                                       h2=tw.enc_h2)),
@@ -437,6 +462,8 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
           "sgnn_encode_edges_bwd")
     check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
                               tw._nblocks, s), "sgnn_reduce_slabs")
+    if use_emb:
+        embedding_backward(tw, epd._encoder.node_fn[0][0].weight, emb_weight, emb_grad, (T - 1) * d, s)
 
 
 class Adam:

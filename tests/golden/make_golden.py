@@ -203,12 +203,12 @@ def forward_case(name, pos_seq, npe, types_, dim, T, H, L, R, ntypes=1, emb=9, s
     print(f"{name}: N={pos_seq.shape[0]} E={out['edge_index'].shape[1]} -> {os.path.getsize(path)/1e3:.0f} KB")
 
 
-def train_case(name, seed=0):
+def train_case(name, seed=0, ntypes=1, L=5):
     """One training step exactly as train.py:231-278 (noise passed in, lr_init=1e-3)."""
-    dim, T, H, L, R = 2, 11, 64, 5, 0.6
+    dim, T, H, R = 2, 11, 64, 0.6
     noise_std = 0.02
     st = synthetic.normalization_stats(dim, noise_std=noise_std)
-    sim, _ = make_sim(dim, T, H, L, R, seed=seed, stats=st)
+    sim, _ = make_sim(dim, T, H, L, R, ntypes=ntypes, seed=seed, stats=st)
     sim.train()
     a = synthetic.trajectory(synthetic.lattice_2d(10, 8), T + 1, seed=11)
     b = synthetic.trajectory(synthetic.lattice_2d(9, 8, x0=0.5, y0=-9.5), T + 1, seed=12)
@@ -217,7 +217,7 @@ def train_case(name, seed=0):
     pos = torch.tensor(seq[:, :T])
     next_pos = torch.tensor(seq[:, T])
     next_strain = torch.tensor(np.random.default_rng(5).normal(0, 1, seq.shape[0]).astype(np.float32))
-    types_ = torch.zeros(seq.shape[0], dtype=torch.long)
+    types_ = torch.from_numpy(np.random.default_rng(seed + 7).integers(0, ntypes, seq.shape[0]))
     torch.manual_seed(123)
     noise = ref_noise.get_random_walk_noise_for_position_sequence(pos, noise_std_last_step=noise_std)
     init = sd_arrays(sim, "w0/")
@@ -232,7 +232,7 @@ def train_case(name, seed=0):
     loss.backward()
     grads = {"g/" + k: p.grad.detach().numpy().copy() for k, p in sim.named_parameters() if p.grad is not None}
     opt.step()
-    out = {**hparams(dim, T, H, L, R, 1, 9), **stats_arrays(st), **init, **grads, **sd_arrays(sim, "w1/"),
+    out = {**hparams(dim, T, H, L, R, ntypes, 9), **stats_arrays(st), **init, **grads, **sd_arrays(sim, "w1/"),
            "positions": seq[:, :T], "next_position": seq[:, T], "next_strain": next_strain.numpy(),
            "noise": noise.numpy(), "nparticles_per_example": npe, "particle_types": types_.numpy(),
            "pred_acc": pred_acc.detach().numpy(), "target_acc": target_acc.detach().numpy(),
@@ -309,6 +309,8 @@ def multi_scale_case(name, base, nframes, T, H, L, num_scales, window, mult, nty
 def main(only=None):
     if only == "ms":
         return main_ms()
+    if only == "train_types":
+        return train_case("train2d_types", seed=2, ntypes=3, L=2)
     if only == "ms_train":
         return multi_scale_train_case("ms_train2d", synthetic.lattice_2d(16, 12, x0=-1.75), 6, 64, 2, 3, 2,
                                       2.0, seed=6)
@@ -336,7 +338,9 @@ def main(only=None):
     forward_case("tiny3d_h128", seq, [seq.shape[0]], np.zeros(seq.shape[0]), 3, 6, 128, 3, 0.75)
     # 7) one training step (loss, grads, Adam update)
     train_case("train2d_r06")
-    # 8-9) multi-scale cases
+    # 8) training step with three particle types (embedding gradient)
+    train_case("train2d_types", seed=2, ntypes=3, L=2)
+    # 9-10) multi-scale cases
     main_ms()
 
 

@@ -155,3 +155,39 @@ def test_wide_and_deep_mlp_gradients_against_oracle(dim, H, nmlp):
         if state[k].grad is not None:
             worst = max(worst, _grad_close(p.grad.cpu().numpy(), state[k].grad.numpy(), k, rel=5e-4))
     print(f"dim={dim} H={H} nmlp={nmlp}: worst relative grad error {worst:.3e}")
+
+
+def test_trainer_with_particle_types_matches_reference():
+    """Three particle types: the embedding enters the encoder features and its
+    gradient (per-type sums of the encoder's first-layer gradient through the
+    embedding columns of W1) is trained like every other parameter."""
+    from sgnn_amd.train import Trainer
+    z = golden("train2d_types")
+    sim = product_sim(z, prefix="w0/")
+    tr = Trainer(sim, lr_init=float(z["lr"]))
+    pos, nxt, strain, noise, npe = _golden_inputs(z)
+    types_ = torch.from_numpy(z["particle_types"]).cuda()
+    out = tr.train_step(pos, nxt, strain, npe, particle_types=types_, noise=noise)
+    torch.cuda.synchronize()
+    assert abs(float(out["loss"]) - float(z["loss"])) <= 1e-5 * abs(float(z["loss"]))
+    grads = {k: p.grad for k, p in sim.named_parameters()}
+    for k in z.files:
+        if k.startswith("g/"):
+            _grad_close(grads[k[2:]].cpu().numpy(), z[k], k)
+    sd = sim.state_dict()
+    for k in z.files:
+        if k.startswith("w1/") and ("g/" + k[3:]) in z.files:
+            np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), z[k], rtol=1e-5, atol=2e-5, err_msg=k)
+
+
+def test_autograd_with_particle_types_matches_reference():
+    z = golden("train2d_types")
+    sim = product_sim(z, prefix="w0/")
+    pos, nxt, strain, noise, npe = _golden_inputs(z)
+    types_ = torch.from_numpy(z["particle_types"]).cuda()
+    pa, ta, ps = sim.predict_accelerations(nxt, noise, pos, npe, types_)
+    loss = ((((pa - ta) ** 2).sum(-1)) + (ps - strain) ** 2).mean()
+    loss.backward()
+    for k, p in sim.named_parameters():
+        if ("g/" + k) in z.files:
+            _grad_close(p.grad.cpu().numpy(), z["g/" + k], k)
