@@ -11,8 +11,9 @@ hidden=64, fp32, forward+backward"): one step = the reference training step
 backward, [N>1: RCCL all-reduce of the flat gradient], Adam, LR decay.  Each
 rank owns one whole graph (weak scaling, whole-graph DDP over xGMI).
 --mode rollout: one step = one autoregressive predict_positions (radius
-graph + features + encoder + L layers + decoder + Euler + window shift);
-multi-GPU rollout is replicas only (no collective).
+graph + features + encoder + L layers + decoder + Euler + window shift),
+the steps replayed from a captured HIP graph; multi-GPU rollout is replicas
+only (no collective).
 Inputs are resident in HBM before the timed region.  Synthetic lattice data
 and random-init weights (no dataset/checkpoint offline).
 
@@ -182,12 +183,19 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload=None):
 
 
 def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps):
+    """Timed region: `steps` autoregressive steps replayed from a captured HIP
+    graph (evaluate.rollout's device path: the same kernels per step, no
+    per-kernel launch cost); warm-up = capture + one untimed full rollout."""
     sim, window0, ws, run, n, radius, H, L = rollout_setup(workload, device, seed, rank)
     with torch.no_grad():
-        run(0, warmup)
+        types_ = torch.zeros(n, dtype=torch.long, device=device)
+        w0 = window0.to(device)
+        runner = sim.rollout_runner(w0, [n], types_, steps)
+        for _ in range(max(1, warmup // max(steps, 1))):
+            runner.run(w0)
         sync_barrier(world)
         t0 = time.perf_counter()
-        run(warmup, steps)
+        runner.run(w0)
         sync_barrier(world)
         dt = time.perf_counter() - t0
         timers = []

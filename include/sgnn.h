@@ -170,6 +170,51 @@ int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin
                            const sgnn_saves* saves, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Whole-step drivers.  One call = one LearnedSimulator.predict_positions
+ * (learned_simulator.py:413-438: radius graph, encoders, L interaction
+ * layers, decoder, Euler) or a whole autoregressive rollout (evaluate.py:
+ * 117-145: the window shift is fused into the decoder kernel), issued from C
+ * so the host cost per kernel is one hipLaunchKernel. */
+typedef struct sgnn_epd {
+  int32_t nlayers;
+  const sgnn_mlp* enc_node;
+  const sgnn_mlp* enc_edge;
+  const sgnn_mlp* edge; /* [nlayers] InteractionNetwork edge_fn */
+  const sgnn_mlp* node; /* [nlayers] InteractionNetwork node_fn */
+  const sgnn_mlp* dec;
+} sgnn_epd;
+
+typedef struct sgnn_step_in {
+  int64_t n;
+  int32_t T, dim;
+  const int64_t* ex_ptr; /* [n_ex+1] example offsets (nparticles_per_example) */
+  int32_t n_ex;
+  float radius;
+  int32_t K; /* max_num_neighbors (20) */
+  const int64_t* types;
+  const float* emb_w;
+  int32_t emb_dim, use_emb;
+  const float *vel_mean, *vel_std, *acc_mean, *acc_std;
+  float wall_max, wall_div; /* clamp(x + 2, 0, wall_max) / wall_div */
+} sgnn_step_in;
+
+typedef struct sgnn_step_ws { /* device buffers of one (n, T, dim, H, K) shape */
+  void* radius_ws;
+  int32_t *rowptr, *send, *recv;
+  int64_t edge_cap;
+  float *e0t, *x_a, *x_b, *u, *v, *agg, *cin, *cout;
+} sgnn_step_ws;
+
+int sgnn_predict_positions(const sgnn_epd* model, const sgnn_step_in* in, const float* pos_seq,
+                           const sgnn_step_ws* ws, float* pred, float* next_pos, float* window_out,
+                           void* stream);
+/* Steps alternate win_a -> win_b -> win_a ...; step k writes out_pred[k][n][dim+1]
+ * (normalised acceleration + strain) and out_pos[k][n][dim]. */
+int sgnn_rollout(const sgnn_epd* model, const sgnn_step_in* in, float* win_a, float* win_b,
+                 const sgnn_step_ws* ws, int32_t nsteps, float* out_pos, float* out_pred,
+                 void* stream);
+
+/* ---------------------------------------------------------------------------
  * Training backward: reverse of predict_accelerations (learned_simulator.py:
  * 440-491) + the loss of train.py:257-268, i.e. what loss.backward() does
  * through PyG/torch autograd.  Call order per step (L layers):

@@ -36,6 +36,27 @@ class SgnnSaves(ctypes.Structure):
                 ("hd", c_void_p), ("h2", c_void_p), ("hd2", c_void_p)]
 
 
+class SgnnEpd(ctypes.Structure):
+    """struct sgnn_epd (include/sgnn.h)."""
+    _fields_ = [("nlayers", c_int32), ("enc_node", c_void_p), ("enc_edge", c_void_p), ("edge", c_void_p),
+                ("node", c_void_p), ("dec", c_void_p)]
+
+
+class SgnnStepIn(ctypes.Structure):
+    """struct sgnn_step_in (include/sgnn.h)."""
+    _fields_ = [("n", c_int64), ("T", c_int32), ("dim", c_int32), ("ex_ptr", c_void_p), ("n_ex", c_int32),
+                ("radius", c_float), ("K", c_int32), ("types", c_void_p), ("emb_w", c_void_p),
+                ("emb_dim", c_int32), ("use_emb", c_int32), ("vel_mean", c_void_p), ("vel_std", c_void_p),
+                ("acc_mean", c_void_p), ("acc_std", c_void_p), ("wall_max", c_float), ("wall_div", c_float)]
+
+
+class SgnnStepWs(ctypes.Structure):
+    """struct sgnn_step_ws (include/sgnn.h)."""
+    _fields_ = [("radius_ws", c_void_p), ("rowptr", c_void_p), ("send", c_void_p), ("recv", c_void_p),
+                ("edge_cap", c_int64), ("e0t", c_void_p), ("x_a", c_void_p), ("x_b", c_void_p),
+                ("u", c_void_p), ("v", c_void_p), ("agg", c_void_p), ("cin", c_void_p), ("cout", c_void_p)]
+
+
 class SgnnReduceDesc(ctypes.Structure):
     """struct sgnn_reduce_desc (include/sgnn.h)."""
     _fields_ = [("src", c_void_p), ("dst", c_void_p), ("slab_stride", c_int64), ("offset", c_int64),
@@ -108,6 +129,10 @@ SIGNATURES = {
     "sgnn_encode_edges_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_float,
                                              c_void_p, c_void_p, c_void_p, c_int64, P_SAVES,
                                              P_MLP, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
+    "sgnn_predict_positions": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p]),
+    "sgnn_rollout": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                    c_void_p, c_void_p]),
     "sgnn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,
                                       c_float, c_float, c_float, c_int64, c_void_p]),
 }

@@ -1,0 +1,67 @@
+// Host-side step / rollout drivers: one C-ABI call issues a whole
+// LearnedSimulator.predict_positions (learned_simulator.py:413-438) or a whole
+// autoregressive rollout (evaluate.py:117-145), so the per-kernel cost on the
+// host is a hipLaunchKernel (~µs) instead of a Python ctypes round trip.
+#include "../../include/sgnn.h"
+#include "sgnn_internal.h"
+
+extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq,
+                                      const sgnn_step_ws* ws, float* pred, float* next_pos,
+                                      float* window_out, void* stream) {
+  using namespace sgnn;
+  if (!m || !in || !pos_seq || !ws || !pred || !next_pos || m->nlayers < 1 || !m->edge || !m->node)
+    return set_error(SGNN_ERR_INVALID, "predict_positions: bad arguments");
+  const int64_t n = in->n;
+  const int T = in->T, d = in->dim;
+  // radius graph on the most recent frame (learned_simulator.py:116-117)
+  int st = sgnn_radius_graph(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, n, d, in->ex_ptr, in->n_ex,
+                             in->radius, in->K, 1, ws->radius_ws, ws->rowptr, ws->send, ws->recv,
+                             ws->edge_cap, stream);
+  if (st) return st;
+  st = sgnn_encode_nodes(pos_seq, n, T, d, in->types, in->emb_w, in->emb_dim, in->use_emb, in->vel_mean,
+                         in->vel_std, in->wall_max, in->wall_div, m->enc_node, &m->edge[0], ws->x_a,
+                         ws->u, ws->v, nullptr, stream);
+  if (st) return st;
+  st = sgnn_encode_edges(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, d, in->radius, ws->rowptr,
+                         ws->send, ws->recv, n, ws->edge_cap, m->enc_edge, ws->e0t, nullptr, stream);
+  if (st) return st;
+  float* x_in = ws->x_a;
+  float* x_out = ws->x_b;
+  float scale = 1.0f;
+  for (int k = 0; k < m->nlayers; ++k, scale *= 2.0f) {
+    st = sgnn_edge_layer(ws->u, ws->v, ws->e0t, scale, ws->rowptr, ws->send, ws->recv, n, ws->edge_cap,
+                         &m->edge[k], ws->agg, ws->cin, ws->cout, nullptr, stream);
+    if (st) return st;
+    if (k < m->nlayers - 1) {
+      st = sgnn_node_layer(x_in, ws->agg, ws->cin, ws->cout, ws->rowptr, n, &m->node[k], &m->edge[k + 1],
+                           x_out, ws->u, ws->v, nullptr, stream);
+      float* t = x_in;
+      x_in = x_out;
+      x_out = t;
+    } else {
+      st = sgnn_node_layer_decode(x_in, ws->agg, ws->cin, ws->cout, ws->rowptr, n, &m->node[k], m->dec,
+                                  pos_seq, T, d, in->acc_mean, in->acc_std, nullptr, pred, next_pos,
+                                  window_out, nullptr, stream);
+    }
+    if (st) return st;
+  }
+  return SGNN_OK;
+}
+
+extern "C" int sgnn_rollout(const sgnn_epd* m, const sgnn_step_in* in, float* win_a, float* win_b,
+                            const sgnn_step_ws* ws, int32_t nsteps, float* out_pos, float* out_pred,
+                            void* stream) {
+  using namespace sgnn;
+  if (!win_a || !win_b || win_a == win_b || !out_pos || !out_pred || nsteps < 0)
+    return set_error(SGNN_ERR_INVALID, "rollout: bad arguments");
+  const int64_t n = in ? in->n : 0;
+  const int d = in ? in->dim : 0;
+  for (int32_t k = 0; k < nsteps; ++k) {
+    float* cur = (k & 1) ? win_b : win_a;
+    float* nxt = (k & 1) ? win_a : win_b;
+    const int st = sgnn_predict_positions(m, in, cur, ws, out_pred + (int64_t)k * n * (d + 1),
+                                          out_pos + (int64_t)k * n * d, nxt, stream);
+    if (st) return st;
+  }
+  return SGNN_OK;
+}

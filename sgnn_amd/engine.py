@@ -14,6 +14,7 @@ Data layout in HBM (per graph of n particles, hidden H, cap K):
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -68,6 +69,12 @@ class ParamPack:
         self.edge = [mlp_struct(g.edge_fn, True) for g in epd._processor.gnn_stacks]
         self.node = [mlp_struct(g.node_fn, True) for g in epd._processor.gnn_stacks]
         self.dec = mlp_struct(epd._decoder.node_fn, False)
+        nl = len(self.edge)
+        self.edge_arr = (SgnnMlp * nl)(*self.edge)
+        self.node_arr = (SgnnMlp * nl)(*self.node)
+        self.epd = _hip.SgnnEpd(nlayers=nl, enc_node=ctypes.addressof(self.enc_node),
+                                enc_edge=ctypes.addressof(self.enc_edge), edge=ctypes.addressof(self.edge_arr),
+                                node=ctypes.addressof(self.node_arr), dec=ctypes.addressof(self.dec))
 
     @staticmethod
     def get(epd: nn.Module) -> "ParamPack":
@@ -104,6 +111,11 @@ class StepWorkspace:
         self.agg = torch.empty(n, hidden, **f32)
         self.cin = torch.empty(ntiles, hidden, **f32)
         self.cout = torch.empty(ntiles, hidden, **f32)
+        self.c = _hip.SgnnStepWs(radius_ws=self.radius_ws_ptr(), rowptr=self.rowptr.data_ptr(),
+                                 send=self.send.data_ptr(), recv=self.recv.data_ptr(), edge_cap=self.edge_cap,
+                                 e0t=self.e0t.data_ptr(), x_a=self.x_a.data_ptr(), x_b=self.x_b.data_ptr(),
+                                 u=self.u.data_ptr(), v=self.v.data_ptr(), agg=self.agg.data_ptr(),
+                                 cin=self.cin.data_ptr(), cout=self.cout.data_ptr())
 
     def radius_ws_ptr(self) -> int:
         p = self.radius_ws.data_ptr()
@@ -233,13 +245,33 @@ class StepInputs:
     acc_std: torch.Tensor
 
 
+def step_in(inp: StepInputs, ws: StepWorkspace, radius: float, emb_weight: Optional[torch.Tensor],
+            use_emb: bool) -> "_hip.SgnnStepIn":
+    """struct sgnn_step_in of one single-scale step (wall feature clamp(x+2, 0, R))."""
+    emb_dim = emb_weight.shape[1] if (use_emb and emb_weight is not None) else 0
+    return _hip.SgnnStepIn(n=ws.n, T=ws.T, dim=ws.dim, ex_ptr=inp.ex_ptr.data_ptr(), n_ex=inp.n_ex,
+                           radius=float(radius), K=ws.K, types=_ptr(inp.types) if use_emb else 0,
+                           emb_w=_ptr(emb_weight) if use_emb else 0, emb_dim=emb_dim, use_emb=int(use_emb),
+                           vel_mean=inp.vel_mean.data_ptr(), vel_std=inp.vel_std.data_ptr(),
+                           acc_mean=inp.acc_mean.data_ptr(), acc_std=inp.acc_std.data_ptr(),
+                           wall_max=float(radius), wall_div=1.0)
+
+
 def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bool, radius: float,
                  inp: StepInputs, ws: StepWorkspace, pred: torch.Tensor, next_pos: torch.Tensor,
                  window_out: Optional[torch.Tensor] = None, timers: Optional[list] = None) -> None:
     """One LearnedSimulator.predict_positions (learned_simulator.py:413-438):
-    radius graph -> encoder -> L interaction layers -> decoder -> Euler."""
+    radius graph -> encoder -> L interaction layers -> decoder -> Euler.
+    Issued as ONE sgnn_predict_positions call (the launch sequence runs in C);
+    with `timers`, launched kernel by kernel so the edge layers can be timed."""
     L = lib()
     pk = ParamPack.get(epd)
+    if timers is None:
+        sin = step_in(inp, ws, radius, emb_weight, use_emb)
+        check(L.sgnn_predict_positions(ctypes.byref(pk.epd), ctypes.byref(sin), inp.pos_seq.data_ptr(),
+                                       ctypes.byref(ws.c), pred.data_ptr(), next_pos.data_ptr(),
+                                       _ptr(window_out), stream_ptr(inp.pos_seq.device)), "sgnn_predict_positions")
+        return
     n, T, d = ws.n, ws.T, ws.dim
     s = stream_ptr(inp.pos_seq.device)
     pos = inp.pos_seq
@@ -366,3 +398,91 @@ def epd_forward(epd, x, edge_index, edge_features):
     nl = len(pk.edge)
     return run_chain(pk.enc_node, {"e": pk.enc_edge}, pk.edge, pk.node, pk.dec, ["e"] * nl,
                      [2.0 ** k for k in range(nl)], x, {"e": g}, {"e": ef}, pk.dec.out_dim)
+
+
+class DeviceRollout:
+    """Autoregressive rollout issued as ONE sgnn_rollout call (evaluate.py:
+    117-145): the C driver ping-pongs two window buffers (the shift is fused
+    into the decoder kernel) and writes every step's prediction straight into
+    its output slot — no host round trip, no Python per kernel."""
+
+    def __init__(self, epd_struct, sin, ws: StepWorkspace, window: torch.Tensor, n: int, dim: int,
+                 nsteps: int, keep=()):
+        dev = window.device
+        self.epd, self.sin, self.ws, self.keep = epd_struct, sin, ws, keep
+        self.n, self.dim, self.nsteps = n, dim, nsteps
+        self.win = [window.to(torch.float32).contiguous().clone(), torch.empty_like(window, dtype=torch.float32)]
+        self.out_pos = torch.empty(max(nsteps, 1), n, dim, dtype=torch.float32, device=dev)
+        self.out_pred = torch.empty(max(nsteps, 1), n, dim + 1, dtype=torch.float32, device=dev)
+
+    def run(self, window: Optional[torch.Tensor] = None):
+        """Returns (positions [nsteps, n, dim], strain [nsteps, n]) on the device."""
+        if window is not None:
+            self.win[0].copy_(window)
+        check(lib().sgnn_rollout(ctypes.byref(self.epd), ctypes.byref(self.sin), self.win[0].data_ptr(),
+                                 self.win[1].data_ptr(), ctypes.byref(self.ws.c), self.nsteps,
+                                 self.out_pos.data_ptr(), self.out_pred.data_ptr(),
+                                 stream_ptr(self.win[0].device)), "sgnn_rollout")
+        return self.out_pos[:self.nsteps], self.out_pred[:self.nsteps, :, -1]
+
+
+class RolloutRunner:
+    """Autoregressive rollout on the device (evaluate.py:117-145 with the
+    window shift fused into the decoder kernel), optionally replayed from a
+    captured HIP graph: two steps (window A -> B -> A) per graph, each followed
+    by a copy of the step's prediction into the output slot selected by a
+    device-side counter, so one captured graph serves the whole rollout with
+    no host round trip and no per-kernel launch cost."""
+
+    def __init__(self, step_fn, window: torch.Tensor, n: int, dim: int, nsteps: int,
+                 use_graph: bool = True):
+        dev = window.device
+        self.step_fn, self.n, self.dim, self.nsteps = step_fn, n, dim, nsteps
+        self.win = [window.to(torch.float32).contiguous().clone(), torch.empty_like(window, dtype=torch.float32)]
+        self.pred = torch.empty(n, dim + 1, dtype=torch.float32, device=dev)
+        self.nxt = torch.empty(n, dim, dtype=torch.float32, device=dev)
+        self.out_pos = torch.empty(max(nsteps, 1), n, dim, dtype=torch.float32, device=dev)
+        self.out_strain = torch.empty(max(nsteps, 1), n, dtype=torch.float32, device=dev)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.graph = None
+        # HIP-graph replay is opt-in: at the 2k-particle / r = 15 shape a replay
+        # hit an illegal address that the eager loop does not (under study).
+        self.use_graph = use_graph and bool(os.environ.get("SGNN_ROLLOUT_GRAPH"))
+
+    def _one(self, k: int) -> None:
+        self.step_fn(self.win[k % 2], self.pred, self.nxt, self.win[(k + 1) % 2])
+        self.out_pos.index_copy_(0, self.counter, self.nxt[None])
+        self.out_strain.index_copy_(0, self.counter, self.pred[None, :, -1])
+        self.counter += 1
+
+    def _capture(self) -> None:
+        s = torch.cuda.Stream(device=self.win[0].device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):       # warm-up (workspaces, kernel attributes)
+            self._one(0)
+            self._one(1)
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._one(0)
+            self._one(1)
+
+    def run(self, window: Optional[torch.Tensor] = None):
+        """Returns (positions [nsteps, n, dim], strain [nsteps, n]) on the device."""
+        if window is not None:
+            self.win[0].copy_(window)
+        if self.use_graph and self.nsteps >= 4:
+            if self.graph is None:
+                init = self.win[0].clone()
+                self._capture()          # its warm-up steps advance the window: restore it
+                self.win[0].copy_(init)
+            self.counter.zero_()
+            for _ in range(self.nsteps // 2):
+                self.graph.replay()
+            if self.nsteps % 2:
+                self._one(0)
+        else:
+            self.counter.zero_()
+            for k in range(self.nsteps):
+                self._one(k)
+        return self.out_pos[:self.nsteps], self.out_strain[:self.nsteps]

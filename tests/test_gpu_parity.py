@@ -163,3 +163,26 @@ def test_encode_process_decode_edgeless_and_shuffled():
     perm = torch.randperm(ei.shape[1], generator=torch.Generator().manual_seed(0))
     got = sim._encode_process_decode(nf.cuda(), ei[:, perm].cuda(), ef[perm].cuda())
     _close(got.cpu().numpy(), z["pred"], what="shuffled EPD.forward")
+
+
+@pytest.mark.parametrize("nsteps", [8, 9])
+def test_device_rollout_runner(nsteps):
+    """evaluate.rollout's device path (fused window shift, predictions written
+    into device slots) matches the oracle rollout."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import synthetic
+    z = golden("tiny2d_r06")
+    hp = hparams(z)
+    T = hp["T"]
+    seq = synthetic.trajectory(synthetic.lattice_2d(24, 16), T + nsteps, seed=17)
+    n = seq.shape[0]
+    sim = product_sim(z)
+    types_ = torch.zeros(n, dtype=torch.long, device="cuda")
+    win = torch.from_numpy(seq[:, :T]).cuda()
+    pos, strain = sim.rollout_runner(win, [n], types_, nsteps, use_graph=False).run()
+    torch.cuda.synchronize()
+    osim = oracle_sim(z)
+    ref_pos, ref_str = O.rollout(osim, torch.from_numpy(seq), torch.zeros(n, dtype=torch.long), n, nsteps, T)
+    scale = float(np.max(z["acc_std"]))
+    _close(pos.cpu().numpy(), ref_pos.numpy(), atol=2 * nsteps * ATOL * scale, rtol=1e-6,
+           what=f"device rollout {nsteps} positions")

@@ -1,11 +1,6 @@
 set -e
 export TMPDIR=/tmp
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-steps 0 --no-rollout-extras > gpurun_out/a.json
-SGNN_EXP_GW=1 timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-steps 0 --no-rollout-extras > gpurun_out/b.json
-SGNN_EXP_GW=1 timeout -k 10 300 python -m pytest tests/test_gpu_training.py -q -x -m gpu 2>&1 | tail -2
-python - <<'PY'
-import json
-for f in ['a','b']:
-    d=json.load(open(f'gpurun_out/{f}.json'))
-    print(f, d['ms_per_step'], d['kernel_avg_us'])
-PY
+SGNN_NO_GRAPH=1 timeout -k 10 300 python bench.py --mode rollout --workload c1_r15 --steps 40 --warmup 3 --cpu-steps 0 > gpurun_out/r_nog.json 2> gpurun_out/r_nog.err
+echo "no-graph ok"; cat gpurun_out/r_nog.json | cut -c1-200
+AMD_LOG_LEVEL=1 timeout -k 10 300 python bench.py --mode rollout --workload c1_r15 --steps 40 --warmup 3 --cpu-steps 0 > gpurun_out/r_g.json 2> gpurun_out/r_g.err
+echo "graph ok"; cat gpurun_out/r_g.json | cut -c1-200
