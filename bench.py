@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", choices=["train", "rollout", "ms-train", "ms-rollout"], default="train")
     ap.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(MS_WORKLOADS), default=None)
-    ap.add_argument("--cpu-steps", type=int, default=6, help="oracle steps for cpu_baseline (0: skip)")
+    ap.add_argument("--cpu-steps", type=int, default=10, help="oracle steps for cpu_baseline (0: skip)")
     ap.add_argument("--no-rollout-extras", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
@@ -350,7 +350,7 @@ def cpu_ms_train_baseline(sim, cfg, steps):
     from oracle import multi_scale_oracle as MO
     from oracle import sgnn_oracle as O
     dims, ns, win, mult, H, L, nmlp = cfg
-    sdims = (16, 16, 12) if len(dims) == 3 else (60, 40)
+    sdims = (24, 24, 16) if len(dims) == 3 else (60, 40)
     base = lattice(sdims)
     base[:, 0] -= 2.0
     seq = synthetic.trajectory(base, T_SEQ + 1, seed=9)
@@ -480,12 +480,20 @@ def main():
         res = bench_ms_rollout(args, world, rank, device)
     elif args.mode == "train":
         res = bench_train(args, world, rank, device)
-        if not args.no_rollout_extras:
+        if not args.no_rollout_extras and world == 1:
+            # the other BASELINE configs, each with its own bounded CPU baseline
             res["rollout"] = {}
-            for wl, cs in (("c2", 2), ("c1_r15", 3)):
-                r = bench_rollout(wl, 20, 3, world, rank, device, args.seed,
+            for wl, cs in (("c2", 2), ("c1_r15", 3), ("c4", 1)):
+                r = bench_rollout(wl, 20 if wl != "c4" else 10, 3, world, rank, device, args.seed,
                                   cs if args.cpu_steps > 0 else 0)[0]
                 res["rollout"][wl] = r
+            import argparse as _ap
+            ms_args = _ap.Namespace(**{**vars(args), "workload": "c5", "steps": 3, "warmup": 1})
+            ms = bench_ms_train(ms_args, world, rank, device)
+            res["multi_scale_c5_train"] = {k: ms[k] for k in ("value", "unit", "ms_per_step", "config",
+                                                              "M_edge_messages_per_s", "hbm_peak_gib",
+                                                              "roofline", "cpu_baseline", "speedup_vs_cpu")
+                                           if k in ms}
     else:
         r, timers, flops, edge_avg_s, E, n, radius, H, L = bench_rollout(
             args.workload, args.steps, args.warmup, world, rank, device, args.seed, args.cpu_steps)
