@@ -1154,12 +1154,33 @@ struct EdgeItemsArgs {
   float *dy_out, *d2_out;  // tiled scratch
 };
 
-template <int NL>
+// (templated on TH; at H = 64 the fused k_edge_bwd measured faster: the
+// split's GEMMs are load-latency bound there, 285 vs 175 us at C2)
+template <int TH, int NL>
 __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
-  constexpr int TH = 4, H = 128, ldh = H + 4;
+  constexpr bool GW = TH > 2;  // H = 64: weight images in LDS
+  constexpr int H = 32 * TH, ldh = H + 4;
+  constexpr int ldl = GW ? H : ldh, lde = GW ? 3 * H : ldh;
   const EdgeBwdArgs& a = p.b;
   extern __shared__ float lds[];
-  float* gam = lds;
+  float* q = lds;
+  const float* WlT = a.wl;
+  const float* WmT = a.wm;
+  const float* WeT = a.we;
+  if (!GW) {
+    stage_matrix_t(q, ldh, a.wl, H, H, H, H, H);
+    WlT = q;
+    q += H * ldh;
+    stage_matrix_t(q, ldh, a.we, 3 * H, H, H, H, H);
+    WeT = q;
+    q += H * ldh;
+    if (NL == 3) {
+      stage_matrix_t(q, ldh, a.wm, H, H, H, H, H);
+      WmT = q;
+      q += H * ldh;
+    }
+  }
+  float* gam = q;
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
   const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
@@ -1196,13 +1217,13 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
     if constexpr (NL == 3) {
       f32x16 d2[TH], act[TH];
       zero<TH>(d2);
-      matvec_t<TH, TH, true>(d2, a.wl, H, dy);
+      matvec_t<TH, TH, GW>(d2, WlT, ldl, dy);
       load_tiled<TH>(act, a.hs2 + tile * (32 * H));
       relu_mask<TH>(d2, act, valid);
       store_tiled<TH>(p.d2_out + tile * (32 * H), d2);
-      matvec_t<TH, TH, true>(dh, a.wm, H, d2);
+      matvec_t<TH, TH, GW>(dh, WmT, ldl, d2);
     } else {
-      matvec_t<TH, TH, true>(dh, a.wl, H, dy);
+      matvec_t<TH, TH, GW>(dh, WlT, ldl, dy);
     }
     {
       f32x16 act[TH];
@@ -1212,7 +1233,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
     {
       f32x16 de[TH];
       zero<TH>(de);
-      matvec_t<TH, TH, true>(de, a.we, 3 * H, dh);
+      matvec_t<TH, TH, GW>(de, WeT, lde, dh);
       float* dtile = a.de0t + tile * (32 * H);
       if (a.de0_accumulate) {
         f32x16 old[TH];
@@ -1636,11 +1657,11 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
     const int nl = edge_fn->nlin;
     const int64_t pad = 32 * ((edge_cap + 31) / 32);
     EdgeItemsArgs p{a, scratch, scratch + pad * H};
-    if (nl == 3) launch_bwd(k_edge_items<3>, nslab, kItemsLds, stream, p);
-    else launch_bwd(k_edge_items<2>, nslab, kItemsLds, stream, p);
     const int64_t vb = slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, nl), W = kWaves, ss = a.slab_stride;
     const int32_t* Edev = rowptr + n;
     const float* hl = nl == 3 ? saves->h2 : saves->h;
+    if (nl == 3) launch_bwd(k_edge_items<4, 3>, nslab, kItemsLds, stream, p);
+    else launch_bwd(k_edge_items<4, 2>, nslab, kItemsLds, stream, p);
     run_wgrad<4, 4>(wg(p.dy_out, 1, 0, hl, 1, 0, slab, 0, H, vb, ss, 0, Edev), nslab, stream);
     run_wgrad<4, 4>(wg(dh_rows, 0, H, e0t, 1, 0, slab, H * H, H, -1, ss, 0, Edev), nslab, stream);
     if (nl == 3)
