@@ -134,10 +134,22 @@ def max_over_ranks(x, world, device):
 
 
 # ----------------------------------------------------------------------------- rollout
+def quiet_decoder(sim):
+    """Scale the random-init decoder's output layer by 1e-3 so that the
+    autoregressive rollout of an untrained model stays physical (particles
+    stay on the lattice, the graph keeps its Taylor-bar connectivity instead
+    of collapsing towards the K-cap).  Work per step is unchanged."""
+    with torch.no_grad():
+        last = [m for m in sim.modules() if isinstance(m, torch.nn.Linear)][-1]
+        last.weight.mul_(1e-3)
+        last.bias.mul_(1e-3)
+    return sim
+
+
 def rollout_setup(workload, device, seed, rank):
     dims, radius, H, L = WORKLOADS[workload]
     dim = len(dims)
-    sim = make_sim(H, L, radius, dim, device, seed)
+    sim = quiet_decoder(make_sim(H, L, radius, dim, device, seed))
     seq = synthetic.trajectory(lattice(dims), T_SEQ, seed=1000 + rank)
     n = seq.shape[0]
     window0 = torch.from_numpy(seq)

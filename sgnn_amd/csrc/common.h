@@ -407,3 +407,59 @@ SGNN_DEV void mlp_tail(f32x16 (&y)[TO], const f32x16 (&h)[TH], const float* Wm, 
   f32x16 h2[TH];
   mlp_tail<TH, NL, TO, GL>(y, h2, h, Wm, ldm, bm_lds, Wl, ldl, bl_lds);
 }
+
+// Segment sum over the receiver-sorted CSR of a wave's 32-item LDS slice
+// (lane = unit) with tile carries (same contract as the forward edge layer).
+// The 32 rows are read up front; whether a segment starts / ends its
+// receiver's row follows from the neighbouring receivers (prev_recv = recv of
+// the edge before the tile, next_recv = of the edge after it, -1 if none), so
+// no rowptr loads sit on the serial path.
+template <int TH>
+SGNN_DEV void segment_sum_store(const float* slice, int ld, int rv, int nvalid, int64_t base,
+                                int64_t tile, int prev_recv, int next_recv, float* dst_rows,
+                                float* cin, float* cout) {
+  constexpr int H = 32 * TH;
+  constexpr int UPL = H / 64 > 0 ? H / 64 : 1;
+  const int l = lane_id();
+  float vals[UPL][32];
+#pragma unroll
+  for (int q = 0; q < UPL; ++q)
+#pragma unroll
+    for (int jj = 0; jj < 32; ++jj) vals[q][jj] = (l + 64 * q < H) ? slice[jj * ld + l + 64 * q] : 0.0f;
+  float acc[UPL];
+#pragma unroll
+  for (int q = 0; q < UPL; ++q) acc[q] = 0.0f;
+  bool starts_row = true;  // does the open segment start its receiver's row?
+#pragma unroll
+  for (int jj = 0; jj < 32; ++jj) {
+    if (jj < nvalid) {
+#pragma unroll
+      for (int q = 0; q < UPL; ++q) acc[q] += vals[q][jj];
+      const int rr = __builtin_amdgcn_readlane(rv, jj);
+      if (jj == 0) starts_row = prev_recv != rr;
+      const int nx = (jj + 1 < nvalid) ? __builtin_amdgcn_readlane(rv, jj + 1) : (jj == 31 ? next_recv : -1);
+      if (nx != rr) {
+        const bool ends_row = true;  // the next edge belongs to another receiver (or none)
+        float* dst = starts_row && ends_row ? dst_rows + (int64_t)rr * H
+                   : starts_row ? cout + tile * H : cin + tile * H;
+        (void)ends_row;
+#pragma unroll
+        for (int q = 0; q < UPL; ++q) {
+          if (l + 64 * q < H) dst[l + 64 * q] = acc[q];
+          acc[q] = 0.0f;
+        }
+        starts_row = true;
+      }
+    }
+  }
+  // an open segment at the tile end continues into the next tile
+  if (nvalid == 32) {
+    const int rr = __builtin_amdgcn_readlane(rv, 31);
+    if (next_recv == rr) {
+      float* dst = starts_row ? cout + tile * H : cin + tile * H;
+#pragma unroll
+      for (int q = 0; q < UPL; ++q)
+        if (l + 64 * q < H) dst[l + 64 * q] = acc[q];
+    }
+  }
+}

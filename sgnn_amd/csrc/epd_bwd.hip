@@ -47,10 +47,20 @@ SGNN_DEV void zero_if(f32x16 (&x)[TH], bool pred) {
 }
 
 // lane = unit: sum over the first nvalid items of a wave's LDS slice
+// (every image row past nvalid holds zeros, so all 32 rows are summed: four
+// independent partial sums over an unrolled loop instead of a dependent
+// load-add chain of runtime length)
 SGNN_DEV float lane_sum(const float* slice, int ld, int nvalid, int unit) {
-  float s = 0.0f;
-  for (int it = 0; it < nvalid; ++it) s += slice[it * ld + unit];
-  return s;
+  (void)nvalid;
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+#pragma unroll
+  for (int it = 0; it < 32; it += 4) {
+    s0 += slice[it * ld + unit];
+    s1 += slice[(it + 1) * ld + unit];
+    s2 += slice[(it + 2) * ld + unit];
+    s3 += slice[(it + 3) * ld + unit];
+  }
+  return (s0 + s1) + (s2 + s3);
 }
 
 template <int TH>
@@ -61,42 +71,6 @@ SGNN_DEV void lane_sums(float (&acc)[TH / 2 > 0 ? TH / 2 : 1], const float* slic
   for (int q = 0; q < UPL; ++q) {
     const int u = lane_id() + 64 * q;
     if (u < 32 * TH) acc[q] += lane_sum(slice, ld, nvalid, u);
-  }
-}
-
-// Segment sum over the receiver-sorted CSR of a wave's 32-item LDS slice
-// (lane = unit) with tile carries (same contract as the forward edge layer).
-template <int TH>
-SGNN_DEV void segment_sum_store(const float* slice, int ld, int rv, int nvalid, int64_t base,
-                                int64_t tile, const int32_t* rowptr, float* dst_rows, float* cin,
-                                float* cout) {
-  constexpr int H = 32 * TH;
-  constexpr int UPL = H / 64 > 0 ? H / 64 : 1;
-  const int l = lane_id();
-  float acc[UPL];
-#pragma unroll
-  for (int q = 0; q < UPL; ++q) acc[q] = 0.0f;
-  int seg0 = 0;
-  for (int jj = 0; jj < nvalid; ++jj) {
-#pragma unroll
-    for (int q = 0; q < UPL; ++q)
-      if (l + 64 * q < H) acc[q] += slice[jj * ld + l + 64 * q];
-    const int rr = __builtin_amdgcn_readlane(rv, jj);
-    const int nx = (jj + 1 < nvalid) ? __builtin_amdgcn_readlane(rv, jj + 1) : -1;
-    if (nx != rr) {
-      const int64_t seg_s = base + seg0, seg_e = base + jj + 1;
-      const int64_t rp0 = rowptr[rr], rp1 = rowptr[rr + 1];
-      float* dst;
-      if (rp0 == seg_s && rp1 == seg_e) dst = dst_rows + (int64_t)rr * H;
-      else if (rp0 == seg_s) dst = cout + tile * H;
-      else dst = cin + tile * H;
-#pragma unroll
-      for (int q = 0; q < UPL; ++q) {
-        if (l + 64 * q < H) dst[l + 64 * q] = acc[q];
-        acc[q] = 0.0f;
-      }
-      seg0 = jj + 1;
-    }
   }
 }
 
@@ -379,6 +353,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
     f32x16 dm[TH], yh[TH], h1[TH], h2[TH];
     float rs = 0.0f;
     int rv = 0;
+    const int prv = (nvalid > 0 && base > 0) ? a.recv[base - 1] : -1;  // receivers around the tile
+    const int nxt = base + 32 < E ? a.recv[base + 32] : -1;
     if (nvalid > 0) {  // tiles past the last valid one are not allocated
       rv = a.recv[ec];
       load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
@@ -427,7 +403,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
     lds_store_items<TH>(im.sB, ldh, j, e0);
     wave_lds_sync();
     if (nvalid > 0)
-      segment_sum_store<TH>(im.sA, ldh, rv, nvalid, base, tile, a.rowptr, a.du, a.cin, a.cout);
+      segment_sum_store<TH>(im.sA, ldh, rv, nvalid, base, tile, prv, nxt, a.du, a.cin, a.cout);
     __syncthreads();
     outer_tiles<NT>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1e = sum dh (x) e0
     __syncthreads();
@@ -1196,6 +1172,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
     const bool valid = e < E;
     const int64_t ec = valid ? e : E - 1;
     const int rv = a.recv[ec];
+    const int prv = base > 0 ? a.recv[base - 1] : -1;  // receivers around the tile
+    const int nxt = base + 32 < E ? a.recv[base + 32] : -1;
     f32x16 dy[TH];
     {
       f32x16 dm[TH], yh[TH];
@@ -1253,7 +1231,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
     if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
     lds_store_items<TH>(sl, ldh, j, dh);
     wave_lds_sync();
-    segment_sum_store<TH>(sl, ldh, rv, nvalid, base, tile, a.rowptr, a.du, a.cin, a.cout);
+    segment_sum_store<TH>(sl, ldh, rv, nvalid, base, tile, prv, nxt, a.du, a.cin, a.cout);
     wave_lds_sync();
   }
   float* v = a.slab + blockIdx.x * a.slab_stride + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, NL);

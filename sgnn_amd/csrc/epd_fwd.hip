@@ -293,6 +293,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     const int64_t ec = valid ? e : E - 1;
     const int rv = a.recv[ec];
     const int64_t s = a.send[ec];
+    const int prv = base > 0 ? a.recv[base - 1] : -1;  // receivers around the tile
+    const int nxt = base + 32 < E ? a.recv[base + 32] : -1;
     f32x16 hacc[TH];
     load_row_clayout<TH>(hacc, a.u + (int64_t)rv * H);
     add_row_clayout<TH>(hacc, a.v + s * H);
@@ -327,31 +329,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     wave_lds_sync();
     // wave-segmented sum over the receiver-sorted CSR: lane = latent unit
     const int nvalid = (E - base) < 32 ? (int)(E - base) : 32;
-    constexpr int UPL = H / 64 > 0 ? H / 64 : 1;  // units per lane
-    float acc[UPL];
-#pragma unroll
-    for (int q = 0; q < UPL; ++q) acc[q] = 0.0f;
-    int seg0 = 0;
-    for (int jj = 0; jj < nvalid; ++jj) {
-#pragma unroll
-      for (int q = 0; q < UPL; ++q) acc[q] += ml[jj * ldh + l + 64 * q];
-      const int rr = __builtin_amdgcn_readlane(rv, jj);
-      const int nx = (jj + 1 < nvalid) ? __builtin_amdgcn_readlane(rv, jj + 1) : -1;
-      if (nx != rr) {
-        const int64_t seg_s = base + seg0, seg_e = base + jj + 1;
-        const int64_t rp0 = a.rowptr[rr], rp1 = a.rowptr[rr + 1];
-        float* dst;
-        if (rp0 == seg_s && rp1 == seg_e) dst = a.agg + (int64_t)rr * H;
-        else if (rp0 == seg_s) dst = a.cout + tile * H;  // continues into the next tile
-        else dst = a.cin + tile * H;                      // began in the previous tile
-#pragma unroll
-        for (int q = 0; q < UPL; ++q) {
-          if (64 * q + l < H) dst[l + 64 * q] = acc[q];
-          acc[q] = 0.0f;
-        }
-        seg0 = jj + 1;
-      }
-    }
+    segment_sum_store<TH>(ml, ldh, rv, nvalid, base, tile, prv, nxt, a.agg, a.cin, a.cout);
     wave_lds_sync();
   }
 }

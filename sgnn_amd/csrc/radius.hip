@@ -217,12 +217,34 @@ SGNN_DEV float dist2_ordered(const float* a, const float* b, int dim) {
   return s;
 }
 
+// Wave-aggregated atomic add of 1 per active lane to counter[key]: one atomic
+// per distinct key in the wave (coarse cells put a whole wave's particles in
+// one or two cells, where per-lane atomics serialise on one address).
+// Returns the lane's slot = old counter value + its rank among same-key lanes.
+SGNN_DEV int32_t wave_aggregated_inc(int32_t* counter, int32_t key, bool active) {
+  const int lane = lane_id();
+  uint64_t remaining = __ballot(active);
+  int32_t slot = 0;
+  while (remaining) {
+    const int leader = __ffsll((unsigned long long)remaining) - 1;
+    const int32_t lkey = __shfl(key, leader, 64);
+    const uint64_t grp = __ballot(active && key == lkey) & remaining;
+    int32_t base = 0;
+    if (lane == leader) base = atomicAdd(&counter[lkey], (int32_t)__popcll(grp));
+    base = __shfl(base, leader, 64);
+    if ((grp >> lane) & 1ull) slot = base + (int32_t)__popcll(grp & ((1ull << lane) - 1ull));
+    remaining &= ~grp;
+  }
+  return slot;
+}
+
 __global__ __launch_bounds__(256) void k_cell_assign(const float* pos, int64_t stride, int64_t n,
                                                      int dim, const int64_t* ex_ptr, int n_ex,
                                                      const uint32_t* bbox, int32_t* cell_of_p,
                                                      int32_t* ex_of, int32_t* count) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i0 < n;
+  const int64_t i = active ? i0 : n - 1;
   const Grid G = *reinterpret_cast<const Grid*>(bbox + 8);
   int lo = 0, hi = n_ex - 1;  // largest b with ex_ptr[b] <= i
   while (lo < hi) {
@@ -233,18 +255,21 @@ __global__ __launch_bounds__(256) void k_cell_assign(const float* pos, int64_t s
   int c[3] = {0, 0, 0};
   for (int d = 0; d < dim; ++d) c[d] = cell_of(p[d], G.lo[d], G.inv_cell, G.g[d]);
   const int32_t key = (int32_t)((((int64_t)lo * G.g[2] + c[2]) * G.g[1] + c[1]) * G.g[0] + c[0]);
-  cell_of_p[i] = key;
-  ex_of[i] = lo;
-  atomicAdd(&count[key], 1);
+  if (active) {
+    cell_of_p[i] = key;
+    ex_of[i] = lo;
+  }
+  (void)wave_aggregated_inc(count, key, active);
 }
 
 __global__ __launch_bounds__(256) void k_cell_scatter(int64_t n, const int32_t* cell_of_p,
                                                       const int32_t* start, int32_t* fill,
                                                       int32_t* order) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int32_t b = cell_of_p[i];
-  order[start[b] + atomicAdd(&fill[b], 1)] = (int32_t)i;
+  const bool active = i < n;
+  const int32_t b = active ? cell_of_p[i] : 0;
+  const int32_t slot = wave_aggregated_inc(fill, b, active);
+  if (active) order[start[b] + slot] = (int32_t)i;
 }
 
 SGNN_DEV int bitonic_sort64(int key, int lane) {

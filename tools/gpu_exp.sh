@@ -1,13 +1,16 @@
 set -e
 export TMPDIR=/tmp
-SGNN_SPLIT_H64=1 timeout -k 10 300 python -m pytest tests/test_gpu_training.py -q -x -m gpu > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
 tail -1 gpurun_out/t.log
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-steps 0 --no-rollout-extras > gpurun_out/a.json
-SGNN_SPLIT_H64=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-steps 0 --no-rollout-extras > gpurun_out/b.json
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-steps 0 --no-rollout-extras > gpurun_out/b.json
 python - <<'PY'
 import json
-for f in ['a','b']:
-    d=json.load(open(f'gpurun_out/{f}.json'))
-    print(f, round(d['ms_per_step'],4), {k: round(v,1) for k,v in d['kernel_avg_us'].items()})
+d=json.load(open('gpurun_out/b.json'))
+print('train', round(d['ms_per_step'],4), {k: round(v,1) for k,v in d['kernel_avg_us'].items()})
 PY
-SGNN_SPLIT_H64=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_split -o run -- python3 bench.py --steps 5 --warmup 2 --cpu-steps 0 --no-rollout-extras > /dev/null 2>&1
+for wl in c2 c1_r15 c4; do
+timeout -k 10 300 python bench.py --mode rollout --workload $wl --steps 20 --warmup 3 --cpu-steps 0 > gpurun_out/r_$wl.json
+python -c "import json;d=json.load(open('gpurun_out/r_$wl.json'));print('$wl', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],4), 'ms', round(d['roofline']['avg_launch_us'],1), 'us', round(d['roofline']['frac'],3))"
+done
+timeout -k 10 300 python bench.py --mode ms-train --workload c5_small --steps 5 --warmup 2 --cpu-steps 0 > gpurun_out/ms.json
+python -c "import json;d=json.load(open('gpurun_out/ms.json'));print('c5s', round(d['ms_per_step'],2), d['kernel_avg_us'])"
