@@ -211,7 +211,7 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps)
         sync_barrier(world)
         dt = time.perf_counter() - t0
         timers = []
-        run(warmup + steps, steps, timers=timers)
+        run(0, steps, timers=timers)   # from the initial window (win[0])
         torch.cuda.synchronize()
     dt = max_over_ranks(dt, world, device)
     E = ws.num_edges()
