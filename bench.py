@@ -292,9 +292,10 @@ def bench_train(args, world, rank, device):
     E = tw.f.num_edges()
     loss = float(out["loss"])
     kstats = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in timers.items()}
-    # dominant kernel by total time: the edge-layer backward (4 MFMA products / edge)
+    # dominant kernel by total time: the edge-layer backward: W2^T dy, dW2 += dy h^T,
+    # dW1e += dh e0^T (+ W1e^T dh when dE0 is accumulated in-layer, H = 128)
     dom = "k_edge_bwd"
-    flops_bwd = E * 8 * H * H   # W2^T dy, W1e^T dh, dW2 += dy h^T, dW1e += dh e0^T
+    flops_bwd = E * (6 if tw.latent_pass else 8) * H * H
     achieved = flops_bwd / kstats[dom]
     prof = profiled_traffic(args.workload, "train", dom)
     res = {

@@ -292,6 +292,14 @@ int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t*
                         float* cout, float* dh_rows, float* de0t, int32_t de0_accumulate,
                         float* slab, int32_t nslab, float* scratch, int64_t edge_cap,
                         void* stream);
+/* dE0 = sum_k scales[k] W1e_k^T dh_k (edge_fns[k].w1 columns 2H..3H) over
+ * nlayers layers that share one encoded edge latent, from each layer's dh
+ * rows [E][H] (the dh_rows output of sgnn_edge_layer_bwd, one buffer per
+ * layer).  With it, sgnn_edge_layer_bwd is called with de0t = NULL (H = 64).
+ * Writes de0t in the tiled layout of e0. */
+int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp* edge_fns,
+                          const float* scales, int32_t nlayers, const int32_t* rowptr, int64_t n,
+                          int64_t edge_cap, float* de0t, void* stream);
 int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, const float* cout,
                 const int32_t* rowptr, const float* dh_rows, const int32_t* tptr,
                 const int32_t* tperm, const float* x_in, int64_t n, const sgnn_mlp* edge_fn,

@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
                                     acc_wl, acc_wm, s_db, s_dg, s_dbl, s_dbm, dh);
     f32x16 e0[TH];
     zero<TH>(e0);
-    if (nvalid > 0) {
+    if (nvalid > 0 && a.de0t) {
       // dE0 += 2^k W1e^T dh (the edge latent feeding layer k is 2^k e0)
       f32x16 de[TH];
       zero<TH>(de);
@@ -395,6 +395,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
           for (int r = 0; r < 16; ++r) de[t][r] *= a.e_scale;
       }
       store_tiled<TH>(dtile, de);
+    }
+    if (nvalid > 0) {
       if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
       load_tiled<TH>(e0, a.e0t + tile * (32 * H));
       zero_if<TH>(e0, !valid);
@@ -1619,8 +1621,8 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
                                    float* scratch, int64_t edge_cap, void* stream) {
   using namespace sgnn;
   if (!edge_fn || !dagg || !rowptr || !send || !recv || !saves || !saves->h || !saves->yhat ||
-      !saves->rstd || !e0t || !du || !cin || !cout || !dh_rows || !de0t || !slab || nslab < 1 ||
-      n <= 0)
+      !saves->rstd || !e0t || !du || !cin || !cout || !dh_rows || !slab || nslab < 1 || n <= 0 ||
+      (!de0t && edge_fn->hidden == 128))
     return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: bad arguments");
   int st = check_bwd_mlp(edge_fn, "edge_layer_bwd: edge MLP");
   if (st) return st;
@@ -1888,4 +1890,81 @@ extern "C" int sgnn_embedding_grad(const float* G, int32_t ntypes, int32_t hidde
                      static_cast<hipStream_t>(stream), G, ntypes, hidden, w1, w1_ld, col0, emb_dim,
                      demb, accumulate);
   return check_launch("embedding_grad");
+}
+
+// ---------------------------------------------------------------------------
+// dE0 = sum_k scale_k W1e_k^T dh_k over the interaction layers sharing one
+// encoded edge latent (the input of layer k is scale_k e0, scale_k = 2^k):
+// one streaming pass over the edges after the layer backwards, instead of a
+// read-modify-write of dE0 inside every layer's edge backward.
+namespace {
+constexpr int kMaxLatentLayers = 16;
+struct EdgeLatentGradArgs {
+  const float* dh[kMaxLatentLayers];   // [E][H] rows per layer
+  const float* we[kMaxLatentLayers];   // edge W1 + 2H per layer (ld 3H)
+  float scale[kMaxLatentLayers];
+  int nlayers;
+  const int32_t* rowptr;
+  int64_t n;
+  float* de0t;
+};
+
+// dE0 = sum_k (2^k W1e_k^T) dh_k per edge tile, the scaled transposed
+// images of every layer staged in LDS once per workgroup; the next layer's dh
+// rows are prefetched under the current layer's MFMAs.  (Measured: the same
+// kernel with the images in L2 and full occupancy is not faster.)
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_edge_latent_grad(EdgeLatentGradArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4;
+  extern __shared__ float lds[];
+  for (int k = 0; k < a.nlayers; ++k)
+    stage_matrix_t(lds + k * H * ldh, ldh, a.we[k], 3 * H, H, H, H, H, a.scale[k]);
+  __syncthreads();
+  const int w = threadIdx.x >> 6, j = lane_id() & 31;
+  const int64_t E = a.rowptr[a.n];
+  const int64_t ntiles = (E + 31) / 32;
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t tile = (int64_t)blockIdx.x * kWaves + w; tile < ntiles; tile += nw) {
+    const int64_t e = tile * 32 + j;
+    const int64_t ec = e < E ? e : E - 1;
+    f32x16 de[TH], cur[TH], nxt[TH];
+    zero<TH>(de);
+    load_row_clayout<TH>(cur, a.dh[0] + ec * H);
+    for (int k = 0; k < a.nlayers; ++k) {
+      if (k + 1 < a.nlayers) load_row_clayout<TH>(nxt, a.dh[k + 1] + ec * H);  // prefetch
+      zero_if<TH>(cur, e >= E);
+      mfma_from_acc<TH, TH>(de, lds + k * H * ldh, ldh, 0, cur);
+#pragma unroll
+      for (int t = 0; t < TH; ++t) cur[t] = nxt[t];
+    }
+    store_tiled<TH>(a.de0t + tile * (32 * H), de);
+  }
+}
+}  // namespace
+
+extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp* edge_fns,
+                                     const float* scales, int32_t nlayers, const int32_t* rowptr,
+                                     int64_t n, int64_t edge_cap, float* de0t, void* stream) {
+  using namespace sgnn;
+  if (!dh_rows || !edge_fns || !scales || !rowptr || !de0t || nlayers < 1 || n <= 0 || edge_cap < 1)
+    return set_error(SGNN_ERR_INVALID, "edge_latent_grad: bad arguments");
+  const int H = edge_fns[0].hidden;
+  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "edge_latent_grad: hidden 64 only (128 accumulates in-layer)");
+  if (nlayers > 9) return set_error(SGNN_ERR_UNSUPPORTED, "edge_latent_grad: at most 9 layers share an edge latent");
+  EdgeLatentGradArgs a{};
+  for (int k = 0; k < nlayers; ++k) {
+    if (!dh_rows[k] || !edge_fns[k].w1 || edge_fns[k].hidden != H)
+      return set_error(SGNN_ERR_INVALID, "edge_latent_grad: layer arguments");
+    a.dh[k] = dh_rows[k];
+    a.we[k] = edge_fns[k].w1 + 2 * H;
+    a.scale[k] = scales[k];
+  }
+  a.nlayers = nlayers;
+  a.rowptr = rowptr;
+  a.n = n;
+  a.de0t = de0t;
+  const size_t lds = 4 * (size_t)nlayers * H * (H + 4);
+  const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 2);
+  launch_bwd(k_edge_latent_grad<2>, (int)grid, lds, stream, a);
+  return check_launch("edge_latent_grad");
 }

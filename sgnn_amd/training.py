@@ -255,8 +255,14 @@ class TrainWorkspace:
         self.pred = e(n, dim + 1)
         self.next_scratch = e(n, dim)
         self.g, self.dxp, self.dagg, self.du = e(n, H), e(n, H), e(n, H), e(n, H)
-        self.dh_rows = e(cap, H)
+        # H = 64: one dh-rows buffer per layer, dE0 formed afterwards in one pass
+        # (sgnn_edge_latent_grad); H = 128 accumulates dE0 inside the layers
+        self.latent_pass = H == 64 and nl <= 9
+        self.dh_layers = [e(cap, H) for _ in range(nl if self.latent_pass else 1)]
+        self.dh_rows = self.dh_layers[0]
         self.de0t = e(tl)
+        self._dh_ptrs = (ctypes.c_void_p * len(self.dh_layers))(*[t.data_ptr() for t in self.dh_layers])
+        self._scales = (ctypes.c_float * nl)(*[float(2.0 ** k) for k in range(nl)])
         i32 = dict(dtype=torch.int32, device=device)
         self.tptr = torch.empty(n + 1, **i32)
         self.tperm = torch.empty(cap, **i32)
@@ -431,19 +437,25 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
               "sgnn_node_layer_bwd")
         with _Timer(timers, "k_edge_bwd"):
           esv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k], h2=tw.e_h2[k])
+          dh_rows = tw.dh_layers[k] if tw.latent_pass else tw.dh_rows
           check(L.sgnn_edge_layer_bwd(tw.dagg.data_ptr(), ws.rowptr.data_ptr(), ws.send.data_ptr(),
                                     ws.recv.data_ptr(), n, ctypes.byref(esv), ws.e0t.data_ptr(), float(2.0 ** k),
                                     ctypes.byref(pk.edge[k]), tw.du.data_ptr(), ws.cin.data_ptr(),
-                                    ws.cout.data_ptr(), tw.dh_rows.data_ptr(), tw.de0t.data_ptr(),
+                                    ws.cout.data_ptr(), dh_rows.data_ptr(),
+                                    None if tw.latent_pass else tw.de0t.data_ptr(),
                                     int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), tw.nslab_of[_hip.SLAB_EDGE],
                                     tw.scratch.data_ptr(), ws.edge_cap, s),
               "sgnn_edge_layer_bwd")
         check(L.sgnn_uv_bwd(tw.dxp.data_ptr(), tw.du.data_ptr(), ws.cin.data_ptr(), ws.cout.data_ptr(),
-                            ws.rowptr.data_ptr(), tw.dh_rows.data_ptr(), tw.tptr.data_ptr(),
+                            ws.rowptr.data_ptr(), dh_rows.data_ptr(), tw.tptr.data_ptr(),
                             tw.tperm.data_ptr(), tw.xs[k].data_ptr(), n, ctypes.byref(pk.edge[k]),
                             tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV],
                             tw.scratch.data_ptr(), s),
               "sgnn_uv_bwd")
+    if tw.latent_pass:
+        check(L.sgnn_edge_latent_grad(tw._dh_ptrs, ctypes.byref(pk.edge_arr), tw._scales, tw.L,
+                                      ws.rowptr.data_ptr(), n, ws.edge_cap, tw.de0t.data_ptr(), s),
+              "sgnn_edge_latent_grad")
     ty, ew, ed, ue = emb_args(inp, emb_weight)
     check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, ty, ew, ed,
                                   int(emb_weight.shape[0]) if ue else 0, ue,

@@ -1,6 +1,6 @@
 set -e
 export TMPDIR=/tmp
-for wl in c2 c1_r06 c4; do
-timeout -k 10 300 python bench.py --mode rollout --workload $wl --steps 20 --warmup 3 --cpu-steps 0 > gpurun_out/r_$wl.json
-python -c "import json;d=json.load(open('gpurun_out/r_$wl.json'));print('$wl', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],4), 'ms', d['config']['edges'], round(d['roofline']['avg_launch_us'],1), 'us', round(d['roofline']['frac'],3))"
-done
+timeout -k 10 300 python -m pytest tests/test_gpu_training.py -q -x -m gpu > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+tail -1 gpurun_out/t.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_t -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-steps 0 --no-rollout-extras > gpurun_out/b.json 2>/dev/null
+python -c "import json;d=json.load(open('gpurun_out/b.json'));print(d['ms_per_step'])"
