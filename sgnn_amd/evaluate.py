@@ -54,8 +54,8 @@ def rollout(simulator, position: torch.Tensor, particle_types: torch.Tensor, n_p
     fast = (inference_mode == "autoregressive" and not any_erosional and nsteps > 0
             and hasattr(simulator, "rollout_runner") and position.is_cuda)
     if fast:
-        # device-resident loop: window shift fused into the decoder kernel, steps
-        # replayed from a captured HIP graph (same kernels, same arithmetic)
+        # device-resident loop: one sgnn_rollout call (window shift fused into the
+        # decoder kernel; same kernels and arithmetic as predict_positions)
         runner = simulator.rollout_runner(initial_positions, [n_particles_per_example], particle_types, nsteps)
         pred_positions, pred_strains = runner.run()
         nsteps = 0

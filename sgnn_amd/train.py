@@ -128,3 +128,192 @@ class Trainer:
         return {"loss": lo[0] / n_global, "loss_position": (lo[1] + lo[2] + lo[3]) / n_global,
                 "loss_strain": lo[4] / n_global, "loss_xyz": lo[1:4] / n_global,
                 "n_global": n_global, "lr": self.opt.lr}
+
+
+# ---------------------------------------------------------------------------
+# Harness around the step (train.py:29-491): config, simulator factory, the
+# training loop with validation-gated best-model checkpoints, resume, and
+# rollout prediction with the reference's output files.
+def load_config(config_path: str) -> dict:
+    """train.py:29-45 (yaml.safe_load)."""
+    import yaml
+    from pathlib import Path
+    p = Path(config_path)
+    if not p.exists():
+        raise FileNotFoundError(f"Config file not found: {config_path}")
+    with open(p) as f:
+        return yaml.safe_load(f)
+
+
+def _get_simulator(metadata: dict, acc_noise_std: float, vel_noise_std: float, device, config: dict):
+    """train.py:431-491: stats sigma = sqrt(sigma_meta^2 + noise^2); nnode_in =
+    (T-1)*dim + 1 (+ embedding size when there is more than one particle type);
+    nmlp_layers = 1."""
+    from .learned_simulator import LearnedSimulator
+    f = lambda k: torch.tensor(metadata[k], dtype=torch.float32)
+    stats = {"acceleration": {"mean": f("acc_mean").to(device),
+                              "std": torch.sqrt(f("acc_std") ** 2 + acc_noise_std ** 2).to(device)},
+             "velocity": {"mean": f("vel_mean").to(device),
+                          "std": torch.sqrt(f("vel_std") ** 2 + vel_noise_std ** 2).to(device)}}
+    ntypes = metadata.get("num_particle_types", 1)
+    dim = config["dim"]
+    nnode_in = (config["input_sequence_length"] - 1) * dim + 1
+    if ntypes > 1:
+        nnode_in += config["particle_type_embedding_size"]
+    return LearnedSimulator(particle_dimensions=dim, nnode_in=nnode_in, nedge_in=dim + 1,
+                            latent_dim=config["hidden_dim"], nmessage_passing_steps=config["layers"],
+                            nmlp_layers=1, mlp_hidden_dim=config["hidden_dim"],
+                            connectivity_radius=config["connection_radius"], normalization_stats=stats,
+                            nparticle_types=ntypes,
+                            particle_type_embedding_size=config["particle_type_embedding_size"],
+                            device=device)
+
+
+def rollout_split(simulator, metadata: dict, device, config: dict, split: str):
+    """Rollouts over every trajectory of `split` (train.py:84-135 / :318-349).
+    Yields (index, example_output) with example_output['metadata'] set."""
+    import os
+    from . import data, evaluate
+    loader = data.get_data_loader_by_trajectories(os.path.join(config["data_path"], f"{split}.npz"))
+    nsteps = metadata["sequence_length"] - config["input_sequence_length"]
+    for i, traj in enumerate(loader):
+        out = evaluate.rollout(simulator, traj["positions"].to(device), traj["particle_type"].to(device),
+                               traj["n_particles_per_example"].to(device), traj["strains"].to(device),
+                               nsteps, config["dim"], device, config["input_sequence_length"],
+                               config.get("inference_mode", "autoregressive"))
+        out["metadata"] = metadata
+        yield i, out
+
+
+def rollout_losses(out: dict) -> dict:
+    """train.py:110-114."""
+    rp, rs = out["rmse_position"], out["rmse_strain"]
+    return {"loss_total": float(rp[-1] + rs[-1]), "loss_position": float(rp[-1]),
+            "loss_strain": float(rs[-1]), "loss_oneStep": float(rp[0] + rs[0])}
+
+
+def predict(simulator, metadata: dict, device, config: dict) -> list:
+    """train.py:53-166: load the model, roll out `test` (mode 'rollout') or
+    `valid`, and in rollout mode write `<output_path>/<run_name>/<case>.pkl`
+    (the rollout dict + 'metadata' + 'case_name', evaluate.py:161-173)."""
+    import os
+    import pickle
+    from pathlib import Path
+    model_path = Path(config["model_path"]) / config["run_name"] / config["model_file"]
+    simulator.load(str(model_path))
+    simulator.to(device)
+    simulator.eval()
+    split = "test" if config["mode"] == "rollout" else "valid"
+    losses = []
+    for i, out in rollout_split(simulator, metadata, device, config, split):
+        losses.append(rollout_losses(out)["loss_total"])
+        if config["mode"] == "rollout":
+            case = metadata["file_test"][i].replace(".npz", "")
+            out["case_name"] = case
+            save_dir = Path(config["output_path"]) / config["run_name"]
+            save_dir.mkdir(parents=True, exist_ok=True)
+            with open(save_dir / f"{case}.pkl", "wb") as f:
+                pickle.dump(out, f)
+    return losses
+
+
+def train(simulator, metadata: dict, device, config: dict, group=None, log_every: int = 10,
+          generator: Optional[torch.Generator] = None) -> dict:
+    """train.py:185-428 on the HIP step.
+
+    Batches come from the split resident in device memory (data.DeviceSamples:
+    the reference DataLoader's samples and order, sliced on the device).  With
+    a process group of W ranks every global batch of `batch_size` windows is
+    split round-robin over the ranks (whole graphs per rank, one gradient
+    all-reduce per step) so the update equals the single-process one.
+    Validation every `nsave_steps` keeps only improving checkpoints
+    (model-best-<step>.pt + train_state-best-<step>.pt); without any
+    validation the final state is saved as model-final-<step>.pt.  Resumes from
+    config['model_file'] / config['train_state_file'] when model_file is set."""
+    import os
+    from pathlib import Path
+    from . import checkpoint_utils, data
+    rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    simulator.to(device)
+    trainer = Trainer(simulator, lr_init=config["lr_init"], lr_decay=config["lr_decay"],
+                      lr_decay_steps=config["lr_decay_steps"], noise_std=config["noise_std"],
+                      loss_weight_position=config.get("loss_weight_position", 1.0),
+                      loss_weight_strain=config.get("loss_weight_strain", 1.0), group=group)
+    if config.get("model_file"):
+        model_dir = os.path.join(config["model_path"], config["run_name"]) + "/"
+        checkpoint_utils.load_model(simulator, model_dir, config["model_file"], config["train_state_file"],
+                                    device, trainer=trainer)
+    samples = data.DeviceSamples(
+        data.TaylorImpactSamplesDataset(os.path.join(config["data_path"], "train.npz"),
+                                        config["input_sequence_length"]), device)
+    save_dir = Path(config["model_path"]) / config["run_name"]
+    lowest = float("inf")
+    history = []
+    nsteps = config["ntraining_steps"]
+    while trainer.step < nsteps:
+        for idx in samples.index_batches(config["batch_size"], shuffle=True, generator=generator):
+            mine = idx[rank::world]            # this rank's whole graphs of the global batch
+            if not mine:
+                raise ValueError(f"batch of {len(idx)} graphs cannot feed {world} ranks")
+            batch = samples.batch(mine)
+            inp, outp = batch["input"], batch["output"]
+            out = trainer.train_step(inp["positions"], outp["next_position"], outp["next_strain"],
+                                     inp["n_particles_per_example"].tolist(), inp["particle_type"],
+                                     n_global=samples.count(idx))
+            step = trainer.step
+            if step % log_every == 0:
+                history.append((step, float(out["loss"])))
+                if rank == 0:
+                    print(f"Step {step}: Total Loss = {history[-1][1]:.6f}")
+            if config.get("nsave_steps") and step % config["nsave_steps"] == 0:
+                simulator.eval()
+                losses = [rollout_losses(o)["loss_total"]
+                          for _, o in rollout_split(simulator, metadata, device, config, "valid")]
+                simulator.train()
+                mean = float(sum(losses) / len(losses))
+                if mean < lowest:
+                    lowest = mean
+                    if rank == 0:
+                        save_dir.mkdir(parents=True, exist_ok=True)
+                        simulator.save(str(save_dir / f"model-best-{step:06}.pt"))
+                        checkpoint_utils.save_train_state(str(save_dir / f"train_state-best-{step:06}.pt"),
+                                                          trainer.opt.state_dict(), step,
+                                                          lowest_eval_loss=lowest)
+            if step >= nsteps:
+                break
+    if lowest == float("inf") and rank == 0:
+        save_dir.mkdir(parents=True, exist_ok=True)
+        simulator.save(str(save_dir / f"model-final-{trainer.step:06}.pt"))
+        checkpoint_utils.save_train_state(str(save_dir / f"train_state-final-{trainer.step:06}.pt"),
+                                          trainer.opt.state_dict(), trainer.step)
+    return {"step": trainer.step, "lowest_eval_loss": lowest, "history": history, "trainer": trainer}
+
+
+def main(argv=None) -> None:
+    """train.py:494-552 without wandb: --config, --mode, --model_file."""
+    import argparse
+    import os
+    from . import data
+    ap = argparse.ArgumentParser(description="Single-scale GNN training (MI355X)")
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--mode", choices=["train", "valid", "rollout"])
+    ap.add_argument("--model_file")
+    args = ap.parse_args(argv)
+    config = load_config(args.config)
+    if args.mode:
+        config["mode"] = args.mode
+    if args.model_file:
+        config["model_file"] = args.model_file
+    device = torch.device("cuda")
+    metadata = data.read_metadata(config["data_path"])
+    sim = _get_simulator(metadata, config["noise_std"], config["noise_std"], device, config).to(device)
+    if config["mode"] == "train":
+        train(sim, metadata, device, config)
+    else:
+        losses = predict(sim, metadata, device, config)
+        print(f"Mean loss: {sum(losses) / max(len(losses), 1):.6f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -35,6 +35,7 @@ class FlatParams:
         self.param = torch.empty(total, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
         self.offsets: Dict[int, Tuple[int, int]] = {}
+        self.order = []   # (offset, numel, shape) in parameters() order
         off = 0
         with torch.no_grad():
             for p in params:
@@ -43,6 +44,7 @@ class FlatParams:
                 p.data = self.param[off:off + n].view_as(p)
                 p.grad = self.grad[off:off + n].view_as(p)
                 self.offsets[id(p)] = (off, n)
+                self.order.append((off, n, tuple(p.shape)))
                 off += n
         self.numel = total
 
@@ -488,6 +490,48 @@ class Adam:
         self.exp_avg = torch.zeros_like(flat.param)
         self.exp_avg_sq = torch.zeros_like(flat.param)
         self.step_count = 0
+
+    def state_dict(self) -> dict:
+        """torch.optim.Adam.state_dict() layout (per-parameter exp_avg /
+        exp_avg_sq / step, parameters numbered in module.parameters() order), so
+        the reference's train_state files and these are interchangeable."""
+        f = self.flat
+        group = dict(torch.optim.Adam([torch.zeros(1)], lr=self.lr, betas=self.betas,
+                                      eps=self.eps).state_dict()["param_groups"][0])
+        group["params"] = list(range(len(f.order)))
+        state = {}
+        if self.step_count > 0:
+            for i, (off, n, shape) in enumerate(f.order):
+                state[i] = {"step": torch.tensor(float(self.step_count)),
+                            "exp_avg": self.exp_avg[off:off + n].view(shape).detach().clone(),
+                            "exp_avg_sq": self.exp_avg_sq[off:off + n].view(shape).detach().clone()}
+        return {"state": state, "param_groups": [group]}
+
+    def load_state_dict(self, sd: dict) -> None:
+        f = self.flat
+        groups = sd["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(f.order):
+            raise ValueError(f"optimizer state has {sum(len(g['params']) for g in groups)} parameters "
+                             f"in {len(groups)} groups; this model has {len(f.order)} in one")
+        g = groups[0]
+        self.lr, self.betas, self.eps = float(g["lr"]), tuple(g["betas"]), float(g["eps"])
+        steps = set()
+        with torch.no_grad():
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            for slot, pid in enumerate(g["params"]):
+                st = sd["state"].get(pid)
+                if st is None:
+                    continue
+                off, n, shape = f.order[slot]
+                if tuple(st["exp_avg"].shape) != tuple(shape):
+                    raise ValueError(f"optimizer state {pid}: shape {tuple(st['exp_avg'].shape)} != {tuple(shape)}")
+                self.exp_avg[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"parameters at different Adam steps {sorted(steps)}: one fused update cannot resume them")
+        self.step_count = steps.pop() if steps else 0
 
     def step(self) -> None:
         self.step_count += 1
