@@ -25,7 +25,7 @@ class _TrainedEPD(torch.autograd.Function):
         training.train_forward(sim._encode_process_decode, sim._connectivity_radius, inp, tw, emb_weight=emb)
         tw.generation = getattr(tw, "generation", 0) + 1
         ctx.sim, ctx.inp, ctx.tw, ctx.gen, ctx.emb = sim, inp, tw, tw.generation, emb
-        return tw.pred.clone()
+        return tw.pred[:tw.n].clone()
 
     @staticmethod
     def backward(ctx, dpred):
@@ -242,15 +242,16 @@ class LearnedSimulator(nn.Module):
 
     def _train_workspace(self, n: int, T: int, device) -> training.TrainWorkspace:
         cache = self.__dict__.setdefault("_tw_cache", {})
-        key = (n, T, str(device))
+        cap = training.capacity(n)
+        key = (cap, T, str(device))
         tw = cache.get(key)
         if tw is None:
             if len(cache) > 4:
                 cache.clear()
-            tw = training.TrainWorkspace(self._encode_process_decode, n, T, self._particle_dimensions,
+            tw = training.TrainWorkspace(self._encode_process_decode, cap, T, self._particle_dimensions,
                                          self._max_num_neighbors, True, device)
             cache[key] = tw
-        return tw
+        return tw.activate(n)
 
     def _inverse_decoder_postprocessor(self, next_position, position_sequence):
         """learned_simulator.py:493-517"""

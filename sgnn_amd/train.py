@@ -82,15 +82,16 @@ class Trainer:
         self._count_cache: Dict[int, int] = {}
 
     def workspace(self, n: int, T: int, device) -> training.TrainWorkspace:
-        key = (n, T, str(device))
+        cap = training.capacity(n)
+        key = (cap, T, str(device))
         tw = self._tw.get(key)
         if tw is None:
             if len(self._tw) > 4:
                 self._tw.clear()
-            tw = training.TrainWorkspace(self.epd, n, T, self.sim._particle_dimensions,
+            tw = training.TrainWorkspace(self.epd, cap, T, self.sim._particle_dimensions,
                                          self.sim._max_num_neighbors, True, device, self.nslab)
             self._tw[key] = tw
-        return tw
+        return tw.activate(n)
 
     def train_step(self, position: torch.Tensor, next_position: torch.Tensor,
                    next_strain: torch.Tensor, nparticles_per_example, particle_types=None,

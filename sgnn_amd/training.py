@@ -221,8 +221,20 @@ def nslab_table(nslab: int) -> Dict[int, int]:
             _hip.SLAB_UV: node_ns, _hip.SLAB_DECODER: node_ns, _hip.SLAB_ENC_NODE: node_ns}
 
 
+def capacity(n: int) -> int:
+    """Particle capacity of the workspace that serves a batch of n particles:
+    n rounded up to 1/8-1/16 of its power of two (min 256), so batches of
+    varying composition (concatenated graphs of different sizes) reuse a few
+    workspaces instead of allocating one per distinct n."""
+    if n <= 2048:
+        return max(256, -(-n // 256) * 256)
+    q = 1 << (n.bit_length() - 4)
+    return -(-n // q) * q
+
+
 class TrainWorkspace:
-    """Forward saves + backward buffers + weight-gradient slabs for one shape."""
+    """Forward saves + backward buffers + weight-gradient slabs for up to n
+    particles (`activate(n)` selects the batch size within the capacity)."""
 
     def __init__(self, epd: nn.Module, n: int, T: int, dim: int, K: int, loop: bool,
                  device: torch.device, nslab: int = DEFAULT_NSLAB):
@@ -230,6 +242,7 @@ class TrainWorkspace:
         H, nl = epd.latent_dim, epd.nlayers
         self.nlin = epd.nmlp_layers + 1
         self.H, self.L, self.n, self.T, self.dim, self.nslab = H, nl, n, T, dim, nslab
+        self.n_cap = n
         self.nslab_of = nslab_table(nslab)
         self.feat = epd.nnode_in
         self.f = engine.StepWorkspace(n, T, dim, H, K, loop, device)
@@ -281,6 +294,14 @@ class TrainWorkspace:
         self.scratch = e(max(1, sc(_hip.SLAB_EDGE, cap), sc(_hip.SLAB_ENC_EDGE, cap),
                              sc(_hip.SLAB_NODE, n), sc(_hip.SLAB_UV, n)))
         self._descs_key = None
+
+    def activate(self, n: int) -> "TrainWorkspace":
+        """Run the next step on n <= n_cap particles (every kernel reads the
+        edge count from rowptr[n]; buffers are sized for the capacity)."""
+        if not 0 < n <= self.n_cap:
+            raise ValueError(f"batch of {n} particles does not fit a workspace of {self.n_cap}")
+        self.n = self.f.n = n
+        return self
 
     def slab(self, kind: int, k: int = 0) -> int:
         return self.slabs.ptr(kind, k)
