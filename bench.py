@@ -292,10 +292,11 @@ def bench_train(args, world, rank, device):
     E = tw.f.num_edges()
     loss = float(out["loss"])
     kstats = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in timers.items()}
-    # dominant kernel by total time: the edge-layer backward: W2^T dy, dW2 += dy h^T,
-    # dW1e += dh e0^T (+ W1e^T dh when dE0 is accumulated in-layer, H = 128)
+    # dominant kernel by total time: the edge-layer backward: W2^T dy, dW2 += dy h^T
+    # (H = 64: dE0 and dW1e of all layers are formed afterwards by
+    # k_edge_latent_grad; H = 128 adds W1e^T dh and dW1e += dh e0^T in-layer)
     dom = "k_edge_bwd"
-    flops_bwd = E * (6 if tw.latent_pass else 8) * H * H
+    flops_bwd = E * (4 if tw.latent_pass else 8) * H * H
     achieved = flops_bwd / kstats[dom]
     prof = profiled_traffic(args.workload, "train", dom)
     res = {

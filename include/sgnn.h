@@ -295,11 +295,16 @@ int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t*
 /* dE0 = sum_k scales[k] W1e_k^T dh_k (edge_fns[k].w1 columns 2H..3H) over
  * nlayers layers that share one encoded edge latent, from each layer's dh
  * rows [E][H] (the dh_rows output of sgnn_edge_layer_bwd, one buffer per
- * layer).  With it, sgnn_edge_layer_bwd is called with de0t = NULL (H = 64).
+ * layer), plus each layer's dW1e = sum_e dh_k (x) e0 into the dW1e block of
+ * its SLAB_EDGE slabs (slabs[k], nslab workgroups, the same arena
+ * sgnn_edge_layer_bwd wrote; the 2^k factor is applied by the slab
+ * reduction as for the in-layer product).  With it, sgnn_edge_layer_bwd is
+ * called with de0t = NULL (H = 64, nlayers <= 9) and skips both products.
  * Writes de0t in the tiled layout of e0. */
 int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp* edge_fns,
                           const float* scales, int32_t nlayers, const int32_t* rowptr, int64_t n,
-                          int64_t edge_cap, float* de0t, void* stream);
+                          int64_t edge_cap, const float* e0t, float* de0t, float* const* slabs,
+                          int32_t nslab, void* stream);
 int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, const float* cout,
                 const int32_t* rowptr, const float* dh_rows, const int32_t* tptr,
                 const int32_t* tperm, const float* x_in, int64_t n, const sgnn_mlp* edge_fn,

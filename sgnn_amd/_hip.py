@@ -125,7 +125,7 @@ SIGNATURES = {
                                              c_void_p, c_void_p, c_float, c_float, P_SAVES,
                                              P_MLP, c_void_p, c_int32, c_void_p]),
     "sgnn_edge_latent_grad": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64,
-                                             c_int64, c_void_p, c_void_p]),
+                                             c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "sgnn_embedding_grad": (ctypes.c_int, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32,
                                            c_int32, c_void_p, c_int32, c_void_p]),
     "sgnn_encode_edges_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_float,

@@ -318,9 +318,11 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
     stage_matrix_t(p, ldh, a.wl, H, H, H, H, H);
     WlT = p;
     p += H * ldh;
-    stage_matrix_t(p, ldh, a.we, 3 * H, H, H, H, H);
-    WeT = p;
-    p += H * ldh;
+    if (a.de0t) {  // only the in-layer dE0 product needs W1e^T (the host sizes LDS to match)
+      stage_matrix_t(p, ldh, a.we, 3 * H, H, H, H, H);
+      WeT = p;
+      p += H * ldh;
+    }
     if (NL == 3) {
       stage_matrix_t(p, ldh, a.wm, H, H, H, H, H);
       WmT = p;
@@ -396,23 +398,29 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
       }
       store_tiled<TH>(dtile, de);
     }
+    // de0t == NULL: sgnn_edge_latent_grad forms dE0 and dW1e of this layer
+    const bool w1e_here = a.de0t != nullptr;
     if (nvalid > 0) {
       if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
-      load_tiled<TH>(e0, a.e0t + tile * (32 * H));
-      zero_if<TH>(e0, !valid);
+      if (w1e_here) {
+        load_tiled<TH>(e0, a.e0t + tile * (32 * H));
+        zero_if<TH>(e0, !valid);
+      }
     }
     lds_store_items<TH>(im.sA, ldh, j, dh);
-    lds_store_items<TH>(im.sB, ldh, j, e0);
+    if (w1e_here) lds_store_items<TH>(im.sB, ldh, j, e0);
     wave_lds_sync();
     if (nvalid > 0)
       segment_sum_store<TH>(im.sA, ldh, rv, nvalid, base, tile, prv, nxt, a.du, a.cin, a.cout);
-    __syncthreads();
-    outer_tiles<NT>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1e = sum dh (x) e0
-    __syncthreads();
+    if (w1e_here) {
+      __syncthreads();
+      outer_tiles<NT>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1e = sum dh (x) e0
+      __syncthreads();
+    }
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
   store_outer<NT>(slab, H, TH, TH, acc_wl);
-  store_outer<NT>(slab + H * H, H, TH, TH, acc_w1);
+  if (a.de0t) store_outer<NT>(slab + H * H, H, TH, TH, acc_w1);
   if (NL == 3) store_outer<NT>(slab + 2 * H * H, H, TH, TH, acc_wm);
   float* v = slab + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, NL);
   store_lane_vec<TH>(v, s_dbl);
@@ -1649,7 +1657,7 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
                       nslab, stream);
     return check_launch("edge_layer_bwd");
   }
-  const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin);
+  const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin) - (de0t ? 0 : 4 * (size_t)H * (H + 4));
   SGNN_BWD_DISPATCH(H, edge_fn->nlin, (launch_bwd(k_edge_bwd<TH_, NL_>, nslab, lds, stream, a)));
   return check_launch("edge_layer_bwd");
 }
@@ -1898,73 +1906,138 @@ extern "C" int sgnn_embedding_grad(const float* G, int32_t ntypes, int32_t hidde
 // one streaming pass over the edges after the layer backwards, instead of a
 // read-modify-write of dE0 inside every layer's edge backward.
 namespace {
-constexpr int kMaxLatentLayers = 16;
+constexpr int kMaxLatentLayers = 9;
 struct EdgeLatentGradArgs {
   const float* dh[kMaxLatentLayers];   // [E][H] rows per layer
   const float* we[kMaxLatentLayers];   // edge W1 + 2H per layer (ld 3H)
+  float* slab[kMaxLatentLayers];       // SLAB_EDGE slab arena of each layer
   float scale[kMaxLatentLayers];
   int nlayers;
   const int32_t* rowptr;
   int64_t n;
+  const float* e0t;
   float* de0t;
+  int64_t slab_stride;
 };
 
-// dE0 = sum_k (2^k W1e_k^T) dh_k per edge tile, the scaled transposed
-// images of every layer staged in LDS once per workgroup; the next layer's dh
-// rows are prefetched under the current layer's MFMAs.  (Measured: the same
-// kernel with the images in L2 and full occupancy is not faster.)
-template <int TH>
+// One pass over the edges after the layer backwards (H = 64), per 128-edge
+// chunk: e0 (loaded once) as an LDS item image, then for every layer k the
+// dh_k rows (next layer's prefetched under this one's MFMAs):
+//   dE0  += (2^k W1e_k^T) dh_k                (register MFMAs)
+//   dW1e_k += sum_items dh_k (x) e0           (LDS images, items as k;
+//                                              2^k applied in the slab reduction)
+// The W1e_k^T images sit in LDS for L <= 5 (GW = false), else are read from L2.
+template <int TH, int L, bool GW>
 __global__ __launch_bounds__(kBlock) void k_edge_latent_grad(EdgeLatentGradArgs a) {
   constexpr int H = 32 * TH, ldh = H + 4;
+  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   extern __shared__ float lds[];
-  for (int k = 0; k < a.nlayers; ++k)
-    stage_matrix_t(lds + k * H * ldh, ldh, a.we[k], 3 * H, H, H, H, H, a.scale[k]);
-  __syncthreads();
-  const int w = threadIdx.x >> 6, j = lane_id() & 31;
-  const int64_t E = a.rowptr[a.n];
-  const int64_t ntiles = (E + 31) / 32;
-  const int64_t nw = (int64_t)gridDim.x * kWaves;
-  for (int64_t tile = (int64_t)blockIdx.x * kWaves + w; tile < ntiles; tile += nw) {
-    const int64_t e = tile * 32 + j;
-    const int64_t ec = e < E ? e : E - 1;
-    f32x16 de[TH], cur[TH], nxt[TH];
-    zero<TH>(de);
-    load_row_clayout<TH>(cur, a.dh[0] + ec * H);
-    for (int k = 0; k < a.nlayers; ++k) {
-      if (k + 1 < a.nlayers) load_row_clayout<TH>(nxt, a.dh[k + 1] + ec * H);  // prefetch
-      zero_if<TH>(cur, e >= E);
-      mfma_from_acc<TH, TH>(de, lds + k * H * ldh, ldh, 0, cur);
+  float* bufA = lds;                  // dh_k item image
+  float* bufB = bufA + kChunk * ldh;  // e0 item image
+  float* wimg = bufB + kChunk * ldh;  // 2^k W1e_k^T (GW = false)
+  if constexpr (!GW) {
 #pragma unroll
-      for (int t = 0; t < TH; ++t) cur[t] = nxt[t];
-    }
-    store_tiled<TH>(a.de0t + tile * (32 * H), de);
+    for (int k = 0; k < L; ++k) stage_matrix_t(wimg + k * H * ldh, ldh, a.we[k], 3 * H, H, H, H, H, a.scale[k]);
   }
+  __syncthreads();
+  const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
+  const int w = threadIdx.x >> 6, j = im.j;
+  f32x16 acc[L][NT];
+#pragma unroll
+  for (int k = 0; k < L; ++k) zero_acc<NT>(acc[k]);
+  const int64_t E = a.rowptr[a.n];
+  const int64_t nchunks = (E + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+    const int nvalid = clamp_items(E - base);
+    const bool valid = e < E;
+    const int64_t ec = valid ? e : E - 1;
+    f32x16 de[TH], cur[TH], nxt[TH], e0[TH];
+    zero<TH>(de);
+    zero<TH>(e0);
+    zero<TH>(cur);
+    if (nvalid > 0) {  // tiles past the last valid one are not allocated
+      load_tiled<TH>(e0, a.e0t + tile * (32 * H));
+      load_row_clayout<TH>(cur, a.dh[0] + ec * H);
+    }
+    zero_if<TH>(e0, !valid);
+    lds_store_items<TH>(im.sB, ldh, j, e0);
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      if (k + 1 < L && nvalid > 0) load_row_clayout<TH>(nxt, a.dh[k + 1] + ec * H);  // prefetch
+      zero_if<TH>(cur, !valid);
+      lds_store_items<TH>(im.sA, ldh, j, cur);
+      if constexpr (GW) {
+#pragma unroll
+        for (int t = 0; t < TH; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cur[t][r] *= a.scale[k];   // 2^k: exact
+        matvec_t<TH, TH, true>(de, a.we[k], 3 * H, cur);
+      } else {
+        mfma_from_acc<TH, TH>(de, wimg + k * H * ldh, ldh, 0, cur);
+      }
+      __syncthreads();
+      outer_tiles<NT>(acc[k], TH, TH, bufA, ldh, 0, bufB, ldh, 0);
+      __syncthreads();
+      if (k + 1 < L) {
+#pragma unroll
+        for (int t = 0; t < TH; ++t) cur[t] = nvalid > 0 ? nxt[t] : cur[t];
+      }
+    }
+    if (nvalid > 0) store_tiled<TH>(a.de0t + tile * (32 * H), de);
+  }
+#pragma unroll
+  for (int k = 0; k < L; ++k)
+    store_outer<NT>(a.slab[k] + blockIdx.x * a.slab_stride + H * H, H, TH, TH, acc[k]);
+}
+
+template <int L>
+void launch_latent(const EdgeLatentGradArgs& a, int nslab, void* stream) {
+  constexpr int H = 64, ldh = H + 4;
+  constexpr bool GW = L > 5;
+  const size_t lds = 4 * (size_t)(2 * kChunk * ldh + (GW ? 0 : L * H * ldh));
+  launch_bwd(k_edge_latent_grad<2, L, GW>, nslab, lds, stream, a);
 }
 }  // namespace
 
 extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp* edge_fns,
                                      const float* scales, int32_t nlayers, const int32_t* rowptr,
-                                     int64_t n, int64_t edge_cap, float* de0t, void* stream) {
+                                     int64_t n, int64_t edge_cap, const float* e0t, float* de0t,
+                                     float* const* slabs, int32_t nslab, void* stream) {
   using namespace sgnn;
-  if (!dh_rows || !edge_fns || !scales || !rowptr || !de0t || nlayers < 1 || n <= 0 || edge_cap < 1)
+  if (!dh_rows || !edge_fns || !scales || !rowptr || !e0t || !de0t || !slabs || nslab < 1 ||
+      nlayers < 1 || n <= 0 || edge_cap < 1)
     return set_error(SGNN_ERR_INVALID, "edge_latent_grad: bad arguments");
   const int H = edge_fns[0].hidden;
   if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "edge_latent_grad: hidden 64 only (128 accumulates in-layer)");
-  if (nlayers > 9) return set_error(SGNN_ERR_UNSUPPORTED, "edge_latent_grad: at most 9 layers share an edge latent");
+  if (nlayers > kMaxLatentLayers)
+    return set_error(SGNN_ERR_UNSUPPORTED, "edge_latent_grad: at most 9 layers share an edge latent");
   EdgeLatentGradArgs a{};
   for (int k = 0; k < nlayers; ++k) {
-    if (!dh_rows[k] || !edge_fns[k].w1 || edge_fns[k].hidden != H)
+    if (!dh_rows[k] || !edge_fns[k].w1 || edge_fns[k].hidden != H || !slabs[k] ||
+        edge_fns[k].nlin != edge_fns[0].nlin)
       return set_error(SGNN_ERR_INVALID, "edge_latent_grad: layer arguments");
     a.dh[k] = dh_rows[k];
     a.we[k] = edge_fns[k].w1 + 2 * H;
+    a.slab[k] = slabs[k];
     a.scale[k] = scales[k];
   }
   a.nlayers = nlayers;
   a.rowptr = rowptr;
   a.n = n;
+  a.e0t = e0t;
   a.de0t = de0t;
-  const size_t lds = 4 * (size_t)nlayers * H * (H + 4);
-  const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 2);
-  launch_bwd(k_edge_latent_grad<2>, (int)grid, lds, stream, a);
+  a.slab_stride = sgnn_bwd_slab_floats(SGNN_SLAB_EDGE, H, 0, edge_fns[0].nlin);
+  switch (nlayers) {
+    case 1: launch_latent<1>(a, nslab, stream); break;
+    case 2: launch_latent<2>(a, nslab, stream); break;
+    case 3: launch_latent<3>(a, nslab, stream); break;
+    case 4: launch_latent<4>(a, nslab, stream); break;
+    case 5: launch_latent<5>(a, nslab, stream); break;
+    case 6: launch_latent<6>(a, nslab, stream); break;
+    case 7: launch_latent<7>(a, nslab, stream); break;
+    case 8: launch_latent<8>(a, nslab, stream); break;
+    default: launch_latent<9>(a, nslab, stream); break;
+  }
   return check_launch("edge_latent_grad");
 }

@@ -476,8 +476,10 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                             tw.scratch.data_ptr(), s),
               "sgnn_uv_bwd")
     if tw.latent_pass:
+        slabs = (ctypes.c_void_p * tw.L)(*[tw.slab(_hip.SLAB_EDGE, k) for k in range(tw.L)])
         check(L.sgnn_edge_latent_grad(tw._dh_ptrs, ctypes.byref(pk.edge_arr), tw._scales, tw.L,
-                                      ws.rowptr.data_ptr(), n, ws.edge_cap, tw.de0t.data_ptr(), s),
+                                      ws.rowptr.data_ptr(), n, ws.edge_cap, ws.e0t.data_ptr(),
+                                      tw.de0t.data_ptr(), slabs, tw.nslab_of[_hip.SLAB_EDGE], s),
               "sgnn_edge_latent_grad")
     ty, ew, ed, ue = emb_args(inp, emb_weight)
     check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, ty, ew, ed,

@@ -121,15 +121,19 @@ def test_gradients_against_oracle_autograd(nx, ny, radius, n_ex):
     print(f"{nx}x{ny} r={radius}: worst relative grad error {worst:.3e}")
 
 
-@pytest.mark.parametrize("dim,H,nmlp", [(2, 64, 2), (2, 128, 1), (3, 128, 2)])
-def test_wide_and_deep_mlp_gradients_against_oracle(dim, H, nmlp):
+@pytest.mark.parametrize("dim,H,nmlp,L", [(2, 64, 2, 3), (2, 128, 1, 3), (3, 128, 2, 3), (2, 64, 1, 7)])
+def test_wide_and_deep_mlp_gradients_against_oracle(dim, H, nmlp, L):
     """H = 128 (weights read from L2) and nmlp_layers = 2 (3-Linear MLPs, middle
-    Linear backward) through the fused backward, vs oracle autograd."""
+    Linear backward) through the fused backward, vs oracle autograd; L = 7 at
+    H = 64 takes the latent pass with the W1e images read from L2."""
     from oracle import sgnn_oracle as O
     from sgnn_amd import synthetic
     from sgnn_amd.learned_simulator import LearnedSimulator
     from sgnn_amd.train import Trainer
-    T, L, R = 6, 3, 0.75
+    T, R = 6, 0.75
+    # at depth 7 the fp32 oracle's own gradient error is 1.2e-3 of max|g|
+    # (measured against the same oracle in float64; the HIP path is 3.3e-4 from it)
+    rel = 5e-4 if L <= 5 else 2e-3
     base = synthetic.lattice_2d(30, 20) if dim == 2 else synthetic.lattice_3d(10, 8, 6)
     seq = synthetic.trajectory(base, T + 1, seed=5)
     n = seq.shape[0]
@@ -153,8 +157,8 @@ def test_wide_and_deep_mlp_gradients_against_oracle(dim, H, nmlp):
     worst = 0.0
     for k, p in sim.named_parameters():
         if state[k].grad is not None:
-            worst = max(worst, _grad_close(p.grad.cpu().numpy(), state[k].grad.numpy(), k, rel=5e-4))
-    print(f"dim={dim} H={H} nmlp={nmlp}: worst relative grad error {worst:.3e}")
+            worst = max(worst, _grad_close(p.grad.cpu().numpy(), state[k].grad.numpy(), k, rel=rel))
+    print(f"dim={dim} H={H} nmlp={nmlp} L={L}: worst relative grad error {worst:.3e}")
 
 
 def test_trainer_with_particle_types_matches_reference():
