@@ -345,12 +345,43 @@ SGNN_DEV void lds_store_items(float* img, int ld, int item, const f32x16 (&x)[TH
 // Outer-product accumulation over items from two LDS images [item][unit]:
 //   acc[u][v] += sum_{item < nitems} A[item][ua + u] * B[item][vb + v]
 // for one 32x32 output tile (u, v in 0..31): MFMA with the items as k.
+// NITEMS is a compile-time multiple of 32: the LDS operands are read in
+// batches of G k-steps one batch ahead of the MFMAs that consume them (the
+// compiler's own schedule waited on every read pair: LDS latency per MFMA).
+template <int NITEMS>
 SGNN_DEV void mfma_outer(f32x16& acc, const float* A, int lda, int ua, const float* B, int ldb,
-                         int vb, int nitems) {
+                         int vb) {
+  static_assert(NITEMS % 32 == 0, "items per outer product: multiple of 32");
+  constexpr int G = 8, NS = NITEMS / 2;   // k-steps per batch, k-steps
   const int l = lane_id() & 31, h = lane_id() >> 5;
-  for (int s = 0; s < nitems; s += 2) {
-    const int it = s + h;
-    acc = mfma32(A[it * lda + ua + l], B[it * ldb + vb + l], acc);
+  const float* pa = A + h * lda + ua + l;
+  const float* pb = B + h * ldb + vb + l;
+  float a0[G], b0[G], a1[G], b1[G];
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    a0[i] = pa[2 * i * lda];
+    b0[i] = pb[2 * i * ldb];
+  }
+#pragma unroll
+  for (int s = 0; s < NS; s += 2 * G) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      a1[i] = pa[2 * (s + G + i) * lda];
+      b1[i] = pb[2 * (s + G + i) * ldb];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs
+#pragma unroll
+    for (int i = 0; i < G; ++i) acc = mfma32(a0[i], b0[i], acc);
+    if (s + 2 * G < NS) {
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        a0[i] = pa[2 * (s + 2 * G + i) * lda];
+        b0[i] = pb[2 * (s + 2 * G + i) * ldb];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < G; ++i) acc = mfma32(a1[i], b1[i], acc);
   }
 }
 

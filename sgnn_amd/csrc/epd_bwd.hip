@@ -103,7 +103,7 @@ SGNN_DEV void outer_tiles(f32x16 (&acc)[NT], int TU, int TV, const float* A, int
     const int tile = w + kWaves * q;
     if (tile < TU * TV) {
       const int tu = tile / TV, tv = tile - tu * TV;
-      mfma_outer(acc[q], A, lda, abase + 32 * tu, B, ldb, bbase + 32 * tv, kChunk);
+      mfma_outer<kChunk>(acc[q], A, lda, abase + 32 * tu, B, ldb, bbase + 32 * tv);
     }
   }
 }
