@@ -257,23 +257,24 @@ struct EdgeLayerArgs {
 
 template <int TH, bool TRAIN, int NL>
 __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
+  // W1e always sits in LDS (67.6 KB at H = 128, next to the per-wave sum
+  // buffers); the last (and middle) Linear is an LDS image at H = 64 and
+  // read from L2 at H = 128.
   constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4;            // ldh: LDS image leading dim
-  constexpr int lde = GW ? 3 * H : ldh, ldw2 = GW ? H : ldh;
+  constexpr int ldw2 = GW ? H : ldh;
   extern __shared__ float lds[];
   float* sW = lds;
-  const float* We = GW ? a.we : sW;
+  const float* We = sW;
   const float* W2 = GW ? a.w2 : sW + H * ldh;
-  float* b2 = GW ? sW : sW + 2 * H * ldh;
+  float* b2 = sW + (GW ? 1 : 2) * H * ldh;
   float* g = b2 + H;
   float* bb = g + H;
   float* bm = bb + H;
   float* mbuf = bm + (NL == 3 ? H : 0);  // per wave [32][ldh]
   if (NL == 3) stage_vec(bm, a.bm, H, H);
-  if (!GW) {
-    stage_matrix(sW, ldh, a.we, 3 * H, H, H, H, H);
-    stage_matrix(sW + H * ldh, ldh, a.w2, H, H, H, H, H);
-  }
+  stage_matrix(sW, ldh, a.we, 3 * H, H, H, H, H);
+  if (!GW) stage_matrix(sW + H * ldh, ldh, a.w2, H, H, H, H, H);
   stage_vec(b2, a.b2, H, H);
   stage_vec(g, a.g, H, H);
   stage_vec(bb, a.bb, H, H);
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     const float* src = a.e0t + tile * (32 * H) + l * 4;
 #pragma unroll
     for (int q = 0; q < TH * 4; ++q) xg[q] = ld4(src + q * 256);
-    mfma_from_groups<TH, TH, GW>(hacc, We, lde, 0, xg, a.e_scale);
+    mfma_from_groups<TH, TH, false>(hacc, We, ldh, 0, xg, a.e_scale);
     acc_relu<TH>(hacc);
     if (TRAIN) store_tiled<TH>(a.sv.h + tile * (32 * H), hacc);
     f32x16 y[TH], h2[TH];
@@ -664,8 +665,8 @@ extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t,
     if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "edge_layer: saves");
     a.sv = *saves;
   }
-  const size_t lds = sizeof(float) * (size_t)((H == 64 ? 2 * H * (H + 4) : 0) + 4 * H + kWaves * 32 * (H + 4));
-  const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, 2);
+  const size_t lds = sizeof(float) * (size_t)((H == 64 ? 2 : 1) * H * (H + 4) + 4 * H + kWaves * 32 * (H + 4));
+  const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, H == 64 ? 2 : 1);  // workgroups per CU LDS allows
   hipStream_t s = static_cast<hipStream_t>(stream);
   SGNN_DISPATCH_H_NL(H, edge_fn->nlin, (go_edge_layer<TH_, NL_>(train, grid, lds, s, a)));
   return check_launch("edge_layer");

@@ -1,4 +1,8 @@
 set -e
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU --output-format csv -d gpurun_out/pmc_c2 -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-steps 0 --no-rollout-extras > /dev/null 2> gpurun_out/pmc.err
-echo pmc done
+timeout -k 10 600 python -m pytest tests -q -x -m gpu > gpurun_out/t.log 2>&1 || { grep -E "Error|assert" gpurun_out/t.log | head; tail -3 gpurun_out/t.log; exit 1; }
+tail -1 gpurun_out/t.log
+timeout -k 10 300 python bench.py --mode rollout --workload c4 --steps 10 --warmup 2 --cpu-steps 0 > gpurun_out/c4.json 2>gpurun_out/c4.err
+python -c "import json;d=json.load(open('gpurun_out/c4.json'));print(d['ms_per_step'], d['value'], d['roofline']['avg_launch_us'], d['roofline']['frac'])"
+timeout -k 10 600 python bench.py --mode ms-train --workload c5_small --steps 5 --warmup 2 --cpu-steps 0 > gpurun_out/c5s.json 2>gpurun_out/c5s.err
+python -c "import json;d=json.load(open('gpurun_out/c5s.json'));print(d['ms_per_step'], d['value'])"
