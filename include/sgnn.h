@@ -331,6 +331,16 @@ int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_strid
                           const sgnn_mlp* enc, float* slab, int32_t nslab, float* scratch,
                           int64_t edge_cap, void* stream);
 
+/* Random-walk training noise (noise_utils.py:4-39) and the noisy window
+ * (learned_simulator.py:467) in one pass: velocity increments
+ * N(0, (std_last/sqrt(T-1))^2) from a Philox4x32-10 stream keyed by
+ * (seed, offset), cumsum twice, noise[n][T][dim] with noise[:,0] = 0,
+ * noisy = pos_seq + noise.  The distribution of the reference's CPU-generator
+ * draw, not its bit stream. */
+int sgnn_random_walk_noise(const float* pos_seq, int64_t n, int32_t T, int32_t dim,
+                           float noise_std_last_step, uint64_t seed, uint64_t offset, float* noise,
+                           float* noisy, void* stream);
+
 /* Fused Adam over a flat fp32 buffer; same update as torch.optim.Adam
  * (amsgrad=False, weight_decay=0) used by train.py:199,271-273. step >= 1. */
 int sgnn_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,

@@ -135,6 +135,8 @@ SIGNATURES = {
                                               c_void_p, c_void_p]),
     "sgnn_rollout": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                     c_void_p, c_void_p]),
+    "sgnn_random_walk_noise": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_float, ctypes.c_uint64,
+                                              ctypes.c_uint64, c_void_p, c_void_p, c_void_p]),
     "sgnn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,
                                       c_float, c_float, c_float, c_int64, c_void_p]),
 }

@@ -24,6 +24,26 @@ import torch.distributed as dist
 from . import engine, training
 
 
+def device_random_walk_noise(position_sequence: torch.Tensor, noise_std_last_step: float,
+                             seed: Optional[int] = None, offset: int = 0):
+    """(noise, noisy window) from one HIP pass (sgnn_random_walk_noise): the
+    distribution of noise_utils.py:4-39 on a Philox stream; `seed` defaults to
+    a draw from torch's CPU generator, so torch.manual_seed fixes it."""
+    from ._hip import check, lib, require_gpu_tensor, stream_ptr
+    pos = position_sequence
+    require_gpu_tensor(pos, "position_sequence")
+    if pos.dtype != torch.float32 or not pos.is_contiguous():
+        pos = pos.to(torch.float32).contiguous()
+    n, T, d = pos.shape
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    noise, noisy = torch.empty_like(pos), torch.empty_like(pos)
+    check(lib().sgnn_random_walk_noise(pos.data_ptr(), n, T, d, float(noise_std_last_step),
+                                       seed & (2 ** 64 - 1), offset & (2 ** 64 - 1), noise.data_ptr(),
+                                       noisy.data_ptr(), stream_ptr(pos.device)), "sgnn_random_walk_noise")
+    return noise, noisy
+
+
 def random_walk_noise(position_sequence: torch.Tensor, noise_std_last_step: float,
                       generator: Optional[torch.Generator] = None) -> torch.Tensor:
     """noise_utils.py:4-39 on the tensor's device (the reference draws on the CPU
@@ -100,10 +120,11 @@ class Trainer:
         """One optimisation step on this rank's graphs; returns device-side loss
         terms (no host sync).  `noise` defaults to fresh random-walk noise."""
         pos = position.to(torch.float32).contiguous()
-        if noise is None:
-            noise = random_walk_noise(pos, self.noise_std)
-        noise = noise.to(pos.device, torch.float32).contiguous()
-        noisy = (pos + noise).contiguous()                          # learned_simulator.py:467
+        if noise is None:       # fused: draw + cumsum twice + noisy window in one kernel
+            noise, noisy = device_random_walk_noise(pos, self.noise_std)
+        else:
+            noise = noise.to(pos.device, torch.float32).contiguous()
+            noisy = (pos + noise).contiguous()                      # learned_simulator.py:467
         inp, _ = self.sim._step_inputs(noisy, nparticles_per_example, particle_types)
         n, T, _ = noisy.shape
         tw = self.workspace(n, T, pos.device)
