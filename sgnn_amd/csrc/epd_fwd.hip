@@ -59,15 +59,16 @@ SGNN_DEV void store_uv(const float* Wi, const float* Wj, const float* b1e, int l
   if (valid) store_row_clayout<TH>(v_row, acc);
 }
 
-template <int TH, bool G = false>
+// GI / GJ: W1e_i / W1e_j read from L2 (buffer loads) instead of an LDS image.
+template <int TH, bool GI, bool GJ>
 SGNN_DEV void store_uv2(const float* Wi, int ldi, const float* Wj, int ldj, const float* b1e,
                         const f32x16 (&x)[TH], float* u_row, float* v_row, bool valid) {
   f32x16 acc[TH];
   acc_bias<TH>(acc, b1e);
-  mfma_from_acc<TH, TH, G>(acc, Wi, ldi, 0, x);
+  mfma_from_acc<TH, TH, GI>(acc, Wi, ldi, 0, x);
   if (valid) store_row_clayout<TH>(u_row, acc);
   acc_bias<TH>(acc, nullptr);
-  mfma_from_acc<TH, TH, G>(acc, Wj, ldj, 0, x);
+  mfma_from_acc<TH, TH, GJ>(acc, Wj, ldj, 0, x);
   if (valid) store_row_clayout<TH>(v_row, acc);
 }
 
@@ -385,14 +386,16 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
   constexpr int lda = GW ? (MODE == 0 ? 3 * H : H) : ldh;
   extern __shared__ float lds[];
   float* sW = lds;
-  // LDS: [W1 | W2 | Wa | Wb] for H = 64; only the padded decoder W2 for H = 128
+  // LDS: [W1 | W2 | Wa | decoder W2 (mode 1, 32 rows)] for H = 64 (70.5 / 79.2
+  // KB: two workgroups per CU); the next layer's W1e_j (mode 0) is read from L2
+  // at both widths.  H = 128: only the padded decoder W2.
   const float* W1 = GW ? a.w1 : sW;
   const float* W2 = GW ? a.w2 : sW + H * ld2;
   const float* Wa = GW ? (MODE == 0 ? a.we : a.wd1) : sW + H * ld2 + H * ldh;
-  float* sWb = GW ? sW : sW + H * ld2 + 2 * H * ldh;  // mode 0: W1e_j  mode 1: decoder W2 (32 rows)
-  const float* Wb = (GW && MODE == 0) ? a.we + H : sWb;
-  const int ldb = (GW && MODE == 0) ? 3 * H : ldh;
-  float* b1 = (GW && MODE == 0) ? sW : sWb + H * ldh;
+  float* sWb = GW ? sW : sW + H * ld2 + 2 * H * ldh;  // mode 1: decoder W2 (32 rows)
+  const float* Wb = MODE == 0 ? a.we + H : sWb;
+  const int ldb = MODE == 0 ? 3 * H : ldh;
+  float* b1 = MODE == 0 ? sWb : sWb + 32 * ldh;
   float* b2 = b1 + H;
   float* g = b2 + H;
   float* bb = g + H;
@@ -409,10 +412,7 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
     stage_matrix(sW + H * ld2, ldh, a.w2, H, H, H, H, H);
   }
   if (MODE == 0) {
-    if (!GW) {
-      stage_matrix(sW + H * ld2 + H * ldh, ldh, a.we, 3 * H, H, H, H, H);
-      stage_matrix(sWb, ldh, a.we + H, 3 * H, H, H, H, H);
-    }
+    if (!GW) stage_matrix(sW + H * ld2 + H * ldh, ldh, a.we, 3 * H, H, H, H, H);
     stage_vec(ba, a.be, H, H);
   } else {
     if (!GW) stage_matrix(sW + H * ld2 + H * ldh, ldh, a.wd1, H, H, H, H, H);
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
       for (int r = 0; r < 16; ++r) x[t][r] = y[t][r] + x[t][r];  // :176 residual
     if (valid && a.x_out) store_row_clayout<TH>(a.x_out + i * H, x);
     if (MODE == 0) {
-      store_uv2<TH, GW>(Wa, lda, Wb, ldb, ba, x, a.u + i * H, a.v + i * H, valid);
+      store_uv2<TH, GW, true>(Wa, lda, Wb, ldb, ba, x, a.u + i * H, a.v + i * H, valid);
     } else {
       f32x16 hd[TH];
       acc_bias<TH>(hd, ba);
@@ -693,9 +693,10 @@ static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode
     a.sv = *saves;
   }
   const size_t vec = 5 * H + 32 + 2 * H;
-  const size_t lds = sizeof(float) * (H == 64 ? H * (2 * H + 4) + 3 * H * (H + 4) + vec
-                                              : H * (H + 4) + vec);
-  const unsigned grid = persistent_grid(a.n, 32 * kWaves, H == 64 ? 1 : 2);
+  const size_t dec_w2 = mode == 1 ? 32 * (H + 4) : 0;  // padded decoder last Linear
+  const size_t lds = sizeof(float) * (H == 64 ? H * (2 * H + 4) + 2 * H * (H + 4) + dec_w2 + vec
+                                              : dec_w2 + vec);
+  const unsigned grid = persistent_grid(a.n, 32 * kWaves, 2);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (mode == 0) SGNN_DISPATCH_H_NL(H, node_fn->nlin, (go_node_layer<TH_, 0, NL_>(train, grid, lds, s, a)));
   else SGNN_DISPATCH_H_NL(H, node_fn->nlin, (go_node_layer<TH_, 1, NL_>(train, grid, lds, s, a)));

@@ -217,24 +217,29 @@ SGNN_DEV float dist2_ordered(const float* a, const float* b, int dim) {
   return s;
 }
 
-// Wave-aggregated atomic add of 1 per active lane to counter[key]: one atomic
-// per distinct key in the wave (coarse cells put a whole wave's particles in
-// one or two cells, where per-lane atomics serialise on one address).
+// Atomic add of 1 per active lane to counter[key], wave-aggregated where it
+// pays: coarse cells put a whole wave's particles in one or two cells, where
+// per-lane atomics serialise on one address, so a key shared by >= 4 lanes
+// takes one atomic for its group; once the leading group is small (fine cells:
+// ~1-2 particles per cell and wave-distinct keys) the remaining lanes issue
+// their own atomics in one instruction instead of one serial round trip per key.
 // Returns the lane's slot = old counter value + its rank among same-key lanes.
 SGNN_DEV int32_t wave_aggregated_inc(int32_t* counter, int32_t key, bool active) {
   const int lane = lane_id();
   uint64_t remaining = __ballot(active);
   int32_t slot = 0;
-  while (remaining) {
+  for (int it = 0; remaining && it < 4; ++it) {
     const int leader = __ffsll((unsigned long long)remaining) - 1;
     const int32_t lkey = __shfl(key, leader, 64);
     const uint64_t grp = __ballot(active && key == lkey) & remaining;
+    if (__popcll(grp) < 4) break;
     int32_t base = 0;
     if (lane == leader) base = atomicAdd(&counter[lkey], (int32_t)__popcll(grp));
     base = __shfl(base, leader, 64);
     if ((grp >> lane) & 1ull) slot = base + (int32_t)__popcll(grp & ((1ull << lane) - 1ull));
     remaining &= ~grp;
   }
+  if ((remaining >> lane) & 1ull) slot = atomicAdd(&counter[key], 1);
   return slot;
 }
 
