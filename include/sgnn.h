@@ -136,7 +136,8 @@ int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t dim, float r
  *   m_e  = LN(W2 relu(u[recv] + v[send] + e_scale * W1[:, 2H:3H] e0_e) + b2)
  *   agg_i = sum over edges e with recv == i of m_e   (aggr='add', :136)
  * e_scale = 2^k reproduces the edge-latent doubling (update returns the input
- * edge features, :176/:222).  agg rows whose edges straddle a 32-edge tile
+ * edge features, :176/:222); it is applied to the staged W1e (exact for a
+ * power of two, the only values the reference produces).  agg rows whose edges straddle a 32-edge tile
  * are left in cin/cout ([ceil(edge_cap/32)][H] each); sgnn_node_layer*
  * resolves them (deterministic, no atomics).
  * ------------------------------------------------------------------------- */

@@ -23,6 +23,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 SGNN_DEV int lane_id() { return threadIdx.x & 63; }
 
+// Wave index within the workgroup as a provably wave-uniform (SGPR) value:
+// tile / item bookkeeping derived from it stays on the scalar unit (scalar
+// loads of uniform indices, s_cbranch on uniform conditions) instead of 64-bit
+// VALU arithmetic and exec-mask branches (hipcc treats threadIdx.x >> 6 as
+// divergent).
+SGNN_DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 SGNN_DEV int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 SGNN_DEV f32x16 mfma32(float a, float b, f32x16 c) {
@@ -156,11 +163,46 @@ SGNN_DEV void acc_bias(f32x16 (&acc)[TH], const float* bias_lds) {
 }
 
 template <int TH>
+SGNN_DEV void zero_acc_regs(f32x16 (&acc)[TH]) {
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+}
+
+template <int TH>
 SGNN_DEV void acc_relu(f32x16 (&acc)[TH]) {
 #pragma unroll
   for (int t = 0; t < TH; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = fmaxf(acc[t][r], 0.0f);
+}
+
+// Row-wise sums of one item's 32*TH units (lane pair l, l^32): four
+// independent partial sums (short dependency chains), then the lane^32 half.
+template <int TH>
+SGNN_DEV float row_sum(const f32x16 (&x)[TH]) {
+  float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) p[r & 3] += x[t][r];
+  const float s = (p[0] + p[1]) + (p[2] + p[3]);
+  return s + wave_xor32(s);
+}
+
+template <int TH>
+SGNN_DEV float row_sum_sq_dev(const f32x16 (&x)[TH], float mean) {
+  float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float d = x[t][r] - mean;
+      p[r & 3] += d * d;
+    }
+  const float s = (p[0] + p[1]) + (p[2] + p[3]);
+  return s + wave_xor32(s);
 }
 
 // Row-wise LayerNorm over the 32*TH units of each item (one lane pair), eps
@@ -169,22 +211,8 @@ template <int TH>
 SGNN_DEV void acc_layernorm(f32x16 (&acc)[TH], const float* gamma_lds, const float* beta_lds) {
   const int h = lane_id() >> 5;
   constexpr float inv_n = 1.0f / (32.0f * TH);
-  float s = 0.0f;
-#pragma unroll
-  for (int t = 0; t < TH; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s += acc[t][r];
-  s += wave_xor32(s);
-  const float mean = s * inv_n;
-  float v = 0.0f;
-#pragma unroll
-  for (int t = 0; t < TH; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float d = acc[t][r] - mean;
-      v += d * d;
-    }
-  v += wave_xor32(v);
+  const float mean = row_sum<TH>(acc) * inv_n;
+  const float v = row_sum_sq_dev<TH>(acc, mean);
   const float rstd = 1.0f / sqrtf(v * inv_n + 1e-5f);
 #pragma unroll
   for (int t = 0; t < TH; ++t)
@@ -243,22 +271,8 @@ SGNN_DEV void acc_layernorm_save(f32x16 (&acc)[TH], const float* gamma_lds, cons
                                  f32x16 (&yhat)[TH], float& rstd_out) {
   const int h = lane_id() >> 5;
   constexpr float inv_n = 1.0f / (32.0f * TH);
-  float s = 0.0f;
-#pragma unroll
-  for (int t = 0; t < TH; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s += acc[t][r];
-  s += wave_xor32(s);
-  const float mean = s * inv_n;
-  float v = 0.0f;
-#pragma unroll
-  for (int t = 0; t < TH; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float d = acc[t][r] - mean;
-      v += d * d;
-    }
-  v += wave_xor32(v);
+  const float mean = row_sum<TH>(acc) * inv_n;
+  const float v = row_sum_sq_dev<TH>(acc, mean);
   const float rstd = 1.0f / sqrtf(v * inv_n + 1e-5f);
   rstd_out = rstd;
 #pragma unroll
@@ -279,16 +293,18 @@ SGNN_DEV void acc_layernorm_bwd(const f32x16 (&dout)[TH], const f32x16 (&yhat)[T
                                 const float* gamma_lds, f32x16 (&dy)[TH]) {
   const int h = lane_id() >> 5;
   constexpr float inv_n = 1.0f / (32.0f * TH);
-  float s1 = 0.0f, s2 = 0.0f;
+  float p1[4] = {0.0f, 0.0f, 0.0f, 0.0f}, p2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int t = 0; t < TH; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float g = dout[t][r] * gamma_lds[32 * t + crow(r, h)];
       dy[t][r] = g;
-      s1 += g;
-      s2 += g * yhat[t][r];
+      p1[r & 3] += g;
+      p2[r & 3] += g * yhat[t][r];
     }
+  float s1 = (p1[0] + p1[1]) + (p1[2] + p1[3]);
+  float s2 = (p2[0] + p2[1]) + (p2[2] + p2[3]);
   s1 += wave_xor32(s1);
   s2 += wave_xor32(s2);
   const float m1 = s1 * inv_n, m2 = s2 * inv_n;

@@ -97,7 +97,7 @@ SGNN_DEV void load_resolved(f32x16 (&a)[TH], const float* rows, const float* cin
 template <int NT>
 SGNN_DEV void outer_tiles(f32x16 (&acc)[NT], int TU, int TV, const float* A, int lda, int abase,
                           const float* B, int ldb, int bbase) {
-  const int w = threadIdx.x >> 6;
+  const int w = wave_id();
 #pragma unroll
   for (int q = 0; q < NT; ++q) {
     const int tile = w + kWaves * q;
@@ -110,7 +110,7 @@ SGNN_DEV void outer_tiles(f32x16 (&acc)[NT], int TU, int TV, const float* A, int
 
 template <int NT>
 SGNN_DEV void store_outer(float* dst, int ld, int TU, int TV, const f32x16 (&acc)[NT]) {
-  const int w = threadIdx.x >> 6;
+  const int w = wave_id();
 #pragma unroll
   for (int q = 0; q < NT; ++q) {
     const int tile = w + kWaves * q;
@@ -134,7 +134,7 @@ template <int TH>
 SGNN_DEV void store_lane_vec(float* dst, const float (&acc)[TH / 2 > 0 ? TH / 2 : 1]) {
   constexpr int H = 32 * TH;
   constexpr int UPL = H / 64 > 0 ? H / 64 : 1;
-  const int w = threadIdx.x >> 6, l = lane_id();
+  const int w = wave_id(), l = lane_id();
 #pragma unroll
   for (int q = 0; q < UPL; ++q)
     if (l + 64 * q < H) dst[w * H + l + 64 * q] = acc[q];
@@ -187,7 +187,7 @@ struct Imgs {
 };
 
 SGNN_DEV Imgs make_imgs(float* bufA, int lda, float* bufB, int ldb) {
-  const int w = threadIdx.x >> 6;
+  const int w = wave_id();
   return Imgs{bufA, bufB, bufA + w * 32 * lda, bufB + w * 32 * ldb, lda, ldb, lane_id() & 31};
 }
 
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
   const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
-  const int j = im.j, w = threadIdx.x >> 6;
+  const int j = im.j, w = wave_id();
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   f32x16 acc_wl[NT], acc_wm[NT], acc_w1[NT];
   zero_acc<NT>(acc_wl);
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(kBlock) void k_node_bwd(NodeBwdArgs a) {
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
   const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
-  const int j = im.j, w = threadIdx.x >> 6;
+  const int j = im.j, w = wave_id();
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   f32x16 acc_wl[NT], acc_wm[NT], acc_w1a[NT], acc_w1x[NT];
   zero_acc<NT>(acc_wl);
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(kBlock) void k_uv_bwd(UvBwdArgs a) {
   float* bufB = bufA + kChunk * ldh;
   __syncthreads();
   const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
-  const int j = im.j, w = threadIdx.x >> 6;
+  const int j = im.j, w = wave_id();
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   f32x16 acc_i[NT], acc_j[NT];
   zero_acc<NT>(acc_i);
@@ -669,7 +669,7 @@ __global__ __launch_bounds__(kBlock) void k_dec_bwd(DecBwdArgs a) {
   float* bufB = bufA + kChunk * ldh;
   __syncthreads();
   const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
-  const int l = lane_id(), j = im.j, h = l >> 5, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = im.j, h = l >> 5, w = wave_id();
   constexpr int NT2 = (TH + kWaves - 1) / kWaves;     // [32 x H] last layer
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   f32x16 acc_wl[NT2], acc_wm[NT], acc_w1[NT];
@@ -824,7 +824,7 @@ __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
   const Imgs im = make_imgs(bufA, ldh, bufB, ldb);
-  const int l = lane_id(), j = im.j, h = l >> 5, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = im.j, h = l >> 5, w = wave_id();
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   constexpr int NT1 = (TH * TKF + kWaves - 1) / kWaves;
   constexpr int NTG = (TH + kWaves - 1) / kWaves;
@@ -957,7 +957,7 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
   const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
-  const int l = lane_id(), j = im.j, h = l >> 5, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = im.j, h = l >> 5, w = wave_id();
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   constexpr int NT1 = (TH + kWaves - 1) / kWaves;
   f32x16 acc_wl[NT], acc_wm[NT], acc_w1[NT1];
@@ -1101,7 +1101,7 @@ __global__ __launch_bounds__(kBlock) void k_wgrad(WgradOp op) {
   extern __shared__ float lds[];
   float* imA = lds;
   float* imB = imA + kChunk * lda;
-  const int l = lane_id(), w = threadIdx.x >> 6;
+  const int l = lane_id(), w = wave_id();
   f32x16 acc[NT];
   zero_acc<NT>(acc);
   float cs[CPL];
@@ -1169,7 +1169,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
   float* gam = q;
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = l & 31, w = wave_id();
   float* sl = gam + H + w * 32 * ldh;
   LANEVEC(s_dg);
   LANEVEC(s_db);
@@ -1263,7 +1263,7 @@ __global__ __launch_bounds__(kBlock) void k_node_items(NodeItemsArgs p) {
   float* gam = lds;
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = l & 31, w = wave_id();
   float* sl = gam + H + w * 32 * ldh;
   LANEVEC(s_dg);
   LANEVEC(s_db);
@@ -1330,7 +1330,7 @@ struct UvItemsArgs {
 __global__ __launch_bounds__(kBlock) void k_uv_items(UvItemsArgs p) {
   constexpr int TH = 4, H = 128;
   const UvBwdArgs& a = p.b;
-  const int l = lane_id(), j = l & 31, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = l & 31, w = wave_id();
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t nw = (int64_t)gridDim.x * kWaves;
   for (int64_t tile = (int64_t)blockIdx.x * kWaves + w; tile < ntiles; tile += nw) {
@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_items(EncEdgeItemsArgs p) {
   stage_vec(b1, a.b1, H, H);
   stage_vec(gam, a.gamma, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = wave_id();
   float* sl = gam + H + w * 32 * ldh;
   LANEVEC(s_dg);
   LANEVEC(s_db);
@@ -1516,7 +1516,7 @@ __global__ __launch_bounds__(256) void k_tcsr_fill(const int32_t* rowptr, int64_
 // one wave per sender segment: rank = number of smaller edge ids in the segment
 __global__ __launch_bounds__(256) void k_tcsr_sort(const int32_t* tptr, int64_t n,
                                                    const int32_t* raw, int32_t* perm) {
-  const int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_id();
   if (s >= n) return;
   const int lane = lane_id();
   const int32_t b = tptr[s], len = tptr[s + 1] - b;
@@ -1941,7 +1941,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_latent_grad(EdgeLatentGradArgs 
   }
   __syncthreads();
   const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
-  const int w = threadIdx.x >> 6, j = im.j;
+  const int w = wave_id(), j = im.j;
   f32x16 acc[L][NT];
 #pragma unroll
   for (int k = 0; k < L; ++k) zero_acc<NT>(acc[k]);

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_nodes(EncNodeArgs a) {
   stage_vec(bb, a.bb, H, H);
   stage_vec(b1e, a.be, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = wave_id();
   const int nvel = (a.T - 1) * a.dim;
   for (int64_t blk = blockIdx.x; blk * (32 * kWaves) < a.n; blk += gridDim.x) {
     const int64_t node0 = blk * (32 * kWaves) + 32 * w;
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
   const int64_t E = a.rowptr[a.n];
   const int64_t ntiles = (E + 31) / 32;
   const int l = lane_id(), j = l & 31, h = l >> 5;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + wave_id();
   const int64_t nw = (int64_t)gridDim.x * kWaves;
   for (int64_t tile = gw; tile < ntiles; tile += nw) {
     const int64_t e = tile * 32 + j;
@@ -274,13 +274,15 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
   float* bm = bb + H;
   float* mbuf = bm + (NL == 3 ? H : 0);  // per wave [32][ldh]
   if (NL == 3) stage_vec(bm, a.bm, H, H);
-  stage_matrix(sW, ldh, a.we, 3 * H, H, H, H, H);
+  // W1e staged pre-scaled by 2^k: (2^k W1e) e0 == W1e (2^k e0) bit for bit
+  // (power-of-two scaling is exact), so the MFMA operands need no scaling.
+  stage_matrix(sW, ldh, a.we, 3 * H, H, H, H, H, a.e_scale);
   if (!GW) stage_matrix(sW + H * ldh, ldh, a.w2, H, H, H, H, H);
   stage_vec(b2, a.b2, H, H);
   stage_vec(g, a.g, H, H);
   stage_vec(bb, a.bb, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = wave_id();
   float* ml = mbuf + w * 32 * ldh;
   const int64_t E = a.rowptr[a.n];
   const int64_t ntiles = (E + 31) / 32;
@@ -288,23 +290,52 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
   const int64_t gw = (int64_t)blockIdx.x * kWaves + w;
   const int64_t nw = (int64_t)gridDim.x * kWaves;
   const int64_t t_begin = ntiles * gw / nw, t_end = ntiles * (gw + 1) / nw;
+  // H = 64 software pipeline: the next tile's indices and e0 are loaded while
+  // this tile computes, and this tile's u[recv] / v[send] gathers are issued
+  // before its W1e e0 product and added after it (the gather latency hides
+  // behind 64 MFMAs).  H = 128 keeps the in-order form (registers).
+  constexpr bool PF = TH == 2;
+  int rv_n = 0, s_n = 0, prv_n = -1, nxt_n = -1;  // int32: no widening right after the load
+  f32x4 xg_n[TH * 4];
+  auto fetch = [&](int64_t t) {
+    const int64_t b = t * 32, ee = b + j;
+    const int64_t ecc = ee < E ? ee : E - 1;
+    rv_n = a.recv[ecc];
+    s_n = a.send[ecc];
+    prv_n = b > 0 ? a.recv[b - 1] : -1;  // receivers around the tile
+    nxt_n = b + 32 < E ? a.recv[b + 32] : -1;
+    const float* src = a.e0t + t * (32 * H) + l * 4;
+#pragma unroll
+    for (int q = 0; q < TH * 4; ++q) xg_n[q] = ld4(src + q * 256);
+  };
+  if (PF && t_begin < t_end) fetch(t_begin);
   for (int64_t tile = t_begin; tile < t_end; ++tile) {
     const int64_t base = tile * 32;
     const int64_t e = base + j;
     const bool valid = e < E;
-    const int64_t ec = valid ? e : E - 1;
-    const int rv = a.recv[ec];
-    const int64_t s = a.send[ec];
-    const int prv = base > 0 ? a.recv[base - 1] : -1;  // receivers around the tile
-    const int nxt = base + 32 < E ? a.recv[base + 32] : -1;
-    f32x16 hacc[TH];
-    load_row_clayout<TH>(hacc, a.u + (int64_t)rv * H);
-    add_row_clayout<TH>(hacc, a.v + s * H);
+    if (!PF) fetch(tile);
+    const int rv = rv_n, prv = prv_n, nxt = nxt_n;
+    const int s = s_n;
     f32x4 xg[TH * 4];
-    const float* src = a.e0t + tile * (32 * H) + l * 4;
 #pragma unroll
-    for (int q = 0; q < TH * 4; ++q) xg[q] = ld4(src + q * 256);
-    mfma_from_groups<TH, TH, false>(hacc, We, ldh, 0, xg, a.e_scale);
+    for (int q = 0; q < TH * 4; ++q) xg[q] = xg_n[q];
+    f32x16 hacc[TH];
+    if constexpr (PF) {
+      f32x16 ur[TH], vr[TH];
+      load_row_clayout<TH>(ur, a.u + (int64_t)rv * H);
+      load_row_clayout<TH>(vr, a.v + (int64_t)s * H);
+      if (tile + 1 < t_end) fetch(tile + 1);
+      zero_acc_regs<TH>(hacc);
+      mfma_from_groups<TH, TH, false>(hacc, We, ldh, 0, xg, 1.0f);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hacc[t][r] += ur[t][r] + vr[t][r];
+    } else {
+      load_row_clayout<TH>(hacc, a.u + (int64_t)rv * H);
+      add_row_clayout<TH>(hacc, a.v + (int64_t)s * H);
+      mfma_from_groups<TH, TH, false>(hacc, We, ldh, 0, xg, 1.0f);
+    }
     acc_relu<TH>(hacc);
     if (TRAIN) store_tiled<TH>(a.sv.h + tile * (32 * H), hacc);
     f32x16 y[TH], h2[TH];
@@ -425,7 +456,7 @@ __global__ __launch_bounds__(kBlock) void k_node_layer(NodeLayerArgs a) {
   stage_vec(g, a.g, H, H);
   stage_vec(bb, a.bb, H, H);
   __syncthreads();
-  const int l = lane_id(), j = l & 31, h = l >> 5, w = threadIdx.x >> 6;
+  const int l = lane_id(), j = l & 31, h = l >> 5, w = wave_id();
   for (int64_t blk = blockIdx.x; blk * (32 * kWaves) < a.n; blk += gridDim.x) {
     const int64_t node0 = blk * (32 * kWaves) + 32 * w;
     if (node0 >= a.n) continue;

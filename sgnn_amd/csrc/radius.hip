@@ -38,7 +38,7 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_block(const int32_t* in, in
     v[k] = i < len ? in[i] : 0;
     s += v[k];
   }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = wave_id();
   int32_t incl = s;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(1024) void k_scan_partials(int32_t* partials, int n
     v[k] = base + k < nb ? partials[base + k] : 0;
     s += v[k];
   }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = wave_id();
   int32_t incl = s;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, 
       }
     }
   }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = wave_id();
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     uint32_t a = v[k];
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void k_radius_query(
     const uint32_t* bbox, const int32_t* cell_of_p, const int32_t* ex_of,
     const int32_t* start, const int32_t* order, int cap, int loop, int32_t* nbr, int32_t* deg) {
   const int lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_id();
   if (i == 0 && lane == 0) deg[n] = 0;  // scan sentinel -> rowptr[n] = E
   if (i >= n) return;
   const Grid G = *reinterpret_cast<const Grid*>(bbox + 8);
@@ -527,7 +527,7 @@ __global__ __launch_bounds__(256) void k_coo_fill(const int64_t* dst, int64_t E,
 __global__ __launch_bounds__(256) void k_coo_sort(const int32_t* ptr, int64_t n, const int32_t* raw,
                                                   const int64_t* src, const int64_t* dst,
                                                   int32_t* send, int32_t* recv, int32_t* perm) {
-  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_id();
   if (i >= n) return;
   const int lane = threadIdx.x & 63;
   const int32_t b = ptr[i], len = ptr[i + 1] - b;

@@ -1,10 +1,10 @@
 set -e
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_training.py tests/test_gpu_harness.py -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
 tail -1 gpurun_out/t.log
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-steps 0 --no-rollout-extras > gpurun_out/b.json 2>gpurun_out/b.err
 python -c "import json;d=json.load(open('gpurun_out/b.json'));print('train', d['ms_per_step'], d['value'], d['kernel_avg_us'])"
-for wl in c1_r15 c2; do
+for wl in c1_r15 c2 c4; do
 timeout -k 10 300 python bench.py --mode rollout --workload $wl --steps 40 --warmup 3 --cpu-steps 0 > gpurun_out/r_$wl.json
 python -c "import json;d=json.load(open('gpurun_out/r_$wl.json'));print('$wl', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],4), 'ms', d['roofline']['frac'])"
 done
