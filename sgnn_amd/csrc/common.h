@@ -153,13 +153,26 @@ SGNN_DEV void mfma_from_groups(f32x16 (&acc)[TH], const float* wl, int ld, int k
 }
 
 // Initialise acc with a per-unit bias (LDS vector, may be null -> 0).
+// (one null test per call, then 16-B LDS reads: registers 4g..4g+3 of a tile
+// hold the contiguous units 32t + 8g + 4h + 0..3)
 template <int TH>
 SGNN_DEV void acc_bias(f32x16 (&acc)[TH], const float* bias_lds) {
   const int h = lane_id() >> 5;
+  if (bias_lds == nullptr) {
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < TH; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = bias_lds ? bias_lds[32 * t + crow(r, h)] : 0.0f;
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 b = ld4(bias_lds + 32 * t + 8 * g + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[t][4 * g + c] = b[c];
+    }
 }
 
 template <int TH>
@@ -217,9 +230,14 @@ SGNN_DEV void acc_layernorm(f32x16 (&acc)[TH], const float* gamma_lds, const flo
 #pragma unroll
   for (int t = 0; t < TH; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int u = 32 * t + crow(r, h);
-      acc[t][r] = (acc[t][r] - mean) * rstd * gamma_lds[u] + beta_lds[u];
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 ga = ld4(gamma_lds + 32 * t + 8 * g + 4 * h);
+      const f32x4 be = ld4(beta_lds + 32 * t + 8 * g + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int r = 4 * g + c;
+        acc[t][r] = (acc[t][r] - mean) * rstd * ga[c] + be[c];
+      }
     }
 }
 
@@ -278,11 +296,16 @@ SGNN_DEV void acc_layernorm_save(f32x16 (&acc)[TH], const float* gamma_lds, cons
 #pragma unroll
   for (int t = 0; t < TH; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int u = 32 * t + crow(r, h);
-      const float yh = (acc[t][r] - mean) * rstd;
-      yhat[t][r] = yh;
-      acc[t][r] = yh * gamma_lds[u] + beta_lds[u];
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 ga = ld4(gamma_lds + 32 * t + 8 * g + 4 * h);
+      const f32x4 be = ld4(beta_lds + 32 * t + 8 * g + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int r = 4 * g + c;
+        const float yh = (acc[t][r] - mean) * rstd;
+        yhat[t][r] = yh;
+        acc[t][r] = yh * ga[c] + be[c];
+      }
     }
 }
 
@@ -297,11 +320,16 @@ SGNN_DEV void acc_layernorm_bwd(const f32x16 (&dout)[TH], const f32x16 (&yhat)[T
 #pragma unroll
   for (int t = 0; t < TH; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float g = dout[t][r] * gamma_lds[32 * t + crow(r, h)];
-      dy[t][r] = g;
-      p1[r & 3] += g;
-      p2[r & 3] += g * yhat[t][r];
+    for (int gq = 0; gq < 4; ++gq) {
+      const f32x4 ga = ld4(gamma_lds + 32 * t + 8 * gq + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int r = 4 * gq + c;
+        const float g = dout[t][r] * ga[c];
+        dy[t][r] = g;
+        p1[r & 3] += g;
+        p2[r & 3] += g * yhat[t][r];
+      }
     }
   float s1 = (p1[0] + p1[1]) + (p1[2] + p1[3]);
   float s2 = (p2[0] + p2[1]) + (p2[2] + p2[3]);
