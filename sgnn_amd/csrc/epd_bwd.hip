@@ -304,7 +304,10 @@ struct EdgeBwdArgs {
   int64_t slab_stride;
 };
 
-template <int TH, int NL>
+// W1E: this layer's dE0 / dW1e products run in-layer (de0t != NULL, the
+// multi-scale path); single-scale H = 64 training leaves them to
+// k_edge_latent_grad, so that variant carries no dW1e accumulator or e0 image.
+template <int TH, int NL, bool W1E>
 __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
   constexpr bool GW = TH > 2;
   constexpr int H = 32 * TH, ldh = H + 4;
@@ -318,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
     stage_matrix_t(p, ldh, a.wl, H, H, H, H, H);
     WlT = p;
     p += H * ldh;
-    if (a.de0t) {  // only the in-layer dE0 product needs W1e^T (the host sizes LDS to match)
+    if (W1E) {  // only the in-layer dE0 product needs W1e^T (the host sizes LDS to match)
       stage_matrix_t(p, ldh, a.we, 3 * H, H, H, H, H);
       WeT = p;
       p += H * ldh;
@@ -377,7 +380,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
                                     acc_wl, acc_wm, s_db, s_dg, s_dbl, s_dbm, dh);
     f32x16 e0[TH];
     zero<TH>(e0);
-    if (nvalid > 0 && a.de0t) {
+    if (W1E && nvalid > 0) {
       // dE0 += 2^k W1e^T dh (the edge latent feeding layer k is 2^k e0)
       f32x16 de[TH];
       zero<TH>(de);
@@ -398,8 +401,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
       }
       store_tiled<TH>(dtile, de);
     }
-    // de0t == NULL: sgnn_edge_latent_grad forms dE0 and dW1e of this layer
-    const bool w1e_here = a.de0t != nullptr;
+    // !W1E: sgnn_edge_latent_grad forms dE0 and dW1e of this layer
+    constexpr bool w1e_here = W1E;
     if (nvalid > 0) {
       if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
       if (w1e_here) {
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
   store_outer<NT>(slab, H, TH, TH, acc_wl);
-  if (a.de0t) store_outer<NT>(slab + H * H, H, TH, TH, acc_w1);
+  if (W1E) store_outer<NT>(slab + H * H, H, TH, TH, acc_w1);
   if (NL == 3) store_outer<NT>(slab + 2 * H * H, H, TH, TH, acc_wm);
   float* v = slab + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, NL);
   store_lane_vec<TH>(v, s_dbl);
@@ -1658,7 +1661,8 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
     return check_launch("edge_layer_bwd");
   }
   const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin) - (de0t ? 0 : 4 * (size_t)H * (H + 4));
-  SGNN_BWD_DISPATCH(H, edge_fn->nlin, (launch_bwd(k_edge_bwd<TH_, NL_>, nslab, lds, stream, a)));
+  if (de0t) SGNN_BWD_DISPATCH(H, edge_fn->nlin, (launch_bwd(k_edge_bwd<TH_, NL_, true>, nslab, lds, stream, a)));
+  else SGNN_BWD_DISPATCH(H, edge_fn->nlin, (launch_bwd(k_edge_bwd<TH_, NL_, false>, nslab, lds, stream, a)));
   return check_launch("edge_layer_bwd");
 }
 

@@ -146,10 +146,9 @@ class Trainer:
         # train.py:276-278: LR for the NEXT step, computed from the pre-increment step
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6
         self.step += 1
-        lo = tw.loss_out
-        return {"loss": lo[0] / n_global, "loss_position": (lo[1] + lo[2] + lo[3]) / n_global,
-                "loss_strain": lo[4] / n_global, "loss_xyz": lo[1:4] / n_global,
-                "n_global": n_global, "lr": self.opt.lr}
+        lo = tw.loss_out[:5] / n_global        # one kernel; the terms are views of it
+        return {"loss": lo[0], "loss_position": lo[1:4].sum(), "loss_strain": lo[4],
+                "loss_xyz": lo[1:4], "n_global": n_global, "lr": self.opt.lr}
 
 
 # ---------------------------------------------------------------------------

@@ -294,6 +294,16 @@ class TrainWorkspace:
         self.scratch = e(max(1, sc(_hip.SLAB_EDGE, cap), sc(_hip.SLAB_ENC_EDGE, cap),
                              sc(_hip.SLAB_NODE, n), sc(_hip.SLAB_UV, n)))
         self._descs_key = None
+        self._side = None
+
+    def side(self, device: torch.device):
+        """Second HIP stream for work off the critical path (the transpose CSR
+        beside the forward layers, the encoder-node backward beside the edge-
+        latent pass) and the events that order it against the launch stream."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=device)
+            self._ev = {k: torch.cuda.Event() for k in ("graph", "tcsr", "g", "enc")}
+        return self._side, self._ev
 
     def activate(self, n: int) -> "TrainWorkspace":
         """Run the next step on n <= n_cap particles (every kernel reads the
@@ -383,6 +393,16 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
     s = stream_ptr(inp.pos_seq.device)
     pos = inp.pos_seq
     engine.radius_graph(ws, pos, (T - 1) * d, T * d, inp.ex_ptr, inp.n_ex, radius)
+    # sender-sorted transpose of the new graph (for dV) on the side stream,
+    # overlapping the forward layers; train_backward waits for it
+    side, ev = tw.side(pos.device)
+    main = torch.cuda.current_stream(pos.device)
+    ev["graph"].record(main)
+    side.wait_event(ev["graph"])
+    check(L.sgnn_transpose_csr(ws.rowptr.data_ptr(), ws.send.data_ptr(), n, ws.edge_cap,
+                               tw.tws_ptr(), tw.tptr.data_ptr(), tw.tperm.data_ptr(), side.cuda_stream),
+          "sgnn_transpose_csr")
+    ev["tcsr"].record(side)
     sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2)
     check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, *emb_args(inp, emb_weight), inp.vel_mean.data_ptr(),
                               inp.vel_std.data_ptr(), float(radius), 1.0, ctypes.byref(pk.enc_node),
@@ -419,9 +439,6 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
                                            inp.acc_std.data_ptr(), tw.xs[k + 1].data_ptr(),
                                            tw.pred.data_ptr(), tw.next_scratch.data_ptr(), 0,
                                            ctypes.byref(sv), s), "sgnn_node_layer_decode")
-    check(L.sgnn_transpose_csr(ws.rowptr.data_ptr(), ws.send.data_ptr(), n, ws.edge_cap,
-                               tw.tws_ptr(), tw.tptr.data_ptr(), tw.tperm.data_ptr(), s),
-          "sgnn_transpose_csr")
 
 
 def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: TrainWorkspace,
@@ -451,6 +468,9 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                   ctypes.byref(pk.dec),
                                   tw.g.data_ptr(), tw.slab(_hip.SLAB_DECODER), tw.nslab_of[_hip.SLAB_DECODER], s),
           "sgnn_decoder_loss_bwd")
+    side, ev = tw.side(inp.pos_seq.device)
+    main = torch.cuda.current_stream(inp.pos_seq.device)
+    main.wait_event(ev["tcsr"])          # tptr / tperm of this step's graph
     for k in range(tw.L - 1, -1, -1):
         nsv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], h2=tw.n_h2[k])
         check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, ctypes.byref(nsv), tw.xs[k].data_ptr(),
@@ -475,12 +495,10 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                             tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV],
                             tw.scratch.data_ptr(), s),
               "sgnn_uv_bwd")
-    if tw.latent_pass:
-        slabs = (ctypes.c_void_p * tw.L)(*[tw.slab(_hip.SLAB_EDGE, k) for k in range(tw.L)])
-        check(L.sgnn_edge_latent_grad(tw._dh_ptrs, ctypes.byref(pk.edge_arr), tw._scales, tw.L,
-                                      ws.rowptr.data_ptr(), n, ws.edge_cap, ws.e0t.data_ptr(),
-                                      tw.de0t.data_ptr(), slabs, tw.nslab_of[_hip.SLAB_EDGE], s),
-              "sgnn_edge_latent_grad")
+    # the encoder-node backward needs only g = dL/dx_0: side stream, beside
+    # the edge-latent pass and the edge-encoder backward
+    ev["g"].record(main)
+    side.wait_event(ev["g"])
     ty, ew, ed, ue = emb_args(inp, emb_weight)
     check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, ty, ew, ed,
                                   int(emb_weight.shape[0]) if ue else 0, ue,
@@ -488,8 +506,15 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                   ctypes.byref(_saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd,
                                                       h2=tw.enc_h2)),
                                   ctypes.byref(pk.enc_node), tw.slab(_hip.SLAB_ENC_NODE),
-                                  tw.nslab_of[_hip.SLAB_ENC_NODE], s),
+                                  tw.nslab_of[_hip.SLAB_ENC_NODE], side.cuda_stream),
           "sgnn_encode_nodes_bwd")
+    ev["enc"].record(side)
+    if tw.latent_pass:
+        slabs = (ctypes.c_void_p * tw.L)(*[tw.slab(_hip.SLAB_EDGE, k) for k in range(tw.L)])
+        check(L.sgnn_edge_latent_grad(tw._dh_ptrs, ctypes.byref(pk.edge_arr), tw._scales, tw.L,
+                                      ws.rowptr.data_ptr(), n, ws.edge_cap, ws.e0t.data_ptr(),
+                                      tw.de0t.data_ptr(), slabs, tw.nslab_of[_hip.SLAB_EDGE], s),
+              "sgnn_edge_latent_grad")
     check(L.sgnn_encode_edges_bwd(tw.de0t.data_ptr(), inp.pos_seq.data_ptr() + 4 * (T - 1) * d, T * d,
                                   d, float(radius), ws.rowptr.data_ptr(), ws.send.data_ptr(),
                                   ws.recv.data_ptr(), n,
@@ -497,6 +522,7 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                   ctypes.byref(pk.enc_edge), tw.slab(_hip.SLAB_ENC_EDGE),
                                   tw.nslab_of[_hip.SLAB_ENC_EDGE], tw.scratch.data_ptr(), ws.edge_cap, s),
           "sgnn_encode_edges_bwd")
+    main.wait_event(ev["enc"])
     check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
                               tw._nblocks, s), "sgnn_reduce_slabs")
     if use_emb:

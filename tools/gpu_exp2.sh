@@ -13,3 +13,4 @@ timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU --output-format csv -d gpurun_out/pmc_c2 -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-steps 0 --no-rollout-extras > /dev/null 2> gpurun_out/pmc.err
 python tools/pmc_summary.py gpurun_out/pmc_c2 k_ > gpurun_out/pmc_c2.txt
 echo pmc done
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/st_c1r -o run -- python3 bench.py --mode rollout --workload c1_r15 --steps 20 --warmup 2 --cpu-steps 0 > /dev/null 2> gpurun_out/st.err
