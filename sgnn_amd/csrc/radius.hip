@@ -320,38 +320,64 @@ __global__ __launch_bounds__(256) void k_radius_query(
     c[2] = k % G.g[2];
   }
   const int rowbase = key - c[0];  // key of cell (0, cy, cz) of this example
-  // the 3^(dim-1) row spans of the neighbourhood, concatenated
+  // the 3^(dim-1) row spans of the neighbourhood, concatenated; all nine
+  // (dz, dy) slots are kept, out-of-grid ones as empty spans, so the bounds
+  // loads go out together and the candidate -> span lookup is a fixed chain
+  // of selects
   int s0[9], pre[10];
-  int nsp = 0;
   pre[0] = 0;
   const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
-  for (int dz = -1; dz <= 1; ++dz) {
-    const int z = c[2] + dz;
-    if (z < 0 || z >= G.g[2]) continue;
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int y = c[1] + dy;
-      if (y < 0 || y >= G.g[1]) continue;
-      const int rk = rowbase + (dz * G.g[1] + dy) * G.g[0];
-      const int a = start[rk + x0], b = start[rk + x1 + 1];
-      s0[nsp] = a;
-      pre[nsp + 1] = pre[nsp] + (b - a);
-      ++nsp;
-    }
+  int sa[9], sb[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const int dz = q / 3 - 1, dy = q % 3 - 1;
+    const int z = c[2] + dz, y = c[1] + dy;
+    const bool ok = z >= 0 && z < G.g[2] && y >= 0 && y < G.g[1];
+    const int rk = ok ? rowbase + (dz * G.g[1] + dy) * G.g[0] : 0;
+    sa[q] = start[rk + x0];
+    sb[q] = start[rk + x1 + 1];
+    sb[q] = ok ? sb[q] : sa[q];
   }
-  const int total = pre[nsp];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    s0[q] = sa[q];
+    pre[q + 1] = pre[q] + (sb[q] - sa[q]);
+  }
+  const int total = pre[9];
   int top = INT32_MAX;  // lanes [0, cnt) hold the kept ids, ascending
   int cnt = 0;
+  // Candidate t of the concatenated spans, clamped to the last one (its
+  // validity, t < total, is tested apart from the load) -- branch-free, so a
+  // load's wait is placed at its first use.
+  auto cand = [&](int t) -> int {
+    const int tc = min(t, total - 1);
+    int off = s0[0] + tc;
+#pragma unroll
+    for (int q = 1; q < 9; ++q)
+      if (tc >= pre[q]) off = s0[q] + (tc - pre[q]);  // empty spans are overridden by the next
+    return order[off];
+  };
+  auto load_pos = [&](int j, float (&p)[3]) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) p[d] = pos[(int64_t)j * stride + min(d, dim - 1)];
+  };
+  // two-stage software pipeline over the 64-candidate steps: the next step's
+  // positions and the ids of the step after are in flight while this step
+  // filters and sorts (the dependent id -> position loads were the per-step
+  // latency of a long candidate list)
+  if (total == 0) {  // only without a finite position of its own
+    if (lane == 0) deg[i] = 0;
+    return;
+  }
+  int jc = cand(lane), jn = cand(64 + lane);
+  float pc[3];
+  load_pos(jc, pc);
   for (int base = 0; base < total; base += 64) {
-    const int t = base + lane;
+    float pn[3];
+    load_pos(jn, pn);
+    const int jnn = cand(base + 128 + lane);
     int key_j = INT32_MAX;
-    if (t < total) {
-      int k = 0;
-      while (k + 1 < nsp && t >= pre[k + 1]) ++k;
-      const int j = order[s0[k] + (t - pre[k])];
-      float pj[3] = {0.0f, 0.0f, 0.0f};
-      for (int d = 0; d < dim; ++d) pj[d] = pos[(int64_t)j * stride + d];
-      if (dist2_ordered(pj, pi, dim) < r2) key_j = j;
-    }
+    if (base + lane < total && dist2_ordered(pc, pi, dim) < r2) key_j = jc;
     if (cnt >= cap) {
       const int kth = __shfl(top, cap - 1, 64);
       if (key_j >= kth) key_j = INT32_MAX;
@@ -365,6 +391,9 @@ __global__ __launch_bounds__(256) void k_radius_query(
       if (lane >= cap) top = INT32_MAX;
       cnt = min(cnt + nnew, cap);
     }
+    jc = jn;  // rotate the pipeline after the sort (a copy of a pending load waits for it)
+    jn = jnn;
+    for (int d = 0; d < 3; ++d) pc[d] = pn[d];
   }
   if (!loop) {  // torch_cluster: K+1 nearest-by-index, then drop the self loop
     const unsigned long long self = __ballot(lane < cnt && top == (int)i);
