@@ -302,7 +302,7 @@ class TrainWorkspace:
         latent pass) and the events that order it against the launch stream."""
         if self._side is None:
             self._side = torch.cuda.Stream(device=device)
-            self._ev = {k: torch.cuda.Event() for k in ("graph", "tcsr", "g", "enc")}
+            self._ev = {k: torch.cuda.Event() for k in ("pos", "encn", "graph", "tcsr", "g", "enc")}
         return self._side, self._ev
 
     def activate(self, n: int) -> "TrainWorkspace":
@@ -392,28 +392,34 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
     n, T, d = ws.n, ws.T, ws.dim
     s = stream_ptr(inp.pos_seq.device)
     pos = inp.pos_seq
+    side, ev = tw.side(pos.device)
+    main = torch.cuda.current_stream(pos.device)
+    # the node encoder (and layer-0 u / v) needs only the positions: side
+    # stream, beside the radius graph; the first edge layer waits for it
+    ev["pos"].record(main)
+    side.wait_event(ev["pos"])
+    sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2)
+    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, *emb_args(inp, emb_weight), inp.vel_mean.data_ptr(),
+                              inp.vel_std.data_ptr(), float(radius), 1.0, ctypes.byref(pk.enc_node),
+                              ctypes.byref(pk.edge[0]), tw.xs[0].data_ptr(), ws.u.data_ptr(),
+                              ws.v.data_ptr(), ctypes.byref(sv), side.cuda_stream), "sgnn_encode_nodes")
+    ev["encn"].record(side)
     engine.radius_graph(ws, pos, (T - 1) * d, T * d, inp.ex_ptr, inp.n_ex, radius)
     # sender-sorted transpose of the new graph (for dV) on the side stream,
     # overlapping the forward layers; train_backward waits for it
-    side, ev = tw.side(pos.device)
-    main = torch.cuda.current_stream(pos.device)
     ev["graph"].record(main)
     side.wait_event(ev["graph"])
     check(L.sgnn_transpose_csr(ws.rowptr.data_ptr(), ws.send.data_ptr(), n, ws.edge_cap,
                                tw.tws_ptr(), tw.tptr.data_ptr(), tw.tperm.data_ptr(), side.cuda_stream),
           "sgnn_transpose_csr")
     ev["tcsr"].record(side)
-    sv = _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2)
-    check(L.sgnn_encode_nodes(pos.data_ptr(), n, T, d, *emb_args(inp, emb_weight), inp.vel_mean.data_ptr(),
-                              inp.vel_std.data_ptr(), float(radius), 1.0, ctypes.byref(pk.enc_node),
-                              ctypes.byref(pk.edge[0]), tw.xs[0].data_ptr(), ws.u.data_ptr(),
-                              ws.v.data_ptr(), ctypes.byref(sv), s), "sgnn_encode_nodes")
     sv = _saves(yhat=tw.ee_yh, rstd=tw.ee_rstd, h2=tw.ee_h2)
     check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius),
                               ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
                               ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(),
                               ctypes.byref(sv), s), "sgnn_encode_edges")
     nl = len(pk.edge)
+    main.wait_event(ev["encn"])          # x0, u, v of layer 0
     for k in range(nl):
         sv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k], h2=tw.e_h2[k])
         with _Timer(timers, "k_edge_layer(train)"):
