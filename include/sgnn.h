@@ -301,7 +301,10 @@ int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t*
  * sgnn_edge_layer_bwd wrote; the 2^k factor is applied by the slab
  * reduction as for the in-layer product).  With it, sgnn_edge_layer_bwd is
  * called with de0t = NULL (H = 64, nlayers <= 9) and skips both products.
- * Writes de0t in the tiled layout of e0. */
+ * Writes de0t in the tiled layout of e0.  Either half may be skipped:
+ * slabs = NULL forms dE0 only; de0t = NULL forms the dW1e blocks only (one
+ * launch per layer, so a layer's dW1e can run on a second stream as soon as
+ * its dh rows exist). */
 int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp* edge_fns,
                           const float* scales, int32_t nlayers, const int32_t* rowptr, int64_t n,
                           int64_t edge_cap, const float* e0t, float* de0t, float* const* slabs,

@@ -1931,15 +1931,18 @@ struct EdgeLatentGradArgs {
 //   dW1e_k += sum_items dh_k (x) e0           (LDS images, items as k;
 //                                              2^k applied in the slab reduction)
 // The W1e_k^T images sit in LDS for L <= 5 (GW = false), else are read from L2.
-template <int TH, int L, bool GW>
+// DE / DW select the two halves: the dW1e-only variant (L = 1) runs per layer
+// on a side stream as soon as that layer's dh is written, the dE0-only pass
+// afterwards carries no item images and no barriers.
+template <int TH, int L, bool GW, bool DE = true, bool DW = true>
 __global__ __launch_bounds__(kBlock) void k_edge_latent_grad(EdgeLatentGradArgs a) {
   constexpr int H = 32 * TH, ldh = H + 4;
   constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
   extern __shared__ float lds[];
   float* bufA = lds;                  // dh_k item image
   float* bufB = bufA + kChunk * ldh;  // e0 item image
-  float* wimg = bufB + kChunk * ldh;  // 2^k W1e_k^T (GW = false)
-  if constexpr (!GW) {
+  float* wimg = DW ? bufB + kChunk * ldh : lds;  // 2^k W1e_k^T (GW = false)
+  if constexpr (DE && !GW) {
 #pragma unroll
     for (int k = 0; k < L; ++k) stage_matrix_t(wimg + k * H * ldh, ldh, a.we[k], 3 * H, H, H, H, H, a.scale[k]);
   }
@@ -1947,8 +1950,10 @@ __global__ __launch_bounds__(kBlock) void k_edge_latent_grad(EdgeLatentGradArgs 
   const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
   const int w = wave_id(), j = im.j;
   f32x16 acc[L][NT];
+  if constexpr (DW) {
 #pragma unroll
-  for (int k = 0; k < L; ++k) zero_acc<NT>(acc[k]);
+    for (int k = 0; k < L; ++k) zero_acc<NT>(acc[k]);
+  }
   const int64_t E = a.rowptr[a.n];
   const int64_t nchunks = (E + kChunk - 1) / kChunk;
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
@@ -1961,17 +1966,20 @@ __global__ __launch_bounds__(kBlock) void k_edge_latent_grad(EdgeLatentGradArgs 
     zero<TH>(e0);
     zero<TH>(cur);
     if (nvalid > 0) {  // tiles past the last valid one are not allocated
-      load_tiled<TH>(e0, a.e0t + tile * (32 * H));
+      if (DW) load_tiled<TH>(e0, a.e0t + tile * (32 * H));
       load_row_clayout<TH>(cur, a.dh[0] + ec * H);
     }
-    zero_if<TH>(e0, !valid);
-    lds_store_items<TH>(im.sB, ldh, j, e0);
+    if constexpr (DW) {
+      zero_if<TH>(e0, !valid);
+      lds_store_items<TH>(im.sB, ldh, j, e0);
+    }
 #pragma unroll
     for (int k = 0; k < L; ++k) {
       if (k + 1 < L && nvalid > 0) load_row_clayout<TH>(nxt, a.dh[k + 1] + ec * H);  // prefetch
       zero_if<TH>(cur, !valid);
-      lds_store_items<TH>(im.sA, ldh, j, cur);
-      if constexpr (GW) {
+      if (DW) lds_store_items<TH>(im.sA, ldh, j, cur);
+      if constexpr (!DE) {
+      } else if constexpr (GW) {
 #pragma unroll
         for (int t = 0; t < TH; ++t)
 #pragma unroll
@@ -1980,27 +1988,39 @@ __global__ __launch_bounds__(kBlock) void k_edge_latent_grad(EdgeLatentGradArgs 
       } else {
         mfma_from_acc<TH, TH>(de, wimg + k * H * ldh, ldh, 0, cur);
       }
-      __syncthreads();
-      outer_tiles<NT>(acc[k], TH, TH, bufA, ldh, 0, bufB, ldh, 0);
-      __syncthreads();
+      if constexpr (DW) {
+        __syncthreads();
+        outer_tiles<NT>(acc[k], TH, TH, bufA, ldh, 0, bufB, ldh, 0);
+        __syncthreads();
+      }
       if (k + 1 < L) {
 #pragma unroll
         for (int t = 0; t < TH; ++t) cur[t] = nvalid > 0 ? nxt[t] : cur[t];
       }
     }
-    if (nvalid > 0) store_tiled<TH>(a.de0t + tile * (32 * H), de);
+    if (DE && nvalid > 0) store_tiled<TH>(a.de0t + tile * (32 * H), de);
   }
+  if constexpr (DW) {
 #pragma unroll
-  for (int k = 0; k < L; ++k)
-    store_outer<NT>(a.slab[k] + blockIdx.x * a.slab_stride + H * H, H, TH, TH, acc[k]);
+    for (int k = 0; k < L; ++k)
+      store_outer<NT>(a.slab[k] + blockIdx.x * a.slab_stride + H * H, H, TH, TH, acc[k]);
+  }
 }
 
-template <int L>
+// DE / DW: both halves (one pass), dE0 only (no item images), or dW1e only
+// (L = 1, one layer per launch).
+template <int L, bool DE, bool DW>
 void launch_latent(const EdgeLatentGradArgs& a, int nslab, void* stream) {
   constexpr int H = 64, ldh = H + 4;
   constexpr bool GW = L > 5;
-  const size_t lds = 4 * (size_t)(2 * kChunk * ldh + (GW ? 0 : L * H * ldh));
-  launch_bwd(k_edge_latent_grad<2, L, GW>, nslab, lds, stream, a);
+  const size_t lds = 4 * (size_t)((DW ? 2 * kChunk * ldh : 0) + (GW || !DE ? 0 : L * H * ldh));
+  launch_bwd(k_edge_latent_grad<2, L, GW, DE, DW>, nslab, lds, stream, a);
+}
+
+template <int L>
+void launch_latent(const EdgeLatentGradArgs& a, int nslab, void* stream, bool dw) {
+  if (dw) return launch_latent<L, true, true>(a, nslab, stream);
+  launch_latent<L, true, false>(a, nslab, stream);
 }
 }  // namespace
 
@@ -2009,7 +2029,7 @@ extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp
                                      int64_t n, int64_t edge_cap, const float* e0t, float* de0t,
                                      float* const* slabs, int32_t nslab, void* stream) {
   using namespace sgnn;
-  if (!dh_rows || !edge_fns || !scales || !rowptr || !e0t || !de0t || !slabs || nslab < 1 ||
+  if (!dh_rows || !edge_fns || !scales || !rowptr || !e0t || (!de0t && !slabs) || nslab < 1 ||
       nlayers < 1 || n <= 0 || edge_cap < 1)
     return set_error(SGNN_ERR_INVALID, "edge_latent_grad: bad arguments");
   const int H = edge_fns[0].hidden;
@@ -2018,12 +2038,12 @@ extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp
     return set_error(SGNN_ERR_UNSUPPORTED, "edge_latent_grad: at most 9 layers share an edge latent");
   EdgeLatentGradArgs a{};
   for (int k = 0; k < nlayers; ++k) {
-    if (!dh_rows[k] || !edge_fns[k].w1 || edge_fns[k].hidden != H || !slabs[k] ||
+    if (!dh_rows[k] || !edge_fns[k].w1 || edge_fns[k].hidden != H || (slabs && !slabs[k]) ||
         edge_fns[k].nlin != edge_fns[0].nlin)
       return set_error(SGNN_ERR_INVALID, "edge_latent_grad: layer arguments");
     a.dh[k] = dh_rows[k];
     a.we[k] = edge_fns[k].w1 + 2 * H;
-    a.slab[k] = slabs[k];
+    a.slab[k] = slabs ? slabs[k] : nullptr;
     a.scale[k] = scales[k];
   }
   a.nlayers = nlayers;
@@ -2032,16 +2052,29 @@ extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp
   a.e0t = e0t;
   a.de0t = de0t;
   a.slab_stride = sgnn_bwd_slab_floats(SGNN_SLAB_EDGE, H, 0, edge_fns[0].nlin);
+  if (!de0t) {  // dW1e only: one launch per layer
+    for (int k = 0; k < nlayers; ++k) {
+      EdgeLatentGradArgs b = a;
+      b.dh[0] = a.dh[k];
+      b.we[0] = a.we[k];
+      b.slab[0] = a.slab[k];
+      b.scale[0] = a.scale[k];
+      b.nlayers = 1;
+      launch_latent<1, false, true>(b, nslab, stream);
+    }
+    return check_launch("edge_latent_grad");
+  }
+  const bool dw = slabs != nullptr;
   switch (nlayers) {
-    case 1: launch_latent<1>(a, nslab, stream); break;
-    case 2: launch_latent<2>(a, nslab, stream); break;
-    case 3: launch_latent<3>(a, nslab, stream); break;
-    case 4: launch_latent<4>(a, nslab, stream); break;
-    case 5: launch_latent<5>(a, nslab, stream); break;
-    case 6: launch_latent<6>(a, nslab, stream); break;
-    case 7: launch_latent<7>(a, nslab, stream); break;
-    case 8: launch_latent<8>(a, nslab, stream); break;
-    default: launch_latent<9>(a, nslab, stream); break;
+    case 1: launch_latent<1>(a, nslab, stream, dw); break;
+    case 2: launch_latent<2>(a, nslab, stream, dw); break;
+    case 3: launch_latent<3>(a, nslab, stream, dw); break;
+    case 4: launch_latent<4>(a, nslab, stream, dw); break;
+    case 5: launch_latent<5>(a, nslab, stream, dw); break;
+    case 6: launch_latent<6>(a, nslab, stream, dw); break;
+    case 7: launch_latent<7>(a, nslab, stream, dw); break;
+    case 8: launch_latent<8>(a, nslab, stream, dw); break;
+    default: launch_latent<9>(a, nslab, stream, dw); break;
   }
   return check_launch("edge_latent_grad");
 }

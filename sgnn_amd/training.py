@@ -495,6 +495,18 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                     int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), tw.nslab_of[_hip.SLAB_EDGE],
                                     tw.scratch.data_ptr(), ws.edge_cap, s),
               "sgnn_edge_layer_bwd")
+        if tw.latent_pass:
+            # dW1e_k = sum_e dh_k e0^T needs only this layer's dh: side stream,
+            # beside the node-level backward of the layers below
+            ev["g"].record(main)
+            side.wait_event(ev["g"])
+            slab_k = (ctypes.c_void_p * 1)(tw.slab(_hip.SLAB_EDGE, k))
+            check(L.sgnn_edge_latent_grad(ctypes.addressof(tw._dh_ptrs) + 8 * k,
+                                          ctypes.addressof(pk.edge_arr) + ctypes.sizeof(_hip.SgnnMlp) * k,
+                                          ctypes.addressof(tw._scales) + 4 * k, 1, ws.rowptr.data_ptr(), n,
+                                          ws.edge_cap, ws.e0t.data_ptr(), None, slab_k,
+                                          tw.nslab_of[_hip.SLAB_EDGE], side.cuda_stream),
+                  "sgnn_edge_latent_grad")
         check(L.sgnn_uv_bwd(tw.dxp.data_ptr(), tw.du.data_ptr(), ws.cin.data_ptr(), ws.cout.data_ptr(),
                             ws.rowptr.data_ptr(), dh_rows.data_ptr(), tw.tptr.data_ptr(),
                             tw.tperm.data_ptr(), tw.xs[k].data_ptr(), n, ctypes.byref(pk.edge[k]),
@@ -515,11 +527,10 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                   tw.nslab_of[_hip.SLAB_ENC_NODE], side.cuda_stream),
           "sgnn_encode_nodes_bwd")
     ev["enc"].record(side)
-    if tw.latent_pass:
-        slabs = (ctypes.c_void_p * tw.L)(*[tw.slab(_hip.SLAB_EDGE, k) for k in range(tw.L)])
+    if tw.latent_pass:   # dE0 = sum_k 2^k W1e_k^T dh_k (the dW1e halves ran per layer)
         check(L.sgnn_edge_latent_grad(tw._dh_ptrs, ctypes.byref(pk.edge_arr), tw._scales, tw.L,
                                       ws.rowptr.data_ptr(), n, ws.edge_cap, ws.e0t.data_ptr(),
-                                      tw.de0t.data_ptr(), slabs, tw.nslab_of[_hip.SLAB_EDGE], s),
+                                      tw.de0t.data_ptr(), None, tw.nslab_of[_hip.SLAB_EDGE], s),
               "sgnn_edge_latent_grad")
     check(L.sgnn_encode_edges_bwd(tw.de0t.data_ptr(), inp.pos_seq.data_ptr() + 4 * (T - 1) * d, T * d,
                                   d, float(radius), ws.rowptr.data_ptr(), ws.send.data_ptr(),
