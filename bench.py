@@ -1,27 +1,36 @@
 #!/usr/bin/env python3
-"""Benchmark: particle-steps/s (+ M edge-messages/s) of the 2D Taylor-impact
-learned simulator on MI355X (BASELINE.json `metric`).
+"""Benchmark: particle-steps/s + M edge-messages/s of the 2D Taylor-impact
+learned-simulator ROLLOUT on MI355X (BASELINE.json `metric`), with the
+1/2/4/8-GPU training curve and the other BASELINE configs as extras.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode train|rollout]
-                  [--workload c2|c1_r15|c1_r06]
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+                  [--mode rollout|train|train-c3|ms-train|ms-rollout] [--workload ...]
 
---mode train (default; BASELINE configs[1] "~50k particles, 5 layers,
-hidden=64, fp32, forward+backward"): one step = the reference training step
-(train.py:231-280): random-walk noise, predict_accelerations forward, loss,
-backward, [N>1: RCCL all-reduce of the flat gradient], Adam, LR decay.  Each
-rank owns one whole graph (weak scaling, whole-graph DDP over xGMI).
---mode rollout: one step = one autoregressive predict_positions (radius
-graph + features + encoder + L layers + decoder + Euler + window shift),
-the steps replayed from a captured HIP graph; multi-GPU rollout is replicas
-only (no collective).
-Inputs are resident in HBM before the timed region.  Synthetic lattice data
-and random-init weights (no dataset/checkpoint offline).
+Default (`--mode rollout --workload c1_r15`, BASELINE.md §3's 10x config):
+one step = one autoregressive `predict_positions` (radius graph + features +
+encoder + 5 InteractionNetworks + decoder + Euler + window shift) on a
+2,000-particle 2D Taylor-bar lattice at r = 15 (cap K = 20 binds), the loop of
+evaluate.py:117-145 issued as ONE `sgnn_rollout` C call.  Inputs are resident
+in HBM before the timed region.  With N > 1 every rank rolls out its own
+trajectory (rollout shards as replicas only) and `value`
+counts all ranks' particle-steps over the max-over-ranks time.
 
-Extra keys: "roofline" (dominant kernel, timed live with HIP events on the
-launch stream, traffic from the committed rocprofv3 PMC summary),
-"cpu_baseline" (the oracle = plain-torch CPU restatement of the reference on
-this box's host cores, rank 0 at N=1 only, bounded sample) and "rollout"
-(C2 and C1 forward-rollout rates with their own CPU baselines).
+Extras in the same JSON line (every N):
+  "training"      C2 training step (noise + fwd + bwd + RCCL all-reduce + Adam),
+                  50k particles per rank, whole-graph DDP: weak scaling.  This
+                  is the north_star's 1/2/4/8-GPU training curve.
+  "training_c3"   C3: global batch of 8 real-size graphs (4,800/6,400/8,000
+                  particles) split over the N ranks: strong scaling.
+  "rollout_extra" C2 (50k, r = 0.6), C1 at r = 0.6 and C4 (3D 200k, L = 10,
+                  H = 128) rollouts (replicas at N > 1).
+  "multi_scale_c5_train"  C5: multi-scale 3D 1M particles per rank, DDP.
+CPU baselines (rank 0 at N = 1 only): the oracle (plain-torch CPU restatement
+of the reference, test infrastructure) on this box's host cores; >= 20 timed
+rollout steps after one warm-up; training legs bounded to ~10-30 s.
+
+`--gpus N` without a torch.distributed environment re-launches this script
+under `python -m torch.distributed.run --nproc-per-node N` as a CHILD process
+(before anything touches the GPU) and exits with its status.
 """
 from __future__ import annotations
 
@@ -30,6 +39,8 @@ import glob
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,8 +50,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from sgnn_amd import engine, synthetic  # noqa: E402
-from sgnn_amd.learned_simulator import LearnedSimulator  # noqa: E402
+from sgnn_amd import synthetic  # noqa: E402
 
 WORKLOADS = {
     # name: (lattice dims, radius, hidden, layers)
@@ -55,68 +65,71 @@ MS_WORKLOADS = {
     "c5_small": ((40, 40, 40), 2, 2, 2.0, 128, 10, 2),
     "ms2d": ((240, 200), 2, 2, 2.0, 128, 10, 2),      # multi_scale_config.yaml widths, 2D
 }
+# C3 (BASELINE configs[2]): global batch of 8 whole graphs at the real Taylor
+# bar sizes (120/160/200 x 40 lattices = 4,800/6,400/8,000 particles)
+C3_GRAPHS = [(120, 40), (160, 40), (200, 40), (120, 40), (160, 40), (200, 40), (120, 40), (160, 40)]
+
+T_SEQ = 11                # config.yaml:20 input_sequence_length
+MFMA_F32_PEAK = 157.3e12  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK = 8.0e12         # MI355X HBM3E bytes/s (MI355X_MICROARCH.md)
+DATA = "synthetic (0.5 mm Taylor-bar lattice + random-walk frames; random-init weights)"
 
 
 def lattice(dims):
     return synthetic.lattice_2d(*dims) if len(dims) == 2 else synthetic.lattice_3d(*dims)
-T_SEQ = 11                # config.yaml:20 input_sequence_length
-MFMA_F32_PEAK = 157.3e12  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["train", "rollout", "ms-train", "ms-rollout"], default="train")
+    ap.add_argument("--mode", choices=["rollout", "train", "train-c3", "ms-train", "ms-rollout"],
+                    default="rollout")
     ap.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(MS_WORKLOADS), default=None)
-    ap.add_argument("--cpu-steps", type=int, default=10, help="oracle steps for cpu_baseline (0: skip)")
-    ap.add_argument("--no-rollout-extras", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=20,
+                    help="timed oracle rollout steps for cpu_baseline (0: skip); training legs use fewer")
+    ap.add_argument("--no-extras", "--no-rollout-extras", dest="no_extras", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
-    return ap.parse_args()
+    ap.add_argument("--selftest-launch", action="store_true",
+                    help="launcher self-test: gloo on CPU, a stub step, no GPU (tests/test_bench_launch.py)")
+    return ap.parse_args(argv)
 
 
-def init_dist():
+# ----------------------------------------------------------------------------- launch / dist
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_workers(args, argv) -> int:
+    """`--gpus N` outside a torch.distributed environment: start N ranks with
+    torch.distributed.run as a child process (this parent never initialises
+    HIP, so nothing is exec'd over a GPU context) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N ranks with "
+                         f"torch.distributed.run --nproc-per-node N, or pass only --gpus N")
     if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.selftest_launch:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
-
-
-def make_sim(H, L, radius, dim, device, seed):
-    torch.manual_seed(seed)
-    stats = synthetic.normalization_stats(dim, noise_std=0.02)
-    st = {k: {kk: torch.tensor(vv) for kk, vv in v.items()} for k, v in stats.items()}
-    sim = LearnedSimulator(dim, (T_SEQ - 1) * dim + 1, dim + 1, H, L, 1, H, radius, st, 1, 9,
-                           device=device)
-    return sim.to(device)
-
-
-def cpu_model():
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return platform.processor() or platform.machine()
-
-
-def profiled_traffic(workload, mode, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/r*_summary.json: FETCH_SIZE x2 + WRITE_SIZE), newest matching tag."""
-    best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
-        d = json.load(open(path))
-        if d.get("workload") != workload or d.get("mode", "rollout") != mode:
-            continue
-        for k, v in d["kernels"].items():
-            if k.split("<")[0] == kernel and "hbm_bytes" in v:
-                best = (v["hbm_bytes"], os.path.relpath(path, ROOT))
-    return best
 
 
 def sync_barrier(world):
@@ -127,13 +140,96 @@ def sync_barrier(world):
 
 
 def max_over_ranks(x, world, device):
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return float(t.item())
 
 
-# ----------------------------------------------------------------------------- rollout
+def sum_over_ranks(x, world, device):
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    if world > 1:
+        torch.distributed.all_reduce(t)
+    return float(t.item())
+
+
+def selftest_launch(world, rank):
+    """Stub step for the launcher test: one gloo all-reduce, no GPU."""
+    t = torch.ones(1)
+    if world > 1:
+        torch.distributed.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": "selftest", "n_gpus": world, "allreduce_sum": float(t.item()),
+                          "ranks_env": os.environ.get("WORLD_SIZE")}))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------- CPU baseline helpers
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_threads() -> dict:
+    """Threads for the CPU baseline: every core this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS when the environment sets
+    it (on the GPU box it is the box's CPU share, while os.cpu_count() shows
+    the whole host).  Reported with the raw counts."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    n = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    torch.set_num_threads(n)
+    return {"cores": torch.get_num_threads(), "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": omp, "cpu_model": cpu_model(), "kind": "port"}
+
+
+def profiled(workload, mode, kernel):
+    """Per-launch HBM bytes and duration of `kernel` from the newest committed
+    rocprofv3 summary (profiles/r*_summary.json: FETCH_SIZE x2 + WRITE_SIZE)."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
+        d = json.load(open(path))
+        if d.get("workload") != workload or d.get("mode", "rollout") != mode:
+            continue
+        for k, v in d["kernels"].items():
+            if k.split("<")[0] == kernel and "hbm_bytes" in v:
+                best = {"bytes": v["hbm_bytes"], "avg_us": v.get("avg_us"), "source": os.path.relpath(path, ROOT)}
+    return best
+
+
+def roofline(kernel, flops, avg_s, workload, mode, alg_bytes=None):
+    prof = profiled(workload, mode, kernel)
+    r = {"bound": "mfma", "kernel": kernel, "achieved": flops / avg_s / 1e12, "peak": MFMA_F32_PEAK / 1e12,
+         "unit": "TFLOP/s", "frac": flops / avg_s / MFMA_F32_PEAK,
+         "traffic": prof["bytes"] if prof else None,
+         "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+         "traffic_source": prof["source"] if prof else None,
+         "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops}
+    if prof:
+        r["hbm_frac"] = prof["bytes"] / avg_s / HBM_PEAK          # achieved HBM fraction (live duration)
+        r["profiled_avg_us"] = prof["avg_us"]
+    if alg_bytes is not None:
+        r["algorithmic_bytes"] = alg_bytes
+    return r
+
+
+# ----------------------------------------------------------------------------- models / data
+def make_sim(H, L, radius, dim, device, seed):
+    from sgnn_amd.learned_simulator import LearnedSimulator
+    torch.manual_seed(seed)
+    stats = synthetic.normalization_stats(dim, noise_std=0.02)
+    st = {k: {kk: torch.tensor(vv) for kk, vv in v.items()} for k, v in stats.items()}
+    sim = LearnedSimulator(dim, (T_SEQ - 1) * dim + 1, dim + 1, H, L, 1, H, radius, st, 1, 9,
+                           device=device)
+    return sim.to(device)
+
+
 def quiet_decoder(sim):
     """Scale the random-init decoder's output layer by 1e-3 so that the
     autoregressive rollout of an untrained model stays physical (particles
@@ -146,40 +242,26 @@ def quiet_decoder(sim):
     return sim
 
 
-def rollout_setup(workload, device, seed, rank):
-    dims, radius, H, L = WORKLOADS[workload]
-    dim = len(dims)
-    sim = quiet_decoder(make_sim(H, L, radius, dim, device, seed))
-    seq = synthetic.trajectory(lattice(dims), T_SEQ, seed=1000 + rank)
-    n = seq.shape[0]
-    window0 = torch.from_numpy(seq)
-    types_ = torch.zeros(n, dtype=torch.long, device=device)
-    inp, use_emb = sim._step_inputs(window0.to(device), [n], types_)
-    ws = sim._workspace(n, T_SEQ, device)
-    win = [inp.pos_seq, torch.empty_like(inp.pos_seq)]
-    pred = torch.empty(n, dim + 1, device=device)
-    nxt = torch.empty(n, dim, device=device)
-
-    def run(k0, nsteps, timers=None):
-        for k in range(k0, k0 + nsteps):
-            inp.pos_seq = win[k % 2]
-            engine.forward_step(sim._encode_process_decode, sim._particle_type_embedding.weight, use_emb,
-                                radius, inp, ws, pred, nxt, window_out=win[(k + 1) % 2], timers=timers)
-    return sim, window0, ws, run, n, radius, H, L
+# ----------------------------------------------------------------------------- rollout
+CPU_SAMPLE_DIMS = {"c4": (20, 20, 20)}   # bounded CPU sample (same spacing / radius / model)
 
 
-CPU_SAMPLE_DIMS = {"c4": (40, 25, 20)}   # bounded CPU sample (same spacing / radius / model)
-
-
-def cpu_rollout_baseline(sim, window, radius, L, steps, workload=None):
-    """Oracle (test infrastructure: CPU restatement of the reference) rollout."""
+def cpu_rollout_baseline(sim, window, radius, L, steps, workload):
+    """Oracle (test infrastructure: CPU restatement of the reference) rollout:
+    one warm-up step, then `steps` timed autoregressive steps (graph build +
+    features + EPD + integration all inside the timed region)."""
     from oracle import sgnn_oracle as O
+    info = cpu_threads()
     state = {k: v.detach().cpu() for k, v in sim.state_dict().items()}
+    sample = ""
     if workload in CPU_SAMPLE_DIMS:
         window = torch.from_numpy(synthetic.trajectory(lattice(CPU_SAMPLE_DIMS[workload]), T_SEQ, seed=7))
+        sample = (f" (a {'x'.join(map(str, CPU_SAMPLE_DIMS[workload]))} sample of the same lattice, "
+                  f"spacing, radius and model: per-particle rate, not the full config size)")
     osim = O.OracleSimulator(state, window.shape[2], L, radius, sim._normalization_stats)
     cur, n = window.cpu(), window.shape[0]
     types_ = torch.zeros(n, dtype=torch.long)
+    edges = 0
     with torch.no_grad():
         nxt, _ = osim.predict_positions(cur, [n], types_)
         cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
@@ -188,62 +270,91 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload=None):
             nxt, _ = osim.predict_positions(cur, [n], types_)
             cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
         dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": torch.get_num_threads(),
-            "kind": "port", "cpu_model": cpu_model(), "seconds": dt,
-            "sample": f"{steps} autoregressive oracle rollout steps (torch CPU fp32 restatement of the "
-                      f"reference ops + C cell-list radius search), {n} particles, after 1 warm-up step"}
+        edges = int(O.radius_graph(cur[:, -1], [n], radius)[0].shape[0])
+    return {"value": n * steps / dt, "unit": "particle-steps/s", **info, "seconds": dt,
+            "M_edge_messages_per_s": edges * L * steps / dt / 1e6,
+            "sample": f"{steps} autoregressive oracle rollout steps after 1 warm-up (torch CPU fp32 "
+                      f"restatement of the reference ops + C cell-list radius search), {n} particles{sample}"}
 
 
 def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps):
-    """Timed region: `steps` autoregressive steps replayed from a captured HIP
-    graph (evaluate.rollout's device path: the same kernels per step, no
-    per-kernel launch cost); warm-up = capture + one untimed full rollout."""
-    sim, window0, ws, run, n, radius, H, L = rollout_setup(workload, device, seed, rank)
+    """Timed region: `steps` autoregressive steps issued as ONE sgnn_rollout
+    call (evaluate.rollout's device path: the C driver launches every kernel of
+    every step; no host round trip).  Warm-up: full untimed rollouts.  The
+    edge-layer launch time comes from a second, event-timed pass."""
+    from sgnn_amd import engine
+    dims, radius, H, L = WORKLOADS[workload]
+    dim = len(dims)
+    sim = quiet_decoder(make_sim(H, L, radius, dim, device, seed))
+    seq = synthetic.trajectory(lattice(dims), T_SEQ, seed=1000 + rank)
+    n = seq.shape[0]
+    window0 = torch.from_numpy(seq)
+    types_ = torch.zeros(n, dtype=torch.long, device=device)
     with torch.no_grad():
-        types_ = torch.zeros(n, dtype=torch.long, device=device)
         w0 = window0.to(device)
         runner = sim.rollout_runner(w0, [n], types_, steps)
-        for _ in range(max(1, warmup // max(steps, 1))):
+        for _ in range(max(1, -(-warmup // max(steps, 1)))):
             runner.run(w0)
         sync_barrier(world)
         t0 = time.perf_counter()
         runner.run(w0)
         sync_barrier(world)
         dt = time.perf_counter() - t0
+        # event-timed pass (same kernels, launched from Python per step)
+        inp, use_emb = sim._step_inputs(w0, [n], types_)
+        ws = sim._workspace(n, T_SEQ, device)
+        win = [inp.pos_seq.clone(), torch.empty_like(inp.pos_seq)]
+        pred = torch.empty(n, dim + 1, device=device)
+        nxt = torch.empty(n, dim, device=device)
         timers = []
-        run(0, steps, timers=timers)   # from the initial window (win[0])
+        edges = []
+        for k in range(steps):
+            inp.pos_seq = win[k % 2]
+            engine.forward_step(sim._encode_process_decode, sim._particle_type_embedding.weight, use_emb,
+                                radius, inp, ws, pred, nxt, window_out=win[(k + 1) % 2], timers=timers)
+            edges.append(ws.num_edges())
         torch.cuda.synchronize()
     dt = max_over_ranks(dt, world, device)
-    E = ws.num_edges()
+    E = float(np.mean(edges))
+    E_all = sum_over_ranks(E, world, device)
     edge_avg_s = float(np.mean([a.elapsed_time(b) for a, b in timers])) * 1e-3
-    flops = E * 4 * H * H
-    out = {"workload": f"{workload}: {'x'.join(map(str, WORKLOADS[workload][0]))} lattice = {n} particles/GPU, "
-                       f"r={radius}, L={L}, H={H}", "particles": n,
-           "edges": E, "value": n * steps * world / dt, "unit": "particle-steps/s",
+    flops = E * 4 * H * H            # two H x H Linears per edge (u/v factorised out of the first)
+    # algorithmic bytes of one edge-layer launch: e0 row (4H) + sender/receiver ids (8) per edge,
+    # u/v rows per node (8H), agg row written per node (4H)
+    alg_bytes = E * (4 * H + 8) + n * 12 * H
+    out = {"workload": f"{workload}: {'x'.join(map(str, dims))} lattice = {n} particles/GPU, "
+                       f"r={radius}, L={L}, H={H}, T={T_SEQ}, K=20", "particles": n, "edges": E,
+           "value": n * steps * world / dt, "unit": "particle-steps/s",
            "ms_per_step": dt / steps * 1e3,
-           "M_edge_messages_per_s": E * L * steps * world / dt / 1e6,
-           "edge_kernel_us": edge_avg_s * 1e6, "edge_kernel_mfma_frac": flops / edge_avg_s / MFMA_F32_PEAK}
+           "M_edge_messages_per_s": E_all * L * steps / dt / 1e6,
+           "roofline": roofline("k_edge_layer", flops, edge_avg_s, workload, "rollout", alg_bytes)}
+    out["roofline"]["share_of_step"] = edge_avg_s * L / (dt / steps)
     if cpu_steps > 0 and rank == 0 and world == 1:
         out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps, workload)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
-    return out, timers, flops, edge_avg_s, E, n, radius, H, L
+    return out
 
 
 # ----------------------------------------------------------------------------- train
-def cpu_train_baseline(state, seq, strain, radius, L, steps, stats):
-    """Oracle training step (noise + forward + torch autograd + torch Adam) on the CPU."""
+def cpu_train_baseline(state, graphs, radius, L, steps, stats):
+    """Oracle training step (noise + forward + torch autograd + torch Adam) on the
+    CPU over the same concatenated batch."""
     from oracle import sgnn_oracle as O
+    info = cpu_threads()
     params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in state.items()}
     osim = O.OracleSimulator(params, 2, L, radius, stats)
     osim.p = params
     opt = torch.optim.Adam([p for k, p in params.items() if "embedding" not in k], lr=1e-3)
-    pos, nxt = torch.from_numpy(seq[:, :T_SEQ]), torch.from_numpy(seq[:, T_SEQ])
+    pos = torch.from_numpy(np.concatenate([g[:, :T_SEQ] for g, _ in graphs]))
+    nxt = torch.from_numpy(np.concatenate([g[:, T_SEQ] for g, _ in graphs]))
+    strain = torch.from_numpy(np.concatenate([s for _, s in graphs]))
+    counts = [g.shape[0] for g, _ in graphs]
     n = pos.shape[0]
     types_ = torch.zeros(n, dtype=torch.long)
 
     def step():
         noise = O.random_walk_noise(pos, 0.02)
-        pa, ta, ps = osim.predict_accelerations(nxt, noise, pos, [n], types_)
+        pa, ta, ps = osim.predict_accelerations(nxt, noise, pos, counts, types_)
         loss = O.training_loss(pa, ta, ps, strain)
         opt.zero_grad()
         loss.backward()
@@ -254,79 +365,91 @@ def cpu_train_baseline(state, seq, strain, radius, L, steps, stats):
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": torch.get_num_threads(),
-            "kind": "port", "cpu_model": cpu_model(), "seconds": dt,
-            "sample": f"{steps} oracle training steps (noise + forward + torch autograd backward + Adam, "
-                      f"torch CPU fp32 restatement of the reference ops), {n} particles, after 1 warm-up"}
+    return {"value": n * steps / dt, "unit": "particle-steps/s", **info, "seconds": dt,
+            "sample": f"{steps} oracle training steps after 1 warm-up (noise + forward + torch autograd "
+                      f"backward + Adam, torch CPU fp32 restatement of the reference ops), {n} particles "
+                      f"in {len(counts)} graph(s) (training steps are ~2.5 s each at 50k: bounded to ~25 s)"}
 
 
-def bench_train(args, world, rank, device):
-    from sgnn_amd.train import Trainer
-    dims, radius, H, L = WORKLOADS[args.workload]
-    nx, ny = dims
-    sim = make_sim(H, L, radius, 2, device, args.seed)
+def _train_graph(dims, seed):
+    seq = synthetic.trajectory(synthetic.lattice_2d(*dims), T_SEQ + 1, seed=seed)
+    strain = np.random.default_rng(seed).normal(0, 1, seq.shape[0]).astype(np.float32)
+    return seq, strain
+
+
+def bench_train(mode, steps, warmup, world, rank, device, seed, cpu_steps):
+    """C2 (`train`: one 50k graph per rank, weak scaling) or C3 (`train-c3`: a
+    global batch of 8 real-size graphs split over the ranks, strong scaling).
+    One step = Trainer.train_step: fused noise, saved-activation forward, fused
+    loss + backward, SUM all-reduce of the flat gradient over RCCL, Adam, LR."""
+    from sgnn_amd.train import Trainer, split_batch
+    if mode == "train":
+        dims, radius, H, L = WORKLOADS["c2"]
+        all_graphs = [dims] * world
+        mine_idx = [rank]
+        desc = (f"c2: 2D lattice {dims[0]}x{dims[1]} = {dims[0] * dims[1]} particles per GPU (one whole graph "
+                f"per rank), r={radius}, L={L}, H={H}, T={T_SEQ}, K=20, training step (noise+fwd+bwd+Adam)")
+        scaling = "weak"
+    else:
+        _, radius, H, L = WORKLOADS["c2"]
+        all_graphs = C3_GRAPHS
+        mine_idx = split_batch(list(range(len(all_graphs))), rank, world)
+        desc = (f"c3: global batch of {len(all_graphs)} whole graphs "
+                f"({'/'.join(str(a * b) for a, b in all_graphs)} particles, real Taylor-bar sizes) split "
+                f"contiguously over the ranks, r={radius}, L={L}, H={H}, T={T_SEQ}, K=20, training step")
+        scaling = "strong"
+    sim = make_sim(H, L, radius, 2, device, seed)
     state0 = {k: v.detach().cpu().clone() for k, v in sim.state_dict().items()}
-    seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny), T_SEQ + 1, seed=2000 + rank)
-    n = seq.shape[0]
-    pos = torch.from_numpy(seq[:, :T_SEQ]).to(device)
-    nxt = torch.from_numpy(seq[:, T_SEQ]).to(device)
-    strain_np = np.random.default_rng(rank).normal(0, 1, n).astype(np.float32)
-    strain = torch.from_numpy(strain_np).to(device)
+    graphs = [_train_graph(all_graphs[i], 2000 + i) for i in mine_idx]
+    counts = [g.shape[0] for g, _ in graphs]
+    all_counts = [a * b for a, b in all_graphs]
+    n_global = sum(all_counts)
+    offset = sum(all_counts[:mine_idx[0]])
+    n = sum(counts)
+    pos = torch.from_numpy(np.concatenate([g[:, :T_SEQ] for g, _ in graphs])).to(device)
+    nxt = torch.from_numpy(np.concatenate([g[:, T_SEQ] for g, _ in graphs])).to(device)
+    strain = torch.from_numpy(np.concatenate([s for _, s in graphs])).to(device)
     tr = Trainer(sim, lr_init=1e-3)
-    for _ in range(args.warmup):
-        tr.train_step(pos, nxt, strain, [n])
+    kw = dict(n_global=n_global, particle_offset=offset)
+    for _ in range(warmup):
+        tr.train_step(pos, nxt, strain, counts, **kw)
     sync_barrier(world)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = tr.train_step(pos, nxt, strain, [n])
+    for _ in range(steps):
+        out = tr.train_step(pos, nxt, strain, counts, **kw)
     sync_barrier(world)
     dt = time.perf_counter() - t0
     timers = {}
     t2 = time.perf_counter()
-    for _ in range(args.steps):
-        tr.train_step(pos, nxt, strain, [n], timers=timers)
+    for _ in range(steps):
+        tr.train_step(pos, nxt, strain, counts, timers=timers, **kw)
     torch.cuda.synchronize()
     dt_ev = time.perf_counter() - t2
     dt = max_over_ranks(dt, world, device)
     tw = tr.workspace(n, T_SEQ, device)
     E = tw.f.num_edges()
-    loss = float(out["loss"])
+    E_all = sum_over_ranks(E, world, device)
     kstats = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in timers.items()}
-    # dominant kernel by total time: the edge-layer backward: W2^T dy, dW2 += dy h^T
-    # (H = 64: dE0 and dW1e of all layers are formed afterwards by
-    # k_edge_latent_grad; H = 128 adds W1e^T dh and dW1e += dh e0^T in-layer)
+    # dominant kernel: the edge-layer backward (W2^T dy, dW2 += dy h^T; H = 64
+    # forms dE0 / dW1e of all layers afterwards in k_edge_latent_grad)
     dom = "k_edge_bwd"
     flops_bwd = E * (4 if tw.latent_pass else 8) * H * H
-    achieved = flops_bwd / kstats[dom]
-    prof = profiled_traffic(args.workload, "train", dom)
     res = {
         "metric": "particle-steps/sec (2D Taylor-impact, training fwd+bwd+Adam)",
-        "value": n * args.steps * world / dt,
-        "unit": "particle-steps/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (0.5 mm Taylor-bar lattice + random-walk frames, random-walk training "
-                "noise; random-init weights)",
-        "config": {"workload": f"{args.workload}: 2D lattice {nx}x{ny} = {n} particles per GPU, r={radius}, "
-                               f"L={L}, H={H}, T={T_SEQ}, K=20, training step (noise+fwd+bwd+Adam)",
-                   "particles_per_gpu": n, "edges_per_gpu": E, "global_batch_graphs": world,
-                   "layers": L, "hidden": H, "radius": radius,
+        "value": n_global * steps / dt, "unit": "particle-steps/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": dt / steps * 1e3, "scaling": scaling, "dtype": "f32", "data": DATA,
+        "config": {"workload": desc, "particles_global": n_global, "particles_rank0": n, "edges_rank": E,
+                   "global_batch_graphs": len(all_graphs), "layers": L, "hidden": H, "radius": radius,
                    "parallelism": f"dp{world} (whole-graph, RCCL all-reduce)" if world > 1 else "single GPU"},
-        "M_edge_messages_per_s": E * L * args.steps * world / dt / 1e6,
-        "final_loss": loss,
-        "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved / 1e12,
-                     "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK,
-                     "traffic": prof[0] if prof else None,
-                     "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-                     "traffic_source": prof[1] if prof else None,
-                     "avg_launch_us": kstats[dom] * 1e6, "flops_per_launch": flops_bwd,
-                     "share_of_step": float(np.sum([a.elapsed_time(b) for a, b in timers[dom]])) / (dt_ev * 1e3)},
+        "M_edge_messages_per_s": E_all * L * steps / dt / 1e6,
+        "final_loss": float(out["loss"]),
+        "roofline": roofline(dom, flops_bwd, kstats[dom], "c2" if mode == "train" else "c3", "train"),
         "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
     }
-    if rank == 0 and world == 1 and args.cpu_steps > 0:
-        res["cpu_baseline"] = cpu_train_baseline(state0, seq, torch.from_numpy(strain_np), radius, L,
-                                                 args.cpu_steps, sim._normalization_stats)
+    res["roofline"]["share_of_step"] = float(np.sum([a.elapsed_time(b) for a, b in timers[dom]])) / (dt_ev * 1e3)
+    if rank == 0 and world == 1 and cpu_steps > 0:
+        res["cpu_baseline"] = cpu_train_baseline(state0, graphs, radius, L, max(3, cpu_steps // 2),
+                                                 sim._normalization_stats)
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     return res
 
@@ -363,6 +486,7 @@ def cpu_ms_train_baseline(sim, cfg, steps):
     bounded CPU sample of the same model (smaller lattice)."""
     from oracle import multi_scale_oracle as MO
     from oracle import sgnn_oracle as O
+    info = cpu_threads()
     dims, ns, win, mult, H, L, nmlp = cfg
     sdims = (24, 24, 16) if len(dims) == 3 else (60, 40)
     base = lattice(sdims)
@@ -389,152 +513,139 @@ def cpu_ms_train_baseline(sim, cfg, steps):
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": torch.get_num_threads(),
-            "kind": "port", "cpu_model": cpu_model(), "seconds": dt,
-            "sample": f"{steps} oracle multi-scale training steps (forward + torch autograd + Adam, torch "
-                      f"CPU fp32 restatement of sgnn/multi_scale) on a {'x'.join(map(str, sdims))} lattice "
-                      f"= {n} particles, same model, after 1 warm-up"}
+    return {"value": n * steps / dt, "unit": "particle-steps/s", **info, "seconds": dt,
+            "sample": f"{steps} oracle multi-scale training steps after 1 warm-up (forward + torch autograd + "
+                      f"Adam, torch CPU fp32 restatement of sgnn/multi_scale) on a "
+                      f"{'x'.join(map(str, sdims))} lattice = {n} particles, same model (per-particle rate "
+                      f"of a bounded sample, not the 1M config)"}
 
 
-def bench_ms_train(args, world, rank, device):
+def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps):
     from sgnn_amd.multi_scale.ms_training import MultiScaleTrainer
-    sim, seq, edges, desc, cfg = ms_setup(args.workload, device, args.seed, rank, T_SEQ + 1)
+    sim, seq, edges, desc, cfg = ms_setup(workload, device, seed, rank, T_SEQ + 1)
     n = seq.shape[0]
-    H, L = cfg[4], cfg[5]
+    H, L, nmlp = cfg[4], cfg[5], cfg[6]
     pos = torch.from_numpy(seq[:, :T_SEQ]).to(device)
     nxt = torch.from_numpy(seq[:, T_SEQ]).to(device)
     strain = torch.from_numpy(np.random.default_rng(rank).normal(0, 1, n).astype(np.float32)).to(device)
     tr = MultiScaleTrainer(sim, lr_init=1e-3)
-    for _ in range(args.warmup):
-        tr.train_step(pos, nxt, strain)
+    kw = dict(n_global=n * world, particle_offset=n * rank)
+    for _ in range(warmup):
+        tr.train_step(pos, nxt, strain, **kw)
     sync_barrier(world)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = tr.train_step(pos, nxt, strain)
+    for _ in range(steps):
+        out = tr.train_step(pos, nxt, strain, **kw)
     sync_barrier(world)
     dt = time.perf_counter() - t0
     timers = {}
-    for _ in range(min(args.steps, 3)):
-        tr.train_step(pos, nxt, strain, timers=timers)
+    for _ in range(min(steps, 3)):
+        tr.train_step(pos, nxt, strain, timers=timers, **kw)
     torch.cuda.synchronize()
     dt = max_over_ranks(dt, world, device)
     kstats = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in timers.items()}
-    nmlp = cfg[6]
     eb = ms_block_edges(edges, L)
     # edge backward per edge: last (+ middle) Linear W^T dy and dW, W1e^T dh and dW1e
     flops_bwd = eb / (L + 2) * (8 + (4 if nmlp == 2 else 0)) * H * H
     dom = "k_edge_bwd"
-    achieved = flops_bwd / kstats[dom]
     res = {
         "metric": "particle-steps/sec (multi-scale training fwd+bwd+Adam)",
-        "value": n * args.steps * world / dt, "unit": "particle-steps/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (0.5 mm lattice + random-walk frames; random-init weights)",
+        "value": n * steps * world / dt, "unit": "particle-steps/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": dt / steps * 1e3, "scaling": "weak", "dtype": "f32",
+        "data": DATA,
         "config": {"workload": desc + ", training step (noise+fwd+bwd+Adam)", "particles_per_gpu": n,
                    "edge_evaluations_per_step": eb, "global_batch_graphs": world,
                    "parallelism": f"dp{world} (whole-graph, RCCL all-reduce)" if world > 1 else "single GPU"},
-        "M_edge_messages_per_s": eb * args.steps * world / dt / 1e6,
+        "M_edge_messages_per_s": eb * steps * world / dt / 1e6,
         "final_loss": float(out["loss"]),
         "hbm_peak_gib": torch.cuda.max_memory_allocated(device) / 2 ** 30,
-        "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved / 1e12, "peak": MFMA_F32_PEAK / 1e12,
-                     "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK, "traffic": None,
-                     "avg_launch_us": kstats[dom] * 1e6, "flops_per_launch": flops_bwd},
+        "roofline": roofline(dom, flops_bwd, kstats.get(dom, float("nan")), workload, "train"),
         "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
     }
-    if rank == 0 and world == 1 and args.cpu_steps > 0:
-        res["cpu_baseline"] = cpu_ms_train_baseline(sim, cfg, max(1, args.cpu_steps // 3))
+    if rank == 0 and world == 1 and cpu_steps > 0:
+        res["cpu_baseline"] = cpu_ms_train_baseline(sim, cfg, max(3, cpu_steps // 2))
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     return res
 
 
-def bench_ms_rollout(args, world, rank, device):
-    sim, seq, edges, desc, cfg = ms_setup(args.workload, device, args.seed, rank, T_SEQ)
+def bench_ms_rollout(workload, steps, warmup, world, rank, device, seed):
+    sim, seq, edges, desc, cfg = ms_setup(workload, device, seed, rank, T_SEQ)
     n = seq.shape[0]
     L = cfg[5]
     cur = torch.from_numpy(seq).to(device).contiguous()
-    nxt_win = torch.empty_like(cur)
-    types_ = None
-
-    def run(k):
-        nonlocal cur, nxt_win
-        for _ in range(k):
-            sim._run(cur, types_, window_out=nxt_win)
-            cur, nxt_win = nxt_win, cur
-
     with torch.no_grad():
-        run(args.warmup)
+        runner = sim.rollout_runner(cur, None, steps)
+        for _ in range(max(1, -(-warmup // max(steps, 1)))):
+            runner.run(cur)
         sync_barrier(world)
         t0 = time.perf_counter()
-        run(args.steps)
+        runner.run(cur)
         sync_barrier(world)
         dt = time.perf_counter() - t0
     dt = max_over_ranks(dt, world, device)
     eb = ms_block_edges(edges, L)
-    return {"metric": "particle-steps/sec (multi-scale rollout)", "value": n * args.steps * world / dt,
-            "unit": "particle-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (0.5 mm lattice + random-walk frames; random-init weights)",
+    return {"metric": "particle-steps/sec (multi-scale rollout)", "value": n * steps * world / dt,
+            "unit": "particle-steps/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": DATA,
             "config": {"workload": desc + ", rollout", "particles": n,
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
-            "M_edge_messages_per_s": eb * args.steps * world / dt / 1e6}
+            "M_edge_messages_per_s": eb * steps * world / dt / 1e6}
 
 
-def main():
-    args = parse()
-    world, rank, local = init_dist()
+# ----------------------------------------------------------------------------- main
+def headline(r, args, world, metric, parallel):
+    res = {"metric": metric, "value": r["value"], "unit": r["unit"], "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": r["ms_per_step"], "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": DATA,
+           "config": {"workload": r["workload"] + ", autoregressive rollout (radius graph + features + EPD + "
+                                                  "Euler + window shift per step)",
+                      "particles_per_gpu": r["particles"], "edges_per_gpu": r["edges"],
+                      "parallelism": parallel},
+           "M_edge_messages_per_s": r["M_edge_messages_per_s"], "roofline": r["roofline"]}
+    if "cpu_baseline" in r:
+        res["cpu_baseline"] = r["cpu_baseline"]
+        res["speedup_vs_cpu"] = r["speedup_vs_cpu"]
+    return res
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_workers(args, argv)          # parent: no GPU call before this point
+    world, rank, local = init_dist(args)
+    if args.selftest_launch:
+        return selftest_launch(world, rank)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if args.workload is None:
-        args.workload = "c5" if args.mode.startswith("ms") else "c2"
+        args.workload = {"rollout": "c1_r15", "ms-train": "c5", "ms-rollout": "c5"}.get(args.mode, "c2")
+    parallel = f"replicas x{world} (one trajectory per GPU, no collective)" if world > 1 else "single GPU"
+    cs = args.cpu_steps
     if args.mode == "ms-train":
-        res = bench_ms_train(args, world, rank, device)
+        res = bench_ms_train(args.workload, args.steps, args.warmup, world, rank, device, args.seed, cs)
     elif args.mode == "ms-rollout":
-        res = bench_ms_rollout(args, world, rank, device)
-    elif args.mode == "train":
-        res = bench_train(args, world, rank, device)
-        if not args.no_rollout_extras and world == 1:
-            # the other BASELINE configs, each with its own bounded CPU baseline
-            res["rollout"] = {}
-            for wl, cs in (("c2", 2), ("c1_r15", 3), ("c4", 1)):
-                r = bench_rollout(wl, 20 if wl != "c4" else 10, 3, world, rank, device, args.seed,
-                                  cs if args.cpu_steps > 0 else 0)[0]
-                res["rollout"][wl] = r
-            import argparse as _ap
-            ms_args = _ap.Namespace(**{**vars(args), "workload": "c5", "steps": 3, "warmup": 1})
-            ms = bench_ms_train(ms_args, world, rank, device)
-            res["multi_scale_c5_train"] = {k: ms[k] for k in ("value", "unit", "ms_per_step", "config",
-                                                              "M_edge_messages_per_s", "hbm_peak_gib",
-                                                              "roofline", "cpu_baseline", "speedup_vs_cpu")
-                                           if k in ms}
+        res = bench_ms_rollout(args.workload, args.steps, args.warmup, world, rank, device, args.seed)
+    elif args.mode in ("train", "train-c3"):
+        res = bench_train(args.mode, args.steps, args.warmup, world, rank, device, args.seed, cs)
+        res["higher_is_better"], res["vs_baseline"] = True, None
     else:
-        r, timers, flops, edge_avg_s, E, n, radius, H, L = bench_rollout(
-            args.workload, args.steps, args.warmup, world, rank, device, args.seed, args.cpu_steps)
-        prof = profiled_traffic(args.workload, "rollout", "k_edge_layer")
-        res = {"metric": "particle-steps/sec (2D Taylor-impact rollout)", "value": r["value"],
-               "unit": "particle-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "f32",
-               "data": "synthetic (0.5 mm Taylor-bar lattice + random-walk frames; random-init weights)",
-               "config": {"workload": r["workload"] + ", rollout", "particles": n, "edges": E,
-                          "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
-               "M_edge_messages_per_s": r["M_edge_messages_per_s"],
-               "roofline": {"bound": "mfma", "kernel": "k_edge_layer", "achieved": flops / edge_avg_s / 1e12,
-                            "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s",
-                            "frac": flops / edge_avg_s / MFMA_F32_PEAK,
-                            "traffic": prof[0] if prof else None,
-                            "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-                            "traffic_source": prof[1] if prof else None,
-                            "avg_launch_us": edge_avg_s * 1e6, "flops_per_launch": flops}}
-        if "cpu_baseline" in r:
-            res["cpu_baseline"] = r["cpu_baseline"]
-            res["speedup_vs_cpu"] = r["speedup_vs_cpu"]
+        r = bench_rollout(args.workload, args.steps, args.warmup, world, rank, device, args.seed, cs)
+        res = headline(r, args, world, "particle-steps/sec (2D Taylor-impact rollout)", parallel)
+        if not args.no_extras:
+            res["training"] = bench_train("train", 10, 3, world, rank, device, args.seed, cs)
+            res["training_c3"] = bench_train("train-c3", 10, 3, world, rank, device, args.seed, 0)
+            res["rollout_extra"] = {}
+            for wl, st in (("c2", 20), ("c1_r06", 20), ("c4", 10)):
+                res["rollout_extra"][wl] = bench_rollout(wl, st, 3, world, rank, device, args.seed, cs)
+            res["multi_scale_c5_train"] = bench_ms_train("c5", 3, 1, world, rank, device, args.seed, cs)
     if rank == 0:
         print(json.dumps(res))
     if world > 1:
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -337,8 +337,9 @@ int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_strid
 
 /* Random-walk training noise (noise_utils.py:4-39) and the noisy window
  * (learned_simulator.py:467) in one pass: velocity increments
- * N(0, (std_last/sqrt(T-1))^2) from a Philox4x32-10 stream keyed by
- * (seed, offset), cumsum twice, noise[n][T][dim] with noise[:,0] = 0,
+ * N(0, (std_last/sqrt(T-1))^2) from a Philox4x32-10 stream keyed by seed
+ * and counted by the global particle index (offset + i: `offset` = index of
+ * this call's first particle in the data-parallel batch), cumsum twice, noise[n][T][dim] with noise[:,0] = 0,
  * noisy = pos_seq + noise.  The distribution of the reference's CPU-generator
  * draw, not its bit stream. */
 int sgnn_random_walk_noise(const float* pos_seq, int64_t n, int32_t T, int32_t dim,

@@ -4,8 +4,11 @@
 //   v_noise = cumsum_t n_v ;  p_noise = [0, cumsum_t v_noise]
 //   noise[i][t][c] = p_noise[t] ;  noisy = pos + noise
 // The reference draws n_v on torch's CPU generator; here the normals come
-// from a counter-based Philox4x32-10 stream keyed by (seed, offset) and
-// indexed by (particle, coordinate), Box-Muller transformed — the same
+// from a counter-based Philox4x32-10 stream keyed by seed and indexed by the
+// GLOBAL (particle, coordinate): particle = offset + local index, so a rank
+// that owns particles [offset, offset + n) of a data-parallel batch draws
+// exactly the slice of the noise one process would draw for the whole
+// concatenated batch (and ranks never share a stream).  Box-Muller transformed — the same
 // distribution, reproducible for a given seed, one pass over the window
 // instead of randn + two cumsums + cat + add.
 #include "common.h"
@@ -52,6 +55,7 @@ __global__ __launch_bounds__(256) void k_random_walk_noise(const float* __restri
   if (q >= n * dim) return;
   const int64_t i = q / dim;
   const int c = (int)(q - i * dim);
+  const uint64_t g = (uint64_t)q + offset * (uint64_t)dim;   // global (particle, coordinate)
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   float acc_v = 0.0f, acc_p = 0.0f;
   const float* src = pos + i * T * dim + c;
@@ -63,8 +67,7 @@ __global__ __launch_bounds__(256) void k_random_walk_noise(const float* __restri
   for (int t = 1; t < T; ++t) {
     const int k = t - 1;  // increment index
     if ((k & 3) == 0) {
-      const u32x4 r = philox4x32_10(u32x4{(uint32_t)q, (uint32_t)(q >> 32) ^ (uint32_t)(k >> 2),
-                                          (uint32_t)offset, (uint32_t)(offset >> 32)}, k0, k1);
+      const u32x4 r = philox4x32_10(u32x4{(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)(k >> 2), 0u}, k0, k1);
       box_muller(r.x, r.y, z[0], z[1]);
       box_muller(r.z, r.w, z[2], z[3]);
     }

@@ -23,7 +23,7 @@ import torch
 
 from .. import _hip, engine
 from .._hip import check, lib, stream_ptr
-from ..train import DataParallel, random_walk_noise
+from ..train import DataParallel, device_random_walk_noise
 from ..training import (DEFAULT_NSLAB, Adam, FlatParams, SlabArena, _saves, _Timer, emb_args,
                         embedding_backward, nslab_table)
 from . import ms_engine
@@ -274,7 +274,6 @@ class MultiScaleTrainer:
         self.nslab = nslab
         self.step = 0
         self._tw: Dict[tuple, MSTrainWorkspace] = {}
-        self._count_cache: Dict[int, int] = {}
 
     def workspace(self, n: int, T: int, device) -> MSTrainWorkspace:
         graphs = self.sim._csr(n, device)
@@ -289,20 +288,26 @@ class MultiScaleTrainer:
 
     def train_step(self, position: torch.Tensor, next_position: torch.Tensor, next_strain: torch.Tensor,
                    particle_types=None, noise: Optional[torch.Tensor] = None,
-                   n_global: Optional[int] = None, timers: Optional[dict] = None) -> dict:
+                   n_global: Optional[int] = None, particle_offset: Optional[int] = None,
+                   timers: Optional[dict] = None) -> dict:
+        """One step on this rank's graph.  DP bookkeeping as Trainer.train_step:
+        (n_global, particle_offset) from the caller or from one all_gather every
+        step; the default noise (fused Philox kernel) is counted by global
+        particle index, so every rank draws its own slice."""
         pos = position.to(torch.float32).contiguous()
+        n = pos.shape[0]
+        if n_global is None or particle_offset is None:
+            n_g, off = self.dp.layout(n, pos.device)
+            n_global = n_g if n_global is None else n_global
+            particle_offset = off if particle_offset is None else particle_offset
         if noise is None:
-            noise = random_walk_noise(pos, self.noise_std)
-        noise = noise.to(pos.device, torch.float32).contiguous()
-        noisy = (pos + noise).contiguous()
+            noise, noisy = device_random_walk_noise(pos, self.noise_std, offset=particle_offset)
+        else:
+            noise = noise.to(pos.device, torch.float32).contiguous()
+            noisy = (pos + noise).contiguous()
         inp, _ = self.sim._step_inputs(noisy, particle_types)
         n, T, _ = noisy.shape
         tw = self.workspace(n, T, pos.device)
-        if n_global is None:
-            n_global = self._count_cache.get(n)
-            if n_global is None:
-                n_global = self.dp.global_count(n, pos.device)
-                self._count_cache[n] = n_global
         rg, rm = self.sim._grid_radius(), self.sim._mesh_radius()
         emb = self.sim._particle_type_embedding.weight if self.sim._nparticle_types > 1 else None
         train_forward(self.gnn, inp, tw, rg, rm, timers=timers, emb_weight=emb)

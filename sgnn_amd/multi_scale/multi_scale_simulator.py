@@ -189,6 +189,14 @@ class MultiScaleSimulator(nn.Module):
                                window_out)
         return inp, pred, nxt
 
+    def rollout_runner(self, window: torch.Tensor, particle_types, nsteps: int):
+        """Device-resident rollout of `nsteps` predict_positions steps from
+        `window` (multi_scale_evaluate.py:163-214): every step's prediction is
+        written by the decoder kernel straight into its output slot and the
+        window shifts on the device, so the loop never waits for the host."""
+        inp, _ = self._step_inputs(window, particle_types)
+        return _MSRollout(self, inp.pos_seq, particle_types, nsteps)
+
     # ------------------------------------------------------------ reference API
     def _time_diff(self, position_sequence: torch.Tensor) -> torch.Tensor:
         """:384-388"""
@@ -294,3 +302,42 @@ class MultiScaleSimulator(nn.Module):
     def load(self, path: str):
         """:370-376 (weights_only: never unpickles code)."""
         self.load_state_dict(torch.load(path, map_location=torch.device("cpu"), weights_only=True))
+
+
+class _MSRollout:
+    """Autoregressive / one-step rollout buffers for MultiScaleSimulator
+    (two ping-pong windows, [nsteps, n, d] positions, [nsteps, n, d+1] raw
+    predictions).  No .item()/.cpu() inside the loop."""
+
+    def __init__(self, sim, window: torch.Tensor, particle_types, nsteps: int):
+        self.sim, self.types, self.nsteps = sim, particle_types, nsteps
+        n, T, d = window.shape
+        dev = window.device
+        self.win = [window.to(torch.float32).contiguous().clone(), torch.empty(n, T, d, device=dev)]
+        self.out_pos = torch.empty(max(nsteps, 1), n, d, dtype=torch.float32, device=dev)
+        self.out_pred = torch.empty(max(nsteps, 1), n, d + 1, dtype=torch.float32, device=dev)
+
+    def run(self, window: torch.Tensor = None, ground_truth: torch.Tensor = None):
+        """ground_truth [n, >= nsteps, d] switches to one_step mode: the window
+        is shifted with the true next position instead of the prediction
+        (multi_scale_evaluate.py:203-214).  Returns (positions [nsteps, n, d],
+        strain [nsteps, n]) on the device."""
+        sim = self.sim
+        if window is not None:
+            self.win[0].copy_(window)
+        n, T, d = self.win[0].shape
+        dev = self.win[0].device
+        gnn = sim._multi_scale_gnn
+        graphs = sim._csr(n, dev)
+        ws = sim._workspace(n, T, dev, graphs)
+        cur, nxt = self.win
+        for k in range(self.nsteps):
+            inp, use_emb = sim._step_inputs(cur, self.types)
+            ms_engine.forward_step(gnn, sim._particle_type_embedding.weight, use_emb, inp, graphs,
+                                   sim._grid_radius(), sim._mesh_radius(), ws, self.out_pred[k],
+                                   self.out_pos[k], nxt if ground_truth is None else None)
+            if ground_truth is not None:
+                nxt[:, :-1].copy_(cur[:, 1:])
+                nxt[:, -1].copy_(ground_truth[:, k])
+            cur, nxt = nxt, cur
+        return self.out_pos[:self.nsteps], self.out_pred[:self.nsteps, :, -1]

@@ -16,7 +16,7 @@ single-process gradient; every rank then applies the identical Adam update.
 from __future__ import annotations
 
 import math
-from typing import Dict, Optional
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -61,15 +61,26 @@ class DataParallel:
 
     def __init__(self, group=None):
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if on else 1
+        self.rank = dist.get_rank(group) if on else 0
+
+    def layout(self, n_local: int, device) -> Tuple[int, int]:
+        """(N_global, offset): the particle count over all ranks (the mean
+        denominator of train.py:268) and the index of this rank's first particle
+        in the concatenated batch (ranks in order).  ONE all_gather, issued by
+        every rank on every call, so ranks whose local counts differ or change
+        from step to step can never pair it with a different collective."""
+        if self.world == 1:
+            return int(n_local), 0
+        t = torch.tensor([int(n_local)], dtype=torch.int64, device=device)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        counts = torch.cat(out).tolist()
+        return int(sum(counts)), int(sum(counts[:self.rank]))
 
     def global_count(self, n_local: int, device) -> int:
-        """N_global = sum of particles over ranks (train.py:268 mean denominator)."""
-        if self.world == 1:
-            return int(n_local)
-        t = torch.tensor([float(n_local)], dtype=torch.float64, device=device)
-        dist.all_reduce(t, group=self.group)
-        return int(t.item())
+        return self.layout(n_local, device)[0]
 
     def allreduce_(self, *tensors: torch.Tensor) -> None:
         """SUM all-reduce (RCCL over xGMI on MI355X; gloo in CPU tests)."""
@@ -77,6 +88,22 @@ class DataParallel:
             return
         for t in tensors:
             dist.all_reduce(t, group=self.group)
+
+
+def split_batch(idx: Sequence[int], rank: int, world: int) -> Optional[List[int]]:
+    """This rank's whole graphs of one global batch: a contiguous, balanced
+    slice (rank r gets idx[s_r:s_{r+1}]), so the ranks' local batches
+    concatenated in rank order ARE the reference's concatenated batch
+    (collate, taylor_impact_data_loader.py:243-284).  None when the batch has
+    fewer graphs than ranks (an epoch's short last batch): every rank sees the
+    same idx, so every rank skips it together and no collective is left
+    unmatched."""
+    idx = list(idx)
+    if len(idx) < world:
+        return None
+    q, r = divmod(len(idx), world)
+    start = rank * q + min(rank, r)
+    return idx[start:start + q + (1 if rank < r else 0)]
 
 
 class Trainer:
@@ -99,7 +126,6 @@ class Trainer:
         self.nslab = nslab
         self.step = 0
         self._tw: Dict[tuple, training.TrainWorkspace] = {}
-        self._count_cache: Dict[int, int] = {}
 
     def workspace(self, n: int, T: int, device) -> training.TrainWorkspace:
         cap = training.capacity(n)
@@ -116,23 +142,33 @@ class Trainer:
     def train_step(self, position: torch.Tensor, next_position: torch.Tensor,
                    next_strain: torch.Tensor, nparticles_per_example, particle_types=None,
                    noise: Optional[torch.Tensor] = None, n_global: Optional[int] = None,
-                   timers: Optional[dict] = None) -> dict:
+                   particle_offset: Optional[int] = None, timers: Optional[dict] = None) -> dict:
         """One optimisation step on this rank's graphs; returns device-side loss
-        terms (no host sync).  `noise` defaults to fresh random-walk noise."""
+        terms.  `noise` defaults to fresh random-walk noise.
+
+        Data parallel (world > 1): `n_global` is the particle count of the whole
+        global batch and `particle_offset` the index of this rank's first
+        particle in it.  A caller that knows the global batch (train() does)
+        passes both; otherwise one all_gather per step computes them (every rank
+        issues it every step: no rank-local caching that could desync the
+        collectives).  The noise stream is counted by global particle index, so
+        ranks draw disjoint slices of the one-process noise."""
         pos = position.to(torch.float32).contiguous()
+        n = pos.shape[0]
+        if n_global is None or particle_offset is None:
+            n_g, off = self.dp.layout(n, pos.device)
+            n_global = n_g if n_global is None else n_global
+            particle_offset = off if particle_offset is None else particle_offset
         if noise is None:       # fused: draw + cumsum twice + noisy window in one kernel
-            noise, noisy = device_random_walk_noise(pos, self.noise_std)
+            # the seed is a draw from torch's CPU generator: the same on every
+            # rank (it also drives the shared shuffle); the offset separates them
+            noise, noisy = device_random_walk_noise(pos, self.noise_std, offset=particle_offset)
         else:
             noise = noise.to(pos.device, torch.float32).contiguous()
             noisy = (pos + noise).contiguous()                      # learned_simulator.py:467
         inp, _ = self.sim._step_inputs(noisy, nparticles_per_example, particle_types)
         n, T, _ = noisy.shape
         tw = self.workspace(n, T, pos.device)
-        if n_global is None:
-            n_global = self._count_cache.get(n)
-            if n_global is None:
-                n_global = self.dp.global_count(n, pos.device)
-                self._count_cache[n] = n_global
         radius = self.sim._connectivity_radius
         emb = self.sim._particle_type_embedding.weight if self.sim._nparticle_types > 1 else None
         training.train_forward(self.epd, radius, inp, tw, timers=timers, emb_weight=emb)
@@ -274,14 +310,15 @@ def train(simulator, metadata: dict, device, config: dict, group=None, log_every
     nsteps = config["ntraining_steps"]
     while trainer.step < nsteps:
         for idx in samples.index_batches(config["batch_size"], shuffle=True, generator=generator):
-            mine = idx[rank::world]            # this rank's whole graphs of the global batch
-            if not mine:
-                raise ValueError(f"batch of {len(idx)} graphs cannot feed {world} ranks")
+            mine = split_batch(idx, rank, world)    # this rank's whole graphs of the global batch
+            if mine is None:
+                continue                            # short last batch: skipped by every rank alike
             batch = samples.batch(mine)
             inp, outp = batch["input"], batch["output"]
             out = trainer.train_step(inp["positions"], outp["next_position"], outp["next_strain"],
                                      inp["n_particles_per_example"].tolist(), inp["particle_type"],
-                                     n_global=samples.count(idx))
+                                     n_global=samples.count(idx),
+                                     particle_offset=samples.count(idx[:idx.index(mine[0])]))
             step = trainer.step
             if step % log_every == 0:
                 history.append((step, float(out["loss"])))

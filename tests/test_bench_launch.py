@@ -1,0 +1,33 @@
+"""bench.py's multi-rank launch (CPU, no GPU): `python bench.py --gpus 2`
+without a torch.distributed environment must start 2 ranks itself (as a child
+torch.distributed.run, before any GPU call), each joining one process group,
+and rank 0 must print one JSON line with n_gpus = 2.  The stub step
+(--selftest-launch) all-reduces a one over gloo instead of touching a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=240)
+
+
+def test_gpus_flag_launches_that_many_ranks():
+    p = _run(["--gpus", "2", "--selftest-launch"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout          # only rank 0 prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["allreduce_sum"] == 2.0 and out["ranks_env"] == "2"
+
+
+def test_gpus_flag_must_agree_with_world_size():
+    p = _run(["--gpus", "4", "--selftest-launch"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert "--gpus 4 but WORLD_SIZE=2" in p.stderr

@@ -92,3 +92,67 @@ def test_whole_graph_dp_matches_single_process():
         assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss)
     # every rank ends with the identical gradient -> identical Adam update
     np.testing.assert_array_equal(res[0][2], res[1][2])
+
+
+def _layout_worker(rank, world, port, q):
+    """Ragged, changing per-rank counts: rank 0 repeats n, rank 1 changes it
+    every step.  Every step = layout (one all_gather) + one gradient-sized
+    all_reduce; a rank-local cache would pair different collectives here."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sgnn_amd.train import DataParallel
+    dp = DataParallel()
+    seen = []
+    for step in range(6):
+        n_local = 100 if rank == 0 else 50 + 7 * step
+        n_global, offset = dp.layout(n_local, "cpu")
+        g = torch.full((1000,), float(rank + 1))
+        dp.allreduce_(g)
+        seen.append((n_global, offset, float(g[0])))
+    q.put((rank, seen))
+    dist.destroy_process_group()
+
+
+def test_layout_never_desyncs_with_ragged_changing_counts():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_layout_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for step in range(6):
+        n1 = 50 + 7 * step
+        assert res[0][step] == (100 + n1, 0, 3.0)
+        assert res[1][step] == (100 + n1, 100, 3.0)
+
+
+def test_split_batch_contiguous_balanced_and_skips_short_batches():
+    from sgnn_amd.train import split_batch
+    for n, world in ((8, 8), (8, 3), (7, 2), (5, 4), (2, 2)):
+        idx = list(range(100, 100 + n))
+        parts = [split_batch(idx, r, world) for r in range(world)]
+        assert sum(parts, []) == idx                       # rank order = concatenation order
+        sizes = [len(p) for p in parts]
+        assert max(sizes) - min(sizes) <= 1 and min(sizes) >= 1
+    # an epoch's short last batch (fewer graphs than ranks): every rank skips it
+    assert all(split_batch([3], r, 2) is None for r in range(2))
+    assert split_batch([3], 0, 1) == [3]
+
+
+def test_dp_epoch_with_odd_sample_count_has_matching_collectives():
+    """train()'s batching at world 2, batch_size 2 and an odd sample count: the
+    last batch holds 1 graph; both ranks must skip it (no rank left waiting
+    in a collective), and every other batch feeds both ranks."""
+    from sgnn_amd.train import split_batch
+    g = torch.Generator().manual_seed(0)
+    sampler = torch.utils.data.RandomSampler(range(9), generator=g)
+    batches = list(torch.utils.data.BatchSampler(sampler, 2, drop_last=False))
+    plans = [[split_batch(b, r, 2) for b in batches] for r in range(2)]
+    steps = [[p is not None for p in plan] for plan in plans]
+    assert steps[0] == steps[1]                            # same number of collectives per rank
+    assert steps[0].count(False) == 1 and steps[0][-1] is False

@@ -38,6 +38,21 @@ def test_random_walk_noise_distribution_and_structure():
     assert torch.equal(a, noise) and not torch.equal(a, b) and not torch.equal(a, e)
 
 
+def test_noise_offset_is_the_global_particle_index():
+    """Data parallelism: a rank owning particles [a, b) of the concatenated
+    batch passes offset=a and draws exactly that slice of the one-process
+    noise (so ranks never share a stream and DP == one process)."""
+    from sgnn_amd.train import device_random_walk_noise
+    n, T, d = 10_000, 11, 2
+    pos = torch.randn(n, T, d, device="cuda")
+    full, _ = device_random_walk_noise(pos, 0.02, seed=77, offset=0)
+    for a, b in ((0, 3000), (3000, 3001), (3001, 10_000)):
+        part, _ = device_random_walk_noise(pos[a:b].contiguous(), 0.02, seed=77, offset=a)
+        assert torch.equal(part, full[a:b])
+    other, _ = device_random_walk_noise(pos[:3000].contiguous(), 0.02, seed=77, offset=3000)
+    assert not torch.equal(other, full[:3000])
+
+
 def test_trainer_default_noise_is_seeded_by_torch():
     from sgnn_amd import synthetic
     from sgnn_amd.learned_simulator import LearnedSimulator
