@@ -421,6 +421,124 @@ __global__ __launch_bounds__(256) void k_compact(int64_t n, int cap, const int32
   recv[e] = (int32_t)i;
 }
 
+// ---------------------------------------------------------------------------
+// Small-graph path (n <= kSmallN, e.g. the 2k-particle Taylor bar): two
+// launches instead of the cell pipeline's eleven.  Every workgroup stages the
+// whole position array in LDS (coalesced, SoA), and one wave per query walks
+// the candidates of the query's example IN ASCENDING INDEX, 64 per step,
+// straight out of LDS; it keeps the in-range ones in order and stops as soon
+// as it holds `cap` of them -- torch_cluster's CUDA rule (first K in ascending
+// index, strict <) needs no sort and no merge in this order.
+constexpr int kSmallN = 8192;
+constexpr int kSmallBlock = 512;  // 8 query waves per workgroup
+
+template <int DIM>
+__global__ __launch_bounds__(kSmallBlock) void k_radius_small(
+    const float* pos, int64_t stride, int n, const int64_t* ex_ptr, int n_ex, float r2, int cap,
+    int loop, int32_t* nbr, int32_t* deg) {
+  extern __shared__ float lds[];
+  float* sp = lds;                       // [DIM][n] SoA
+  __shared__ int32_t kept[kSmallBlock / 64][32];
+  for (int t = threadIdx.x; t < n * DIM; t += blockDim.x) {
+    const int i = t / DIM, d = t - i * DIM;
+    sp[d * n + i] = pos[(int64_t)i * stride + d];
+  }
+  __syncthreads();
+  const int lane = lane_id(), w = wave_id();
+  int32_t* kw = kept[w];
+  for (int i = blockIdx.x * (kSmallBlock / 64) + w; i < n; i += gridDim.x * (kSmallBlock / 64)) {
+    int lo = 0, hi = n_ex - 1;  // example of i: largest b with ex_ptr[b] <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (ex_ptr[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int jb = (int)ex_ptr[lo], je = (int)ex_ptr[lo + 1];
+    float pi[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) pi[d] = sp[d * n + i];
+    int cnt = 0;
+    for (int base = jb; base < je && cnt < cap; base += 64) {
+      const int j = base + lane;
+      bool in = false;
+      if (j < je) {
+        float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) {
+          const float t = __fsub_rn(sp[d * n + j], pi[d]);
+          s = __fadd_rn(s, __fmul_rn(t, t));
+        }
+        in = s < r2;
+      }
+      const uint64_t bal = __ballot(in);
+      const int slot = cnt + (int)__popcll(bal & ((1ull << lane) - 1ull));
+      if (in && slot < cap) kw[slot] = j;
+      cnt += (int)__popcll(bal);
+    }
+    wave_lds_sync();
+    cnt = min(cnt, cap);
+    int top = lane < cnt ? kw[lane] : INT32_MAX;
+    if (!loop) {  // torch_cluster: K+1 first-by-index, then drop the self loop
+      const uint64_t self = __ballot(lane < cnt && top == i);
+      if (self) {
+        const int at = __ffsll((long long)self) - 1;
+        const int nxt = __shfl(top, (lane + 1) & 63, 64);
+        if (lane >= at) top = (lane + 1 < cnt) ? nxt : INT32_MAX;
+        cnt -= 1;
+      }
+    }
+    if (lane < cnt) nbr[(int64_t)i * cap + lane] = top;
+    if (lane == 0) deg[i] = cnt;
+    wave_lds_sync();
+  }
+}
+
+// deg -> rowptr (exclusive scan, rowptr[n] = E) and the padded lists ->
+// receiver-sorted CSR.  n <= kSmallN: every workgroup scans all of deg in LDS
+// (8 rows per thread) -- cheaper than a grid-wide scan's extra launches --
+// then copies the rows of its own 32-row slice (thread = (row, slot), cap <=
+// 32); workgroup 0 writes rowptr.
+__global__ __launch_bounds__(1024) void k_csr_small(int n, int cap, const int32_t* nbr,
+                                                    const int32_t* deg, int32_t* rowptr,
+                                                    int32_t* send, int32_t* recv) {
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t srow[kSmallN + 1];
+  const int base = threadIdx.x * 8;
+  int32_t v[8], s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[k] = base + k < n ? deg[base + k] : 0;
+    s += v[k];
+  }
+  const int lane = lane_id(), w = wave_id();
+  int32_t incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int32_t run = incl - s;
+  for (int k = 0; k < w; ++k) run += wsum[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (base + k <= n) srow[base + k] = run;  // index n gets E (items past n add 0)
+    run += v[k];
+  }
+  if (base + 8 == n) srow[n] = run;  // n == 8192: index n lies past every thread's range
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i <= n; i += blockDim.x) rowptr[i] = srow[i];
+  const int i = blockIdx.x * 32 + (threadIdx.x >> 5), t = threadIdx.x & 31;
+  if (i < n) {
+    const int r0 = srow[i];
+    if (t < srow[i + 1] - r0) {
+      send[r0 + t] = nbr[i * cap + t];
+      recv[r0 + t] = i;
+    }
+  }
+}
+
 struct RadiusWs {
   uint32_t nbuckets;  // cell capacity (cells of all examples)
   int32_t *count, *fill, *start, *bucket_of, *ex_of, *order, *nbr, *deg, *partials;
@@ -503,10 +621,27 @@ extern "C" int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n
   if (!pos || !ex_ptr || !workspace || !rowptr || !send || !recv)
     return set_error(SGNN_ERR_INVALID, "radius_graph: null pointer");
   RadiusWs w = radius_layout(n, K, loop, workspace);
+  const float r2 = radius * radius;
+  if (n <= kSmallN) {  // small graphs: brute force over LDS in index order, two launches
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 7) / 8, 512);
+    const size_t lds = sizeof(float) * (size_t)n * dim;
+    const int nn = (int)n;
+    auto go = [&](auto kern) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(float) * kSmallN * 3));
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kSmallBlock), lds, stream, pos, pos_stride, nn, ex_ptr, n_ex,
+                         r2, cap, loop, w.nbr, w.deg);
+    };
+    if (dim == 1) go(k_radius_small<1>);
+    else if (dim == 2) go(k_radius_small<2>);
+    else go(k_radius_small<3>);
+    hipLaunchKernelGGL(k_csr_small, dim3((unsigned)((n + 31) / 32)), dim3(1024), 0, stream, nn, cap, w.nbr,
+                       w.deg, rowptr, send, recv);
+    return check_launch("radius_graph(small)");
+  }
   if ((int64_t)n_ex > (int64_t)w.nbuckets)
     return set_error(SGNN_ERR_UNSUPPORTED, "radius_graph: more examples than cell capacity (2n)");
   const float cell0 = radius * 1.01f;  // margin keeps |dp| < r inside +-1 cell under rounding
-  const float r2 = radius * radius;
   const int64_t max_cells = w.nbuckets;
   const unsigned nblk = (unsigned)((n + 255) / 256);
   (void)hipMemsetAsync(w.count, 0, sizeof(int32_t) * (2 * (size_t)w.nbuckets + 2 + 16), stream);

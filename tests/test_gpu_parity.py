@@ -97,12 +97,16 @@ def test_large_against_oracle(nx, ny, radius, n_ex):
 
 
 def test_radius_graph_random_vs_bruteforce():
-    """Random clouds, several examples, loop on/off, cap binding, a NaN particle."""
+    """Random clouds, several examples, loop on/off, cap binding, a NaN particle;
+    sizes on both sides of the small-graph path's limit (n <= 8192: LDS brute
+    force in index order; above: the cell-list pipeline)."""
     from oracle import sgnn_oracle as O
     from sgnn_amd import engine
     g = torch.Generator().manual_seed(3)
     for trial, (n, dim, r, loop) in enumerate([(700, 2, 0.9, True), (500, 3, 1.3, True),
-                                               (600, 2, 3.0, False), (400, 3, 0.5, False)]):
+                                               (600, 2, 3.0, False), (400, 3, 0.5, False),
+                                               (8192, 3, 0.9, False), (9000, 2, 0.25, True),
+                                               (12000, 3, 1.2, False)]):
         pos = torch.rand(n, dim, generator=g) * 10.0
         pos[5] = float("nan")
         counts = [n // 3, n // 3, n - 2 * (n // 3)]
