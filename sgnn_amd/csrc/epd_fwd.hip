@@ -21,6 +21,7 @@
 #include "common.h"
 #include "../../include/sgnn.h"
 #include "sgnn_internal.h"
+#include "fwd16.h"
 
 namespace {
 
@@ -722,6 +723,13 @@ static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode
         (mode == 1 && dec_nlin == 3 && !saves->hd2))
       return set_error(SGNN_ERR_INVALID, "node_layer: saves");
     a.sv = *saves;
+  }
+  if (!train && H == 64) {  // inference: 16-node tiles, output units split over 4 waves (fwd16.hip)
+    sgnn::Node16Args b{a.x_in, a.agg, a.cin, a.cout, a.rowptr, a.n, a.w1, a.b1, a.wm, a.bm, a.w2, a.b2,
+                       a.g, a.bb, a.we, a.be, a.u, a.v, a.wd1, a.bd1, a.wdm, a.bdm, a.wd2, a.bd2,
+                       a.pos_seq, a.T, a.dim, a.acc_mean, a.acc_std, a.pred, a.next_pos,
+                       a.window_out, a.x_out};
+    return sgnn::node16_launch(b, mode, node_fn->nlin, static_cast<hipStream_t>(stream));
   }
   const size_t vec = 5 * H + 32 + 2 * H;
   const size_t dec_w2 = mode == 1 ? 32 * (H + 4) : 0;  // padded decoder last Linear
