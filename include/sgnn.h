@@ -170,6 +170,27 @@ int sgnn_node_layer_decode(const float* x_in, const float* agg, const float* cin
                            float* pred, float* next_pos, float* window_out,
                            const sgnn_saves* saves, void* stream);
 
+/* One whole InteractionNetwork.forward (graph_network.py:150-222, inference,
+ * hidden 64) in ONE launch: edge half + receiver sums + node half as above,
+ * without the agg/cin/cout round trip -- each workgroup owns a run of
+ * consecutive receivers and all of their (contiguous) CSR edges.  u_in/v_in
+ * are this layer's node halves, u_out/v_out receive the next layer's (they
+ * must be different buffers: other workgroups still read u_in/v_in).
+ * Replaces the pair sgnn_edge_layer + sgnn_node_layer(_decode). */
+int sgnn_interaction_layer(const float* x_in, const float* u_in, const float* v_in,
+                           const float* e0t, float e_scale, const int32_t* rowptr,
+                           const int32_t* send, const int32_t* recv, int64_t n,
+                           const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
+                           const sgnn_mlp* next_edge, float* x_out, float* u_out, float* v_out,
+                           void* stream);
+int sgnn_interaction_layer_decode(const float* x_in, const float* u_in, const float* v_in,
+                                  const float* e0t, float e_scale, const int32_t* rowptr,
+                                  const int32_t* send, const int32_t* recv, int64_t n,
+                                  const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
+                                  const sgnn_mlp* decoder, const float* pos_seq, int32_t T,
+                                  int32_t dim, const float* acc_mean, const float* acc_std,
+                                  float* pred, float* next_pos, float* window_out, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Whole-step drivers.  One call = one LearnedSimulator.predict_positions
  * (learned_simulator.py:413-438: radius graph, encoders, L interaction
@@ -204,6 +225,8 @@ typedef struct sgnn_step_ws { /* device buffers of one (n, T, dim, H, K) shape *
   int32_t *rowptr, *send, *recv;
   int64_t edge_cap;
   float *e0t, *x_a, *x_b, *u, *v, *agg, *cin, *cout;
+  float *u2, *v2; /* [n][H] second node-half buffers: with both set, H = 64 and n <= 8192 each
+                     layer runs as ONE sgnn_interaction_layer launch (u/v ping-pong); else two */
 } sgnn_step_ws;
 
 int sgnn_predict_positions(const sgnn_epd* model, const sgnn_step_in* in, const float* pos_seq,

@@ -54,7 +54,8 @@ class SgnnStepWs(ctypes.Structure):
     """struct sgnn_step_ws (include/sgnn.h)."""
     _fields_ = [("radius_ws", c_void_p), ("rowptr", c_void_p), ("send", c_void_p), ("recv", c_void_p),
                 ("edge_cap", c_int64), ("e0t", c_void_p), ("x_a", c_void_p), ("x_b", c_void_p),
-                ("u", c_void_p), ("v", c_void_p), ("agg", c_void_p), ("cin", c_void_p), ("cout", c_void_p)]
+                ("u", c_void_p), ("v", c_void_p), ("agg", c_void_p), ("cin", c_void_p), ("cout", c_void_p),
+                ("u2", c_void_p), ("v2", c_void_p)]
 
 
 class SgnnReduceDesc(ctypes.Structure):
@@ -94,6 +95,13 @@ SIGNATURES = {
                                               c_int64, P_MLP, P_MLP, c_void_p, c_int32, c_int32,
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p, P_SAVES, c_void_p]),
+    "sgnn_interaction_layer": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
+                                              c_void_p, c_void_p, c_int64, P_MLP, P_MLP, P_MLP, c_void_p,
+                                              c_void_p, c_void_p, c_void_p]),
+    "sgnn_interaction_layer_decode": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                                                     c_void_p, c_void_p, c_void_p, c_int64, P_MLP, P_MLP,
+                                                     P_MLP, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                                     c_void_p, c_void_p, c_void_p, c_void_p]),
     "sgnn_coo_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64]),
     "sgnn_coo_to_csr": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -632,6 +632,16 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
     if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "encode_nodes: saves");
     a.sv = *saves;
   }
+  if (!train && H == 64 && feat <= 48) {  // inference: 16-node tiles, units split over 4 waves (fwd16.hip)
+    sgnn::EncNode16Args b{};
+    b.nd.n = n; b.nd.wm = mid_w(enc); b.nd.bm = mid_b(enc); b.nd.w2 = last_w(enc); b.nd.b2 = last_b(enc);
+    b.nd.g = enc->ln_g; b.nd.bb = enc->ln_b; b.nd.we = edge0->w1; b.nd.be = edge0->b1;
+    b.nd.u = u; b.nd.v = v; b.nd.x_out = x0;
+    b.pos_seq = pos_seq; b.T = T; b.dim = dim; b.types = types; b.emb_w = emb_w; b.emb_dim = emb_dim;
+    b.use_emb = use_emb; b.vel_mean = vel_mean; b.vel_std = vel_std; b.wall_max = wall_max;
+    b.wall_div = wall_div; b.feat = feat; b.w1 = enc->w1; b.b1 = enc->b1;
+    return sgnn::enc_node16_launch(b, enc->nlin, static_cast<hipStream_t>(stream));
+  }
   const unsigned grid = persistent_grid(n, 32 * kWaves, 2);
   const int tkf = (feat + 31) / 32;
   const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + (H == 64 ? 3 * H * (H + 4) : 0) + 6 * H);
@@ -836,3 +846,76 @@ extern "C" int sgnn_encode_edge_features(const float* e, int32_t fe, const int32
   SGNN_DISPATCH_H_NL(H, enc->nlin, (go_encode_edges<TH_, NL_>(false, grid, lds, s, a)));
   return check_launch("encode_edge_features");
 }
+
+// ---------------------------------------------------------------------------
+// Fused InteractionNetwork layer (inference, H = 64): edge MLP + receiver sums
+// + node update in one launch (fwd16.hip k_layer16).  Nodes per workgroup
+// tile: enough tiles for two workgroups per CU, at most 16.
+static int layer_common(sgnn::Layer16Args& L, const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn, int mode,
+                        int dec_nlin, void* stream) {
+  using namespace sgnn;
+  const int H = node_fn ? node_fn->hidden : 0;
+  int st = check_mlp(node_fn, 2 * H, H, H, true, "interaction_layer: node MLP shape");
+  if (!st) st = check_mlp(edge_fn, 3 * H, H, H, true, "interaction_layer: edge MLP shape");
+  if (st) return st;
+  if (H != 64) return set_error(SGNN_ERR_UNSUPPORTED, "interaction_layer: fused layer needs hidden 64");
+  if (edge_fn->nlin != node_fn->nlin || (mode == 1 && dec_nlin != node_fn->nlin))
+    return set_error(SGNN_ERR_UNSUPPORTED, "interaction_layer: MLP depths differ");
+  Node16Args& a = L.nd;
+  a.w1 = node_fn->w1; a.b1 = node_fn->b1; a.w2 = last_w(node_fn); a.b2 = last_b(node_fn);
+  a.wm = mid_w(node_fn); a.bm = mid_b(node_fn); a.g = node_fn->ln_g; a.bb = node_fn->ln_b;
+  L.ewe = edge_fn->w1 + 2 * H; L.ewm = mid_w(edge_fn); L.ebm = mid_b(edge_fn);
+  L.ew2 = last_w(edge_fn); L.eb2 = last_b(edge_fn); L.eg = edge_fn->ln_g; L.ebb = edge_fn->ln_b;
+  L.nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, (a.n + 511) / 512));
+  return layer16_launch(L, mode, node_fn->nlin, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int sgnn_interaction_layer(const float* x_in, const float* u_in, const float* v_in,
+                                      const float* e0t, float e_scale, const int32_t* rowptr,
+                                      const int32_t* send, const int32_t* recv, int64_t n,
+                                      const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
+                                      const sgnn_mlp* next_edge, float* x_out, float* u_out,
+                                      float* v_out, void* stream) {
+  using namespace sgnn;
+  if (n <= 0) return SGNN_OK;
+  if (!x_in || !u_in || !v_in || !e0t || !rowptr || !send || !recv || !x_out || !u_out || !v_out ||
+      !next_edge || u_out == u_in || v_out == v_in)
+    return set_error(SGNN_ERR_INVALID, "interaction_layer: bad arguments (u/v out must not alias u/v in)");
+  const int H = node_fn ? node_fn->hidden : 0;
+  int st = check_mlp(next_edge, 3 * H, H, H, true, "interaction_layer: next edge MLP shape");
+  if (st) return st;
+  Layer16Args L{};
+  L.nd.x_in = x_in; L.nd.rowptr = rowptr; L.nd.n = n; L.nd.we = next_edge->w1; L.nd.be = next_edge->b1;
+  L.nd.u = u_out; L.nd.v = v_out; L.nd.x_out = x_out;
+  L.u_in = u_in; L.v_in = v_in; L.e0t = e0t; L.e_scale = e_scale; L.send = send; L.recv = recv;
+  return layer_common(L, edge_fn, node_fn, 0, 0, stream);
+}
+
+extern "C" int sgnn_interaction_layer_decode(const float* x_in, const float* u_in, const float* v_in,
+                                             const float* e0t, float e_scale, const int32_t* rowptr,
+                                             const int32_t* send, const int32_t* recv, int64_t n,
+                                             const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
+                                             const sgnn_mlp* decoder, const float* pos_seq, int32_t T,
+                                             int32_t dim, const float* acc_mean, const float* acc_std,
+                                             float* pred, float* next_pos, float* window_out,
+                                             void* stream) {
+  using namespace sgnn;
+  if (n <= 0) return SGNN_OK;
+  if (!x_in || !u_in || !v_in || !e0t || !rowptr || !send || !recv || !pred || dim < 1 || dim > 3 ||
+      (pos_seq && (!acc_mean || !acc_std || !next_pos || T < 2)))
+    return set_error(SGNN_ERR_INVALID, "interaction_layer_decode: bad arguments");
+  if (window_out && window_out == pos_seq)
+    return set_error(SGNN_ERR_INVALID, "interaction_layer_decode: window_out aliases pos_seq");
+  const int H = node_fn ? node_fn->hidden : 0;
+  int st = check_mlp(decoder, H, H, dim + 1, false, "interaction_layer_decode: decoder MLP shape");
+  if (st) return st;
+  Layer16Args L{};
+  L.nd.x_in = x_in; L.nd.rowptr = rowptr; L.nd.n = n;
+  L.nd.wd1 = decoder->w1; L.nd.bd1 = decoder->b1; L.nd.wd2 = last_w(decoder); L.nd.bd2 = last_b(decoder);
+  L.nd.wdm = mid_w(decoder); L.nd.bdm = mid_b(decoder);
+  L.nd.pos_seq = pos_seq; L.nd.T = T; L.nd.dim = dim; L.nd.acc_mean = acc_mean; L.nd.acc_std = acc_std;
+  L.nd.pred = pred; L.nd.next_pos = next_pos; L.nd.window_out = window_out; L.nd.x_out = nullptr;
+  L.u_in = u_in; L.v_in = v_in; L.e0t = e0t; L.e_scale = e_scale; L.send = send; L.recv = recv;
+  return layer_common(L, edge_fn, node_fn, 1, decoder->nlin, stream);
+}
+

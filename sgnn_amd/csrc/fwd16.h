@@ -29,4 +29,38 @@ struct Node16Args {
 // Launches the H = 64 kernel (nl = Linear layers per MLP, 2 or 3).
 int node16_launch(const Node16Args& a, int mode, int nl, hipStream_t stream);
 
+// One whole InteractionNetwork layer (graph_network.py:150-222) in ONE launch:
+// a workgroup owns `nt` consecutive receivers, runs the edge MLP over all of
+// their incoming edges (a contiguous range of the receiver-sorted CSR), sums
+// the messages in LDS, and applies the node update of node16 to them.  Reads
+// u_in / v_in (this layer's node halves), writes nd.u / nd.v (the next
+// layer's) -- distinct buffers, since other workgroups still gather u_in.
+struct Layer16Args {
+  Node16Args nd;
+  const float *u_in, *v_in, *e0t;
+  float e_scale;
+  const int32_t *send, *recv;
+  const float *ewe, *ewm, *ebm, *ew2, *eb2, *eg, *ebb;  // edge MLP (ewe = W1 + 2H, ld 3H)
+  int nt;
+};
+
+int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t stream);
+
+// Encoder, node side (learned_simulator.py:256-290 features -> Encoder.node_fn,
+// graph_network.py:86-90) + the first layer's u/v; nd carries the encoder's
+// tail Linear(s)/LayerNorm, edge0's first Linear (we, be), x_out = x0, u, v.
+struct EncNode16Args {
+  Node16Args nd;
+  const float* pos_seq;
+  int T, dim;
+  const int64_t* types;
+  const float* emb_w;
+  int emb_dim, use_emb;
+  const float *vel_mean, *vel_std;
+  float wall_max, wall_div;
+  int feat;
+  const float *w1, *b1;  // encoder first Linear [H][feat]
+};
+int enc_node16_launch(const EncNode16Args& a, int nl, hipStream_t stream);
+
 }  // namespace sgnn

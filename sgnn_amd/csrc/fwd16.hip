@@ -139,114 +139,403 @@ SGNN_DEV void load_agg16(f32x4 (&ag)[KQ], const Node16Args& a, int64_t i, int g)
 
 SGNN_DEV float comp(f32x4 v, int c) { return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3]; }
 
+// Node-side weights of one wave's 16 output rows (node MLP, then the next
+// edge MLP's node halves or the decoder), resident for the whole launch.
+template <int NL, int MODE>
+struct NodeW {
+  f32x4 w1a[KQ], w1x[KQ], wm[KQ], w2[KQ], wa[KQ], wmd[KQ], wb[KQ];
+  f32x4 vb1, vb2, vg, vbb, vbm, vba, vbmd, vbo;
+  SGNN_DEV void load(const Node16Args& a, int b, int j, int g) {
+    const int urow = 16 * b + j, ucol = 16 * b + 4 * g;
+    load_wrow(w1a, a.w1, 2 * H, urow, 0, g);
+    load_wrow(w1x, a.w1, 2 * H, urow, H, g);
+    vb1 = ld4(a.b1 + ucol);
+    load_tail(a, b, j, g);
+  }
+  // everything after the first Linear (the encoder supplies its own first Linear)
+  SGNN_DEV void load_tail(const Node16Args& a, int b, int j, int g) {
+    const int urow = 16 * b + j, ucol = 16 * b + 4 * g;
+    if (NL == 3) load_wrow(wm, a.wm, H, urow, 0, g);
+    load_wrow(w2, a.w2, H, urow, 0, g);
+    vb2 = ld4(a.b2 + ucol);
+    vg = ld4(a.g + ucol);
+    vbb = ld4(a.bb + ucol);
+    vbm = NL == 3 ? ld4(a.bm + ucol) : zero4();
+    vbmd = zero4();
+    vbo = zero4();
+    if (MODE == 0) {  // next edge MLP: u = W1_i x + b1 (cols 0..H), v = W1_j x (cols H..2H)
+      load_wrow(wa, a.we, 3 * H, urow, 0, g);
+      load_wrow(wb, a.we, 3 * H, urow, H, g);
+      vba = ld4(a.be + ucol);
+    } else {          // decoder: H -> H (-> H) -> dim + 1, no LayerNorm
+      load_wrow(wa, a.wd1, H, urow, 0, g);
+      vba = ld4(a.bd1 + ucol);
+      if (NL == 3) {
+        load_wrow(wmd, a.wdm, H, urow, 0, g);
+        vbmd = ld4(a.bdm + ucol);
+      }
+      load_wrow(wb, a.wd2, H, j, 0, g, j <= a.dim);  // output rows 0..dim of a 16-row tile
+#pragma unroll
+      for (int c = 0; c < 4; ++c) vbo[c] = 4 * g + c <= a.dim ? a.bd2[4 * g + c] : 0.0f;
+    }
+  }
+};
+
+// The node update of 16 items (node i on lane row j; `valid` false on padding
+// rows) from their aggregated messages `ag` (full rows): node MLP + LN +
+// residual -> x_out, then u/v (mode 0) or decoder + integrator (mode 1).
+// bufs: kBufs exchange buffers [16][LDX] (every wave of the workgroup calls).
+// x rows of the 16 items (B layout) and this wave's own units (residual).
+SGNN_DEV void load_x16(const Node16Args& a, int64_t ic, int b, int g, f32x4 (&xr)[KQ], f32x4& xo) {
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) xr[q] = ld4(a.x_in + ic * H + 16 * q + 4 * g);
+  xo = ld4(a.x_in + ic * H + 16 * b + 4 * g);
+}
+
+template <int NL, int MODE>
+SGNN_DEV void node_tail(const Node16Args& a, const NodeW<NL, MODE>& W, float (*bufs)[16 * LDX], int64_t i,
+                        bool valid, f32x4 h, f32x4 xo, int b, int j, int g);
+
+template <int NL, int MODE>
+SGNN_DEV void node_tile(const Node16Args& a, const NodeW<NL, MODE>& W, float (*bufs)[16 * LDX], int64_t i,
+                        bool valid, const f32x4 (&ag)[KQ], const f32x4 (&xr)[KQ], f32x4 xo, int b, int j,
+                        int g) {
+  const f32x4 h = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));  // graph_network.py:220
+  node_tail<NL, MODE>(a, W, bufs, i, valid, h, xo, b, j, g);
+}
+
+// From the first Linear's post-ReLU output h (own units) on: (middle Linear),
+// last Linear, LayerNorm, + xo (residual; zero in the encoder) -> x_out, then
+// u/v (mode 0) or decoder + integrator (mode 1).
+template <int NL, int MODE>
+SGNN_DEV void node_tail(const Node16Args& a, const NodeW<NL, MODE>& W, float (*bufs)[16 * LDX], int64_t i,
+                        bool valid, f32x4 h, f32x4 xo, int b, int j, int g) {
+  const int ucol = 16 * b + 4 * g;
+  f32x4 hr[KQ], yr[KQ];
+  xchg(bufs[0], j, ucol, g, h, hr);
+  f32x4 y;
+  if constexpr (NL == 3) {
+    f32x4 mr[KQ];
+    xchg(bufs[1], j, ucol, g, relu4(mm(W.vbm, W.wm, hr)), mr);
+    y = mm(W.vb2, W.w2, mr);
+  } else {
+    y = mm(W.vb2, W.w2, hr);
+  }
+  xchg(bufs[2], j, ucol, g, y, yr);
+  float mean, rstd;
+  ln_stats(yr, mean, rstd);
+  f32x4 xn;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xn[c] = (y[c] - mean) * rstd * W.vg[c] + W.vbb[c] + xo[c];  // LN (+ :176 residual)
+  if (valid && a.x_out) st4(a.x_out + i * H + ucol, xn);
+  f32x4 xnr[KQ];
+  xchg(bufs[3], j, ucol, g, xn, xnr);
+  if constexpr (MODE == 0) {
+    const f32x4 u = mm(W.vba, W.wa, xnr);
+    const f32x4 v = mm(zero4(), W.wb, xnr);
+    if (valid) {
+      st4(a.u + i * H + ucol, u);
+      st4(a.v + i * H + ucol, v);
+    }
+  } else {
+    f32x4 hdr[KQ];
+    xchg(bufs[4], j, ucol, g, relu4(mm(W.vba, W.wa, xnr)), hdr);
+    if constexpr (NL == 3) {
+      f32x4 hd2r[KQ];
+      xchg(bufs[5], j, ucol, g, relu4(mm(W.vbmd, W.wmd, hdr)), hd2r);
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) hdr[q] = hd2r[q];
+    }
+    const int D = a.dim;
+    if (b == 0) {
+      const f32x4 o = mm(W.vbo, W.wb, hdr);  // lanes g == 0 hold outputs 0..3
+      if (valid && g == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c <= D) a.pred[i * (D + 1) + c] = comp(o, c);
+        if (a.pos_seq) {  // learned_simulator.py:398-411
+          const float* p = a.pos_seq + i * a.T * D;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            if (c >= D) break;
+            const float acc = __fadd_rn(__fmul_rn(comp(o, c), a.acc_std[c]), a.acc_mean[c]);
+            const float pT = p[(a.T - 1) * D + c], pT1 = p[(a.T - 2) * D + c];
+            const float np = __fadd_rn(pT, __fadd_rn(__fsub_rn(pT, pT1), acc));
+            a.next_pos[i * D + c] = np;
+            if (a.window_out) a.window_out[(i * a.T + a.T - 1) * D + c] = np;
+          }
+        }
+      }
+    } else if (b == 1 && g == 0 && valid && a.pos_seq && a.window_out) {  // evaluate.py:136-139
+      const float* p = a.pos_seq + i * a.T * D;
+      float* w = a.window_out + i * a.T * D;
+      for (int k = 0; k < (a.T - 1) * D; ++k) w[k] = p[k + D];
+    }
+  }
+}
+
 template <int NL, int MODE>
 __global__ __launch_bounds__(kBlock16) void k_node16(Node16Args a) {
   __shared__ float xb[kBufs][16 * LDX];
   const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
-  const int urow = 16 * b + j;      // the W row this lane feeds as the A operand
-  const int ucol = 16 * b + 4 * g;  // the 4 output units this lane holds in D
-  // weights of this wave's 16 output rows, resident for the whole launch
-  f32x4 w1a[KQ], w1x[KQ], wm[KQ], w2[KQ], wa[KQ], wmd[KQ], wb[KQ];
-  load_wrow(w1a, a.w1, 2 * H, urow, 0, g);
-  load_wrow(w1x, a.w1, 2 * H, urow, H, g);
-  if (NL == 3) load_wrow(wm, a.wm, H, urow, 0, g);
-  load_wrow(w2, a.w2, H, urow, 0, g);
-  const f32x4 vb1 = ld4(a.b1 + ucol), vb2 = ld4(a.b2 + ucol);
-  const f32x4 vg = ld4(a.g + ucol), vbb = ld4(a.bb + ucol);
-  const f32x4 vbm = NL == 3 ? ld4(a.bm + ucol) : zero4();
-  f32x4 vba, vbmd = zero4(), vbo = zero4();
-  if (MODE == 0) {  // next edge MLP: u = W1_i x + b1 (cols 0..H), v = W1_j x (cols H..2H)
-    load_wrow(wa, a.we, 3 * H, urow, 0, g);
-    load_wrow(wb, a.we, 3 * H, urow, H, g);
-    vba = ld4(a.be + ucol);
-  } else {          // decoder: H -> H (-> H) -> dim + 1, no LayerNorm
-    load_wrow(wa, a.wd1, H, urow, 0, g);
-    vba = ld4(a.bd1 + ucol);
-    if (NL == 3) {
-      load_wrow(wmd, a.wdm, H, urow, 0, g);
-      vbmd = ld4(a.bdm + ucol);
-    }
-    load_wrow(wb, a.wd2, H, j, 0, g, j <= a.dim);  // output rows 0..dim of a 16-row tile
-#pragma unroll
-    for (int c = 0; c < 4; ++c) vbo[c] = 4 * g + c <= a.dim ? a.bd2[4 * g + c] : 0.0f;
-  }
-  float* bh = xb[0];
-  float* bm = xb[1];
-  float* by = xb[2];
-  float* bx = xb[3];
-  float* bd = xb[4];
-  float* bd2 = xb[5];
+  NodeW<NL, MODE> W;
+  W.load(a, b, j, g);
   for (int64_t tile = blockIdx.x; tile * 16 < a.n; tile += gridDim.x) {
     const int64_t i = tile * 16 + j;
     const bool valid = i < a.n;
-    const int64_t ic = valid ? i : a.n - 1;
-    f32x4 ag[KQ], xr[KQ];
-    load_agg16(ag, a, ic, g);
+    f32x4 ag[KQ], xr[KQ], xo;
+    load_agg16(ag, a, valid ? i : a.n - 1, g);
+    load_x16(a, valid ? i : 0, b, g, xr, xo);
+    node_tile<NL, MODE>(a, W, xb, i, valid, ag, xr, xo, b, j, g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused layer (edge MLP -> receiver sums in LDS -> node update), see fwd16.h.
+
+// e0 of edge e, units 16 q + 4 g .. +3 (32-edge MFMA-C-layout tiles)
+SGNN_DEV f32x4 ld_e0_edge(const float* e0t, int64_t e, int q, int g) {
+  const int64_t tile = e >> 5;
+  const int item = (int)(e & 31);
+  const int t = q >> 1, gg = 2 * (q & 1) + (g >> 1), hh = g & 1;
+  return ld4(e0t + tile * (32 * H) + (t * 4 + gg) * 256 + (item + 32 * hh) * 4);
+}
+
+// Row-local (16-lane) DPP shifts: lane j of a row receives lane j - d (shr)
+// or j + 1 (shl 1); lanes without a source keep `fill`.
+template <int D>
+SGNN_DEV int dpp_shr_c(int v, int fill) {
+  return __builtin_amdgcn_update_dpp(fill, v, 0x110 + D, 0xf, 0xf, false);
+}
+SGNN_DEV int dpp_row_shr(int v, int d, int fill) {
+  return d == 1 ? dpp_shr_c<1>(v, fill) : d == 2 ? dpp_shr_c<2>(v, fill) : d == 4 ? dpp_shr_c<4>(v, fill)
+                                                                                  : dpp_shr_c<8>(v, fill);
+}
+SGNN_DEV int dpp_row_shl1(int v, int fill) { return __builtin_amdgcn_update_dpp(fill, v, 0x101, 0xf, 0xf, false); }
+
+// One Linear over all H units of 16 items held as 4 unit tiles (lane (j, g):
+// units 16 t + 4 g + c of item j in acc[t][c]); A rows from an LDS image
+// [H][LDX]; B = x (the same tile layout: tile q supplies k = 16 q + 4 g + c).
+// Four independent accumulator chains, so the MFMAs issue back to back.
+SGNN_DEV void mm_full(f32x4 (&acc)[KQ], const float* Wl, const f32x4 (&x)[KQ], int j, int g) {
+  f32x4 w[2][KQ];  // the A rows of k-group q + 1 are read while group q multiplies
 #pragma unroll
-    for (int q = 0; q < KQ; ++q) xr[q] = ld4(a.x_in + ic * H + 16 * q + 4 * g);
-    const f32x4 xo = ld4(a.x_in + ic * H + ucol);  // residual: own units
-    f32x4 hr[KQ], yr[KQ];
-    const f32x4 h = relu4(mm_cat(vb1, w1a, ag, w1x, xr));  // graph_network.py:220
-    xchg(bh, j, ucol, g, h, hr);
-    f32x4 y;
-    if constexpr (NL == 3) {
-      f32x4 mr[KQ];
-      xchg(bm, j, ucol, g, relu4(mm(vbm, wm, hr)), mr);
-      y = mm(vb2, w2, mr);
-    } else {
-      y = mm(vb2, w2, hr);
+  for (int t = 0; t < KQ; ++t) w[0][t] = ld4(Wl + (16 * t + j) * LDX + 4 * g);
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    if (q + 1 < KQ) {
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) w[(q + 1) & 1][t] = ld4(Wl + (16 * t + j) * LDX + 16 * (q + 1) + 4 * g);
     }
-    xchg(by, j, ucol, g, y, yr);
-    float mean, rstd;
-    ln_stats(yr, mean, rstd);
-    f32x4 xn;
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) xn[c] = (y[c] - mean) * rstd * vg[c] + vbb[c] + xo[c];  // LN, :176 residual
-    if (valid && a.x_out) st4(a.x_out + i * H + ucol, xn);
-    f32x4 xnr[KQ];
-    xchg(bx, j, ucol, g, xn, xnr);
-    if constexpr (MODE == 0) {
-      const f32x4 u = mm(vba, wa, xnr);
-      const f32x4 v = mm(zero4(), wb, xnr);
-      if (valid) {
-        st4(a.u + i * H + ucol, u);
-        st4(a.v + i * H + ucol, v);
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) acc[t] = mfma16(w[q & 1][t][c], x[q][c], acc[t]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Stage a [H][H] weight block (row stride ldg, optional scale) into an LDS
+// image [H][LDX] in two parts: float4 loads into registers, later the LDS
+// stores (loads issued first, so the stores wait on one memory latency and
+// later-issued loads stay in flight).
+constexpr int kStagePer = H * H / 4 / kBlock16;
+SGNN_DEV void stage_w64_load(f32x4 (&v)[kStagePer], const float* src, int ldg) {
+#pragma unroll
+  for (int k = 0; k < kStagePer; ++k) {
+    const int idx = threadIdx.x + k * kBlock16, r = idx / (H / 4), c = (idx % (H / 4)) * 4;
+    v[k] = ld4(src + (int64_t)r * ldg + c);
+  }
+}
+SGNN_DEV void stage_w64_store(float* dst, const f32x4 (&v)[kStagePer], float scale) {
+#pragma unroll
+  for (int k = 0; k < kStagePer; ++k) {
+    const int idx = threadIdx.x + k * kBlock16, r = idx / (H / 4), c = (idx % (H / 4)) * 4;
+    st4(dst + r * LDX + c, v[k] * scale);
+  }
+}
+
+template <int NL, int MODE>
+__global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) void k_layer16(sgnn::Layer16Args a) {
+  // LDS: edge MLP weights (W1e pre-scaled by 2^k, exact) and per-wave
+  // receiver sums; the node phase's exchange buffers alias the sums (barriers
+  // separate the phases)
+  constexpr int NW = NL == 3 ? 3 : 2;
+  __shared__ float sw[NW][H * LDX];
+  __shared__ float svec[4][H];                    // b2, gamma, beta, bm
+  __shared__ float scratch[kBufs * 16 * LDX];  // per-wave receiver sums; = xb in the node phase
+  static_assert(kBufs >= kWaves16, "the per-wave sums fit the node buffers");
+  float* sums_all = scratch;
+  auto xb = reinterpret_cast<float (*)[16 * LDX]>(scratch);
+  const Node16Args& nd = a.nd;
+  const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
+  const int NT = a.nt;
+  // the first tile's edge range and first half are requested before the
+  // weight staging, so their dependent loads overlap it
+  int64_t tile = blockIdx.x;
+  int32_t ea = 0, eb = 0;
+  int r_n = 0, s_n = 0;
+  f32x4 x_n[KQ], uv_n[KQ];
+  auto load_half = [&](int32_t hs) {  // indices, e0 row, u[recv] + v[send] of edge hs + j
+    const int32_t e = hs + j;
+    const int32_t ec = e < eb ? e : eb - 1;
+    r_n = a.recv[ec];
+    s_n = a.send[ec];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) x_n[q] = ld_e0_edge(a.e0t, ec, q, g);
+#pragma unroll
+    for (int t = 0; t < KQ; ++t)
+      uv_n[t] = ld4(a.u_in + (int64_t)r_n * H + 16 * t + 4 * g) + ld4(a.v_in + (int64_t)s_n * H + 16 * t + 4 * g);
+  };
+  auto start_tile = [&](int64_t tl) {
+    const int64_t i0 = tl * NT;
+    ea = nd.rowptr[i0];
+    eb = nd.rowptr[min<int64_t>(i0 + NT, nd.n)];
+    if (ea + 16 * b < eb) load_half(ea + 16 * b);
+  };
+  f32x4 st0[kStagePer], st1[kStagePer], st2[kStagePer];
+  stage_w64_load(st0, a.ewe, 3 * H);
+  if (NL == 3) stage_w64_load(st1, a.ewm, H);
+  stage_w64_load(st2, a.ew2, H);
+  if (tile * NT < nd.n) start_tile(tile);
+  stage_w64_store(sw[0], st0, a.e_scale);
+  if (NL == 3) stage_w64_store(sw[1], st1, 1.0f);
+  stage_w64_store(sw[NW - 1], st2, 1.0f);
+  stage_vec(svec[0], a.eb2, H, H);
+  stage_vec(svec[1], a.eg, H, H);
+  stage_vec(svec[2], a.ebb, H, H);
+  stage_vec(svec[3], a.ebm, H, H);
+  NodeW<NL, MODE> NWt;
+  NWt.load(nd, b, j, g);
+  float* sums = sums_all + b * 16 * LDX;
+  for (; tile * NT < nd.n; tile += gridDim.x) {
+    __syncthreads();  // staging done / the previous node phase no longer reads the scratch
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) st4(sums + j * LDX + 16 * q + 4 * g, zero4());
+    const int64_t i0 = tile * NT;
+    const int64_t i = i0 + j;
+    const bool valid = j < NT && i < nd.n;
+    f32x4 xr[KQ], xo;  // the node phase's x rows, requested now
+    load_x16(nd, valid ? i : 0, b, g, xr, xo);
+    // edge phase: wave b takes the 16-edge halves b, b + 4, ... of the tile's
+    // receivers' (contiguous) edge range, all H units per wave, no barriers
+    for (int32_t hs = ea + 16 * b; hs < eb; hs += 16 * kWaves16) {
+      const bool ev = hs + j < eb;
+      const int r = r_n;
+      f32x4 x[KQ], acc[KQ];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        x[q] = x_n[q];
+        acc[q] = uv_n[q];
       }
-    } else {
-      f32x4 hdr[KQ];
-      xchg(bd, j, ucol, g, relu4(mm(vba, wa, xnr)), hdr);
+      if (hs + 16 * kWaves16 < eb) load_half(hs + 16 * kWaves16);
+      // first Linear: u[recv] + v[send] + 2^k W1_e e0 (graph_network.py:197 on cat[x_i, x_j, e])
+      mm_full(acc, sw[0], x, j, g);
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) x[t] = relu4(acc[t]);
       if constexpr (NL == 3) {
-        f32x4 hd2r[KQ];
-        xchg(bd2, j, ucol, g, relu4(mm(vbmd, wmd, hdr)), hd2r);
 #pragma unroll
-        for (int q = 0; q < KQ; ++q) hdr[q] = hd2r[q];
+        for (int t = 0; t < KQ; ++t) acc[t] = ld4(svec[3] + 16 * t + 4 * g);
+        mm_full(acc, sw[1], x, j, g);
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) x[t] = relu4(acc[t]);
       }
-      const int D = a.dim;
-      if (b == 0) {
-        const f32x4 o = mm(vbo, wb, hdr);  // lanes g == 0 hold outputs 0..3
-        if (valid && g == 0) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (c <= D) a.pred[i * (D + 1) + c] = comp(o, c);
-          if (a.pos_seq) {  // learned_simulator.py:398-411
-            const float* p = a.pos_seq + i * a.T * D;
+      for (int t = 0; t < KQ; ++t) acc[t] = ld4(svec[0] + 16 * t + 4 * g);
+      mm_full(acc, sw[NW - 1], x, j, g);
+      float mu, rs;
+      ln_stats(acc, mu, rs);
+      f32x4 m[KQ];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              if (c >= D) break;
-              const float acc = __fadd_rn(__fmul_rn(comp(o, c), a.acc_std[c]), a.acc_mean[c]);
-              const float pT = p[(a.T - 1) * D + c], pT1 = p[(a.T - 2) * D + c];
-              const float np = __fadd_rn(pT, __fadd_rn(__fsub_rn(pT, pT1), acc));
-              a.next_pos[i * D + c] = np;
-              if (a.window_out) a.window_out[(i * a.T + a.T - 1) * D + c] = np;
-            }
+      for (int t = 0; t < KQ; ++t) {
+        const f32x4 ga = ld4(svec[1] + 16 * t + 4 * g), be = ld4(svec[2] + 16 * t + 4 * g);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) m[t][c] = (acc[t][c] - mu) * rs * ga[c] + be[c];
+      }
+      // receiver runs of the half (recv sorted along the 16-lane rows):
+      // segmented inclusive scan with DPP row shifts, then the last lane of
+      // each run adds its total to the receiver's row of this wave's sums
+      const int rk = ev ? r : -1 - j;  // padding lanes: runs of their own
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1) {
+        const int pr = dpp_row_shr(rk, d, INT32_MIN);
+#pragma unroll
+        for (int t = 0; t < KQ; ++t)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float pv = __int_as_float(dpp_row_shr(__float_as_int(m[t][c]), d, 0));
+            m[t][c] = pr == rk ? m[t][c] + pv : m[t][c];
           }
-        }
-      } else if (b == 1 && g == 0 && valid && a.pos_seq && a.window_out) {  // evaluate.py:136-139
-        const float* p = a.pos_seq + i * a.T * D;
-        float* w = a.window_out + i * a.T * D;
-        for (int k = 0; k < (a.T - 1) * D; ++k) w[k] = p[k + D];
+      }
+      const int rn = dpp_row_shl1(rk, INT32_MIN);
+      if (ev && rn != rk) {
+        float* dst = sums + (r - (int)i0) * LDX + 4 * g;
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) st4(dst + 16 * t, ld4(dst + 16 * t) + m[t]);
       }
     }
+    __syncthreads();
+    if ((tile + gridDim.x) * NT < nd.n) start_tile(tile + gridDim.x);  // overlaps the node phase
+    // node phase: the messages summed over the waves in a fixed order
+    f32x4 ag[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      ag[q] = ld4(sums_all + j * LDX + 16 * q + 4 * g);
+#pragma unroll
+      for (int w = 1; w < kWaves16; ++w) ag[q] += ld4(sums_all + w * 16 * LDX + j * LDX + 16 * q + 4 * g);
+    }
+    __syncthreads();  // the node buffers alias the sums
+    node_tile<NL, MODE>(nd, NWt, xb, i, valid, ag, xr, xo, b, j, g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Encoders (inference).
+
+template <int NL, int KQF>
+__global__ __launch_bounds__(kBlock16) void k_enc_node16(sgnn::EncNode16Args a) {
+  __shared__ float xb[kBufs][16 * LDX];
+  const Node16Args& nd = a.nd;
+  const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
+  const int urow = 16 * b + j, ucol = 16 * b + 4 * g;
+  NodeW<NL, 0> W;
+  W.load_tail(nd, b, j, g);
+  f32x4 w1f[KQF];  // first Linear [H][feat] (feat not a multiple of 4: scalar loads)
+#pragma unroll
+  for (int q = 0; q < KQF; ++q)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int f = 16 * q + 4 * g + c;
+      w1f[q][c] = f < a.feat ? a.w1[(int64_t)urow * a.feat + f] : 0.0f;
+    }
+  const f32x4 vb1 = ld4(a.b1 + ucol);
+  const int D = a.dim, nvel = (a.T - 1) * D;
+  for (int64_t tile = blockIdx.x; tile * 16 < nd.n; tile += gridDim.x) {
+    const int64_t i = tile * 16 + j;
+    const bool valid = i < nd.n;
+    const int64_t ic = valid ? i : nd.n - 1;
+    const float* p = a.pos_seq + ic * a.T * D;
+    f32x4 xf[KQF];
+#pragma unroll
+    for (int q = 0; q < KQF; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * q + 4 * g + c;
+        float val = 0.0f;
+        if (f < nvel) {  // learned_simulator.py:258,272-278 normalised velocity history
+          const int t = f / D, cc = f - t * D;
+          const float vel = __fsub_rn(p[(t + 1) * D + cc], p[t * D + cc]);
+          val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[cc]), a.vel_std[cc]);
+        } else if (f == nvel) {  // :282-284 wall distance
+          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(p[(a.T - 1) * D], 2.0f), 0.0f), a.wall_max), a.wall_div);
+        } else if (a.use_emb && f < nvel + 1 + a.emb_dim) {  // :287-290 type embedding
+          val = a.emb_w[a.types[ic] * a.emb_dim + (f - nvel - 1)];
+        }
+        xf[q][c] = val;
+      }
+    const f32x4 h = relu4(mm(vb1, w1f, xf));
+    node_tail<NL, 0>(nd, W, xb, i, valid, h, zero4(), b, j, g);
   }
 }
 
@@ -263,6 +552,33 @@ int node16_launch(const Node16Args& a, int mode, int nl, hipStream_t s) {
   else if (nl == 2) hipLaunchKernelGGL((k_node16<2, 1>), dim3(grid), dim3(kBlock16), 0, s, a);
   else hipLaunchKernelGGL((k_node16<3, 1>), dim3(grid), dim3(kBlock16), 0, s, a);
   return check_launch("node_layer16");
+}
+
+int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t s) {
+  if (a.nd.n <= 0) return SGNN_OK;
+  if (a.nt < 1 || a.nt > 16) return set_error(SGNN_ERR_INVALID, "layer16: nodes per tile must be 1..16");
+  const int64_t tiles = (a.nd.n + a.nt - 1) / a.nt;
+  const unsigned grid = (unsigned)std::min<int64_t>(tiles, 512);
+  if (mode == 0 && nl == 2) hipLaunchKernelGGL((k_layer16<2, 0>), dim3(grid), dim3(kBlock16), 0, s, a);
+  else if (mode == 0) hipLaunchKernelGGL((k_layer16<3, 0>), dim3(grid), dim3(kBlock16), 0, s, a);
+  else if (nl == 2) hipLaunchKernelGGL((k_layer16<2, 1>), dim3(grid), dim3(kBlock16), 0, s, a);
+  else hipLaunchKernelGGL((k_layer16<3, 1>), dim3(grid), dim3(kBlock16), 0, s, a);
+  return check_launch("layer16");
+}
+
+int enc_node16_launch(const EncNode16Args& a, int nl, hipStream_t s) {
+  if (a.nd.n <= 0) return SGNN_OK;
+  const int kqf = (a.feat + 15) / 16;
+  if (kqf > 3) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes16: more than 48 node features");
+  const unsigned grid = (unsigned)std::min<int64_t>((a.nd.n + 15) / 16, 256 * 4);
+#define SGNN_ENC16(NL_, KQF_) hipLaunchKernelGGL((k_enc_node16<NL_, KQF_>), dim3(grid), dim3(kBlock16), 0, s, a)
+  if (nl == 2) {
+    if (kqf == 1) SGNN_ENC16(2, 1); else if (kqf == 2) SGNN_ENC16(2, 2); else SGNN_ENC16(2, 3);
+  } else {
+    if (kqf == 1) SGNN_ENC16(3, 1); else if (kqf == 2) SGNN_ENC16(3, 2); else SGNN_ENC16(3, 3);
+  }
+#undef SGNN_ENC16
+  return check_launch("encode_nodes16");
 }
 
 }  // namespace sgnn

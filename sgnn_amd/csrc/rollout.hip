@@ -28,6 +28,26 @@ extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in,
   float* x_in = ws->x_a;
   float* x_out = ws->x_b;
   float scale = 1.0f;
+  // small graphs (n <= 8192, hidden 64): one fused launch per layer (u/v ping-pong); larger graphs
+  // keep the edge / node kernel pair (more workgroups, no per-workgroup weight staging per node tile)
+  if (ws->u2 && ws->v2 && m->node[0].hidden == 64 && n <= 8192) {
+    float *u_in = ws->u, *v_in = ws->v, *u_out = ws->u2, *v_out = ws->v2;
+    for (int k = 0; k < m->nlayers; ++k, scale *= 2.0f) {
+      if (k < m->nlayers - 1) {
+        st = sgnn_interaction_layer(x_in, u_in, v_in, ws->e0t, scale, ws->rowptr, ws->send, ws->recv, n,
+                                    &m->edge[k], &m->node[k], &m->edge[k + 1], x_out, u_out, v_out, stream);
+        std::swap(x_in, x_out);
+        std::swap(u_in, u_out);
+        std::swap(v_in, v_out);
+      } else {
+        st = sgnn_interaction_layer_decode(x_in, u_in, v_in, ws->e0t, scale, ws->rowptr, ws->send, ws->recv,
+                                           n, &m->edge[k], &m->node[k], m->dec, pos_seq, T, d, in->acc_mean,
+                                           in->acc_std, pred, next_pos, window_out, stream);
+      }
+      if (st) return st;
+    }
+    return SGNN_OK;
+  }
   for (int k = 0; k < m->nlayers; ++k, scale *= 2.0f) {
     st = sgnn_edge_layer(ws->u, ws->v, ws->e0t, scale, ws->rowptr, ws->send, ws->recv, n, ws->edge_cap,
                          &m->edge[k], ws->agg, ws->cin, ws->cout, nullptr, stream);

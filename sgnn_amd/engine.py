@@ -25,6 +25,7 @@ from . import _hip
 from ._hip import SgnnMlp, check, lib, stream_ptr
 
 MAX_NUM_NEIGHBORS = 20  # learned_simulator.py:117
+FUSED_MAX_N = 8192      # fused per-layer kernel for graphs up to this size (sgnn_predict_positions)
 
 
 def _ptr(t: Optional[torch.Tensor]) -> int:
@@ -108,6 +109,11 @@ class StepWorkspace:
         self.x_b = torch.empty(n, hidden, **f32)
         self.u = torch.empty(n, hidden, **f32)
         self.v = torch.empty(n, hidden, **f32)
+        # second node-half buffers: small graphs at hidden 64 run each layer as one fused
+        # sgnn_interaction_layer launch (u/v ping-pong); the C driver applies the same limit
+        fused = hidden == 64 and n <= FUSED_MAX_N
+        self.u2 = torch.empty(n, hidden, **f32) if fused else None
+        self.v2 = torch.empty(n, hidden, **f32) if fused else None
         self.agg = torch.empty(n, hidden, **f32)
         self.cin = torch.empty(ntiles, hidden, **f32)
         self.cout = torch.empty(ntiles, hidden, **f32)
@@ -115,7 +121,8 @@ class StepWorkspace:
                                  send=self.send.data_ptr(), recv=self.recv.data_ptr(), edge_cap=self.edge_cap,
                                  e0t=self.e0t.data_ptr(), x_a=self.x_a.data_ptr(), x_b=self.x_b.data_ptr(),
                                  u=self.u.data_ptr(), v=self.v.data_ptr(), agg=self.agg.data_ptr(),
-                                 cin=self.cin.data_ptr(), cout=self.cout.data_ptr())
+                                 cin=self.cin.data_ptr(), cout=self.cout.data_ptr(),
+                                 u2=_ptr(self.u2), v2=_ptr(self.v2))
 
     def radius_ws_ptr(self) -> int:
         p = self.radius_ws.data_ptr()
@@ -289,6 +296,31 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
           "sgnn_encode_edges")
     x_in, x_out = ws.x_a, ws.x_b
     nl = len(pk.edge)
+    if ws.u2 is not None:   # hidden 64: one fused sgnn_interaction_layer launch per layer
+        uv_in, uv_out = (ws.u, ws.v), (ws.u2, ws.v2)
+        for k in range(nl):
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            if k < nl - 1:
+                check(L.sgnn_interaction_layer(x_in.data_ptr(), uv_in[0].data_ptr(), uv_in[1].data_ptr(),
+                                               ws.e0t.data_ptr(), float(2.0 ** k), ws.rowptr.data_ptr(),
+                                               ws.send.data_ptr(), ws.recv.data_ptr(), n, ctypes.byref(pk.edge[k]),
+                                               ctypes.byref(pk.node[k]), ctypes.byref(pk.edge[k + 1]),
+                                               x_out.data_ptr(), uv_out[0].data_ptr(), uv_out[1].data_ptr(), s),
+                      "sgnn_interaction_layer")
+                x_in, x_out = x_out, x_in
+                uv_in, uv_out = uv_out, uv_in
+            else:
+                check(L.sgnn_interaction_layer_decode(
+                    x_in.data_ptr(), uv_in[0].data_ptr(), uv_in[1].data_ptr(), ws.e0t.data_ptr(), float(2.0 ** k),
+                    ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n, ctypes.byref(pk.edge[k]),
+                    ctypes.byref(pk.node[k]), ctypes.byref(pk.dec), pos.data_ptr(), T, d, inp.acc_mean.data_ptr(),
+                    inp.acc_std.data_ptr(), pred.data_ptr(), next_pos.data_ptr(), _ptr(window_out), s),
+                    "sgnn_interaction_layer_decode")
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            timers.append((ev0, ev1))
+        return
     for k in range(nl):
         if timers is not None:
             ev0 = torch.cuda.Event(enable_timing=True)

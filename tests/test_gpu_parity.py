@@ -190,3 +190,41 @@ def test_device_rollout_runner(nsteps):
     scale = float(np.max(z["acc_std"]))
     _close(pos.cpu().numpy(), ref_pos.numpy(), atol=2 * nsteps * ATOL * scale, rtol=1e-6,
            what=f"device rollout {nsteps} positions")
+
+
+@pytest.mark.parametrize("dim,nmlp,dims,radius,n_ex,ntypes", [
+    (2, 2, (40, 30), 1.1, 3, 1),      # nmlp_layers = 2 (3-Linear MLPs), several examples
+    (3, 1, (16, 14, 12), 0.75, 1, 1),  # 3D at hidden 64
+    (2, 1, (60, 40), 15.0, 2, 3),     # cap binds, particle-type embeddings
+    (2, 1, (100, 82), 0.6, 1, 1),     # n = 8200 > 8192: the edge / node kernel pair
+])
+def test_inference_paths_against_oracle(dim, nmlp, dims, radius, n_ex, ntypes):
+    """predict_positions at hidden 64 on both inference paths (the fused
+    per-layer kernel for n <= 8192, the edge / node pair above) vs the oracle:
+    strain and next positions within the module's forward bound."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import synthetic
+    from sgnn_amd.learned_simulator import LearnedSimulator
+    lat = synthetic.lattice_2d if dim == 2 else synthetic.lattice_3d
+    seqs = [synthetic.trajectory(lat(*dims), 11, seed=40 + k) for k in range(n_ex)]
+    for k, sq in enumerate(seqs):
+        sq[..., 0] += 0.13 * k
+    seq = np.concatenate(seqs, 0)
+    counts = [s.shape[0] for s in seqs]
+    n = seq.shape[0]
+    st = synthetic.normalization_stats(dim, noise_std=0.02)
+    stats = {k: {kk: torch.from_numpy(vv) for kk, vv in v.items()} for k, v in st.items()}
+    torch.manual_seed(7)
+    emb = 16 if ntypes > 1 else 0
+    sim = LearnedSimulator(dim, 10 * dim + 1 + emb, dim + 1, 64, 5, nmlp, 64, radius, stats, ntypes, emb or 9)
+    state = {k: v.detach().clone() for k, v in sim.state_dict().items()}
+    types_ = torch.from_numpy(np.random.default_rng(1).integers(0, ntypes, n))
+    pos = torch.from_numpy(seq)
+    osim = O.OracleSimulator(state, dim, 5, radius, stats, ntypes, nmlp_layers=nmlp)
+    ref_next, ref_strain = osim.predict_positions(pos, counts, types_)
+    sim = sim.cuda()
+    nxt, strain = sim.predict_positions(pos.cuda(), counts, types_.cuda())
+    torch.cuda.synchronize()
+    _close(strain.cpu().numpy(), ref_strain.numpy(), what=f"n={n} dim={dim} nmlp={nmlp} strain")
+    scale = float(np.max(st["acceleration"]["std"]))
+    _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * scale, rtol=1e-6, what=f"n={n} next_pos")

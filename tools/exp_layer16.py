@@ -1,0 +1,36 @@
+"""Fused-layer experiment: time one sgnn_interaction_layer launch (HIP events,
+100 launches) at a bench workload."""
+import ctypes, os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench
+from sgnn_amd import engine, synthetic
+from sgnn_amd._hip import lib, check, stream_ptr
+
+wl = sys.argv[1]
+dims, radius, H, L = bench.WORKLOADS[wl]
+dev = torch.device("cuda", 0)
+sim = bench.quiet_decoder(bench.make_sim(H, L, radius, len(dims), dev, 0))
+seq = synthetic.trajectory(bench.lattice(dims), bench.T_SEQ, seed=1000)
+n = seq.shape[0]
+w0 = torch.from_numpy(seq).to(dev)
+types_ = torch.zeros(n, dtype=torch.long, device=dev)
+inp, use_emb = sim._step_inputs(w0, [n], types_)
+ws = sim._workspace(n, bench.T_SEQ, dev)
+pred = torch.empty(n, len(dims) + 1, device=dev); nxt = torch.empty(n, len(dims), device=dev)
+engine.forward_step(sim._encode_process_decode, sim._particle_type_embedding.weight, use_emb, radius, inp, ws, pred, nxt)
+pk = engine.ParamPack.get(sim._encode_process_decode)
+s = stream_ptr(dev)
+def call():
+    check(lib().sgnn_interaction_layer(ws.x_a.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), ws.e0t.data_ptr(), 2.0,
+                                       ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
+                                       ctypes.byref(pk.edge[1]), ctypes.byref(pk.node[1]), ctypes.byref(pk.edge[2]),
+                                       ws.x_b.data_ptr(), ws.u2.data_ptr(), ws.v2.data_ptr(), s), "layer")
+for _ in range(20): call()
+torch.cuda.synchronize()
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+a.record()
+for _ in range(100): call()
+b.record(); torch.cuda.synchronize()
+print(f"{wl}: {a.elapsed_time(b) / 100 * 1e3:.2f} us/launch (no instrumentation)")
