@@ -1,21 +1,25 @@
 // Radius-graph neighbour search for gfx950 (replaces torch_cluster.radius as
 // reached by sgnn/single_scale/learned_simulator.py:116-117).
 //
-// Pipeline (5-9 launches, no host sync, capturable in a hipGraph):
-//   0. k_bbox          bounding box of the finite coordinates (device atomics)
-//   1. k_cell_assign   particle -> (example, dense cell of side 1.01 r, grown
-//                      x2 until the grid fits the workspace); histogram
-//   2. scan            bucket counts -> bucket starts
-//   3. k_cell_scatter  counting-sort particle ids into bucket order
-//   4. k_radius_query  one wave per query particle: walks the 3^(d-1) row
-//                      spans of its neighbour cells as one concatenated list
-//                      (64 candidates per wave step), keeps in-range
-//                      same-example candidates, and maintains the `cap`
-//                      smallest sender ids with a 64-lane bitonic sort +
-//                      merge in registers (torch_cluster's CUDA rule: first K
-//                      in ascending index).  Writes deg and a padded list.
-//   5. scan            deg -> rowptr (rowptr[n] = E, left on the device)
-//   6. k_compact       padded lists -> receiver-sorted CSR (send, recv)
+// Small graphs (n <= 8192): k_radius_small (every workgroup stages all
+// positions in LDS; one wave per query scans its example in ascending index
+// and stops at the cap) + k_csr_small (scan + compaction): two launches.
+//
+// Large graphs (no host sync, capturable in a hipGraph):
+//   0. k_bbox             bounding box of the finite coordinates (device atomics)
+//   1. k_cell_assign      particle -> (example, dense cell of side 1.01 r, grown
+//                         x2 until the grid fits the workspace); histogram
+//   2. scan               cell counts -> cell starts
+//   3. k_cell_scatter     counting sort into cell order + a cell-ordered copy
+//                         of the positions (x, y, z, id)
+//   4. k_radius_query_lds LDS spatial binning: a workgroup per tile of 64
+//                         cells of one grid row stages the 3^(d-1) neighbour
+//                         row spans with coalesced float4 loads; one lane per
+//                         particle keeps the cap smallest in-range ids
+//                         (torch_cluster's CUDA rule: first K in ascending
+//                         index).  Writes deg and a padded list.
+//   5. scan               deg -> rowptr (rowptr[n] = E, left on the device)
+//   6. k_compact          padded lists -> receiver-sorted CSR (send, recv)
 #include "common.h"
 #include "../../include/sgnn.h"
 #include "sgnn_internal.h"
@@ -59,38 +63,21 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_block(const int32_t* in, in
   if (threadIdx.x == blockDim.x - 1) partials[blockIdx.x] = woff + incl;
 }
 
-// Exclusive scan of up to 1024*8 block totals in one block.
-__global__ __launch_bounds__(1024) void k_scan_partials(int32_t* partials, int nb) {
-  __shared__ int32_t wsum[16];
-  const int base = threadIdx.x * 8;
-  int32_t v[8], s = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    v[k] = base + k < nb ? partials[base + k] : 0;
-    s += v[k];
-  }
-  const int lane = threadIdx.x & 63, w = wave_id();
-  int32_t incl = s;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int32_t woff = 0;
-  for (int k = 0; k < w; ++k) woff += wsum[k];
-  int32_t run = woff + incl - s;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (base + k < nb) partials[base + k] = run;
-    run += v[k];
-  }
-}
-
+// Adds the exclusive prefix of the block totals: each block reduces the
+// totals of the blocks before it itself (<= 8192 of them), so the totals need
+// no scan launch of their own.
 __global__ __launch_bounds__(kScanBlock) void k_scan_add(int32_t* out, int64_t len,
                                                          const int32_t* partials) {
-  const int32_t add = partials[blockIdx.x];
+  __shared__ int32_t wsum[kScanBlock / 64];
+  int32_t s = 0;
+  for (int b = threadIdx.x; b < (int)blockIdx.x; b += blockDim.x) s += partials[b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane_id() == 0) wsum[wave_id()] = s;
+  __syncthreads();
+  int32_t add = 0;
+#pragma unroll
+  for (int k = 0; k < kScanBlock / 64; ++k) add += wsum[k];
   const int64_t base = (int64_t)blockIdx.x * kScanTile;
   for (int k = threadIdx.x; k < kScanTile; k += blockDim.x) {
     const int64_t i = base + k;
@@ -122,9 +109,6 @@ SGNN_DEV float ord2f(uint32_t o) {
 // bbox words: [0..2] = ~ord(min_d) (atomicMax of the complement = min),
 // [3..5] = ord(max_d), [6] = arrival counter, [8..15] = the derived Grid
 // (written by the last-arriving block: agent-scope atomics + fence fan-in).
-__global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, int64_t n, int dim,
-                                              int n_ex, float cell0, int64_t max_cells,
-                                              uint32_t* bbox);
 
 // Every thread derives the same grid from the bbox (identical float ops).
 SGNN_DEV Grid make_grid(const uint32_t (&bbox)[6], int dim, int n_ex, float cell0, int64_t max_cells) {
@@ -152,15 +136,18 @@ SGNN_DEV Grid make_grid(const uint32_t (&bbox)[6], int dim, int n_ex, float cell
   return G;
 }
 
-__global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, int64_t n, int dim,
+template <int DIM>
+__global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, int64_t n,
                                               int n_ex, float cell0, int64_t max_cells,
                                               uint32_t* bbox) {
+  constexpr int dim = DIM;
   __shared__ uint32_t red[6][4];
   __shared__ bool last;
   uint32_t v[6] = {0, 0, 0, 0, 0, 0};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    for (int d = 0; d < dim; ++d) {
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
       const float x = pos[i * stride + d];
       if (isfinite(x)) {
         const uint32_t o = f2ord(x);
@@ -243,170 +230,180 @@ SGNN_DEV int32_t wave_aggregated_inc(int32_t* counter, int32_t key, bool active)
   return slot;
 }
 
+// DIM is a template parameter: with a runtime dimension loop the compiler kept
+// the Grid in LDS and issued the coordinate loads one after another (measured
+// 25 us vs 4 us for 50k particles, tools/bench_assign.hip).
+template <int DIM>
 __global__ __launch_bounds__(256) void k_cell_assign(const float* pos, int64_t stride, int64_t n,
-                                                     int dim, const int64_t* ex_ptr, int n_ex,
+                                                     const int64_t* ex_ptr, int n_ex,
                                                      const uint32_t* bbox, int32_t* cell_of_p,
                                                      int32_t* ex_of, int32_t* count) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i0 < n;
   const int64_t i = active ? i0 : n - 1;
+  float x[DIM];
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) x[d] = pos[i * stride + d];
   const Grid G = *reinterpret_cast<const Grid*>(bbox + 8);
   int lo = 0, hi = n_ex - 1;  // largest b with ex_ptr[b] <= i
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (ex_ptr[mid] <= i) lo = mid; else hi = mid - 1;
   }
-  const float* p = pos + i * stride;
   int c[3] = {0, 0, 0};
-  for (int d = 0; d < dim; ++d) c[d] = cell_of(p[d], G.lo[d], G.inv_cell, G.g[d]);
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) c[d] = cell_of(x[d], G.lo[d], G.inv_cell, G.g[d]);
   const int32_t key = (int32_t)((((int64_t)lo * G.g[2] + c[2]) * G.g[1] + c[1]) * G.g[0] + c[0]);
   if (active) {
     cell_of_p[i] = key;
     ex_of[i] = lo;
+    // histogram only: a non-returning atomic (the slot is taken in k_cell_scatter)
+    __hip_atomic_fetch_add(&count[key], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  (void)wave_aggregated_inc(count, key, active);
 }
 
+template <int DIM>
 __global__ __launch_bounds__(256) void k_cell_scatter(int64_t n, const int32_t* cell_of_p,
                                                       const int32_t* start, int32_t* fill,
-                                                      int32_t* order) {
+                                                      int32_t* order, const float* pos, int64_t stride,
+                                                      f32x4* cpos) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < n;
   const int32_t b = active ? cell_of_p[i] : 0;
   const int32_t slot = wave_aggregated_inc(fill, b, active);
-  if (active) order[start[b] + slot] = (int32_t)i;
-}
-
-SGNN_DEV int bitonic_sort64(int key, int lane) {
+  if (active) {
+    const int32_t at = start[b] + slot;
+    order[at] = (int32_t)i;
+    if (cpos) {  // cell-ordered copy (x, y, z, id): the LDS-binned query stages contiguous spans of it
+      f32x4 v = {0.0f, 0.0f, 0.0f, __int_as_float((int)i)};
 #pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int other = __shfl_xor(key, j, 64);
-      const bool up = (lane & k) == 0;
-      const bool lower = (lane & j) == 0;
-      key = (lower == up) ? min(key, other) : max(key, other);
+      for (int d = 0; d < DIM; ++d) v[d] = pos[i * stride + d];
+      cpos[at] = v;
     }
   }
-  return key;
 }
 
-SGNN_DEV int bitonic_merge64(int key, int lane) {
+// ---------------------------------------------------------------------------
+// LDS-binned query (large graphs): a workgroup owns a tile of kTX consecutive
+// cells of one grid row (same example, z, y).  Its candidates -- the
+// 3^(dim-1) neighbour rows over cells [x0 - 1, x0 + kTX] -- are contiguous
+// spans of the cell-ordered copy `cpos`, staged once into LDS with coalesced
+// float4 loads together with the cell starts of those spans; every particle of
+// the tile's own cells is then one lane, which walks its 3^dim neighbour
+// cells out of LDS and keeps the `cap` smallest in-range ids in a sorted
+// register list (torch_cluster's rule: first K by ascending index).  A tile
+// whose candidates overflow the LDS capacity reads the same spans from HBM.
+constexpr int kTX = 64;
+constexpr int kQBlock = 256;
+constexpr int kLdsCand = 3072;   // staged candidates (48 KB of float4)
+constexpr int kMaxCap = 32;
+
+SGNN_DEV void sorted_insert(int (&top)[kMaxCap], int x) {
+  // keep top[] ascending: x shifts the larger entries one slot up
 #pragma unroll
-  for (int j = 32; j > 0; j >>= 1) {
-    const int other = __shfl_xor(key, j, 64);
-    key = ((lane & j) == 0) ? min(key, other) : max(key, other);
+  for (int s = kMaxCap - 1; s > 0; --s) {
+    const int lo = top[s - 1];
+    top[s] = x < lo ? lo : (x < top[s] ? x : top[s]);
   }
-  return key;
+  top[0] = x < top[0] ? x : top[0];
 }
 
-__global__ __launch_bounds__(256) void k_radius_query(
-    const float* pos, int64_t stride, int64_t n, int dim, float r2,
-    const uint32_t* bbox, const int32_t* cell_of_p, const int32_t* ex_of,
-    const int32_t* start, const int32_t* order, int cap, int loop, int32_t* nbr, int32_t* deg) {
-  const int lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_id();
-  if (i == 0 && lane == 0) deg[n] = 0;  // scan sentinel -> rowptr[n] = E
-  if (i >= n) return;
+template <int DIM>
+__global__ __launch_bounds__(kQBlock) void k_radius_query_lds(
+    const f32x4* cpos, const int32_t* start, const uint32_t* bbox, int n_ex, float r2, int cap, int loop,
+    int32_t* nbr, int32_t* deg, int64_t n) {
+  __shared__ f32x4 cand[kLdsCand];
+  __shared__ int32_t cstart[9][kTX + 3];  // cell starts of each neighbour row's span (+ end)
+  __shared__ int32_t seg_base[9];
+  __shared__ int32_t seg_g0[9];           // global index of each span's first candidate
   const Grid G = *reinterpret_cast<const Grid*>(bbox + 8);
-  float pi[3] = {0.0f, 0.0f, 0.0f};
-  for (int d = 0; d < dim; ++d) pi[d] = pos[i * stride + d];
-  const int key = cell_of_p[i];
-  int c[3];
-  {
-    int k = key;
-    c[0] = k % G.g[0]; k /= G.g[0];
-    c[1] = k % G.g[1]; k /= G.g[1];
-    c[2] = k % G.g[2];
-  }
-  const int rowbase = key - c[0];  // key of cell (0, cy, cz) of this example
-  // the 3^(dim-1) row spans of the neighbourhood, concatenated; all nine
-  // (dz, dy) slots are kept, out-of-grid ones as empty spans, so the bounds
-  // loads go out together and the candidate -> span lookup is a fixed chain
-  // of selects
-  int s0[9], pre[10];
-  pre[0] = 0;
-  const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
-  int sa[9], sb[9];
-#pragma unroll
-  for (int q = 0; q < 9; ++q) {
-    const int dz = q / 3 - 1, dy = q % 3 - 1;
-    const int z = c[2] + dz, y = c[1] + dy;
-    const bool ok = z >= 0 && z < G.g[2] && y >= 0 && y < G.g[1];
-    const int rk = ok ? rowbase + (dz * G.g[1] + dy) * G.g[0] : 0;
-    sa[q] = start[rk + x0];
-    sb[q] = start[rk + x1 + 1];
-    sb[q] = ok ? sb[q] : sa[q];
-  }
-#pragma unroll
-  for (int q = 0; q < 9; ++q) {
-    s0[q] = sa[q];
-    pre[q + 1] = pre[q] + (sb[q] - sa[q]);
-  }
-  const int total = pre[9];
-  int top = INT32_MAX;  // lanes [0, cnt) hold the kept ids, ascending
-  int cnt = 0;
-  // Candidate t of the concatenated spans, clamped to the last one (its
-  // validity, t < total, is tested apart from the load) -- branch-free, so a
-  // load's wait is placed at its first use.
-  auto cand = [&](int t) -> int {
-    const int tc = min(t, total - 1);
-    int off = s0[0] + tc;
-#pragma unroll
-    for (int q = 1; q < 9; ++q)
-      if (tc >= pre[q]) off = s0[q] + (tc - pre[q]);  // empty spans are overridden by the next
-    return order[off];
-  };
-  auto load_pos = [&](int j, float (&p)[3]) {
-#pragma unroll
-    for (int d = 0; d < 3; ++d) p[d] = pos[(int64_t)j * stride + min(d, dim - 1)];
-  };
-  // two-stage software pipeline over the 64-candidate steps: the next step's
-  // positions and the ids of the step after are in flight while this step
-  // filters and sorts (the dependent id -> position loads were the per-step
-  // latency of a long candidate list)
-  if (total == 0) {  // only without a finite position of its own
-    if (lane == 0) deg[i] = 0;
-    return;
-  }
-  int jc = cand(lane), jn = cand(64 + lane);
-  float pc[3];
-  load_pos(jc, pc);
-  for (int base = 0; base < total; base += 64) {
-    float pn[3];
-    load_pos(jn, pn);
-    const int jnn = cand(base + 128 + lane);
-    int key_j = INT32_MAX;
-    if (base + lane < total && dist2_ordered(pc, pi, dim) < r2) key_j = jc;
-    if (cnt >= cap) {
-      const int kth = __shfl(top, cap - 1, 64);
-      if (key_j >= kth) key_j = INT32_MAX;
+  const int tiles_x = (G.g[0] + kTX - 1) / kTX;
+  const int64_t ntiles = (int64_t)n_ex * G.g[2] * G.g[1] * tiles_x;
+  constexpr int NR = DIM == 3 ? 9 : (DIM == 2 ? 3 : 1);
+  if (threadIdx.x == 0 && blockIdx.x == 0) deg[n] = 0;  // scan sentinel -> rowptr[n] = E
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row = tile / tiles_x;  // row = (ex * g2 + cz) * g1 + cy
+    const int x0 = (int)(tile - row * tiles_x) * kTX;
+    const int x1 = min(x0 + kTX, G.g[0]);                     // own cells [x0, x1)
+    const int xa = max(x0 - 1, 0), xb = min(x1, G.g[0] - 1);  // span cells [xa, xb]
+    const int nspan = xb - xa + 1;
+    const int cy = (int)(row % G.g[1]);
+    const int cz = (int)((row / G.g[1]) % G.g[2]);
+    __syncthreads();  // the previous tile's LDS is no longer read
+    for (int q = threadIdx.x; q < NR * (kTX + 3); q += blockDim.x) {
+      const int rq = q / (kTX + 3), c = q - rq * (kTX + 3);
+      const int dz = DIM == 3 ? rq / 3 - 1 : 0, dy = DIM >= 2 ? rq % 3 - 1 : 0;
+      const bool ok = cy + dy >= 0 && cy + dy < G.g[1] && cz + dz >= 0 && cz + dz < G.g[2];
+      const int64_t rk = (row + (int64_t)dz * G.g[1] + dy) * G.g[0];
+      if (c <= nspan) cstart[rq][c] = ok ? start[rk + xa + c] : 0;
     }
-    const unsigned long long bal = __ballot(key_j != INT32_MAX);
-    if (bal) {
-      const int nnew = __popcll(bal);
-      key_j = bitonic_sort64(key_j, lane);
-      const int other = __shfl(key_j, 63 - lane, 64);
-      top = bitonic_merge64(min(top, other), lane);
-      if (lane >= cap) top = INT32_MAX;
-      cnt = min(cnt + nnew, cap);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int rq = 0; rq < NR; ++rq) {
+        seg_base[rq] = tot;
+        seg_g0[rq] = cstart[rq][0];
+        tot += cstart[rq][nspan] - cstart[rq][0];
+      }
+      seg_base[NR] = tot;
     }
-    jc = jn;  // rotate the pipeline after the sort (a copy of a pending load waits for it)
-    jn = jnn;
-    for (int d = 0; d < 3; ++d) pc[d] = pn[d];
-  }
-  if (!loop) {  // torch_cluster: K+1 nearest-by-index, then drop the self loop
-    const unsigned long long self = __ballot(lane < cnt && top == (int)i);
-    if (self) {
-      const int at = __ffsll((long long)self) - 1;
-      const int nxt = __shfl(top, (lane + 1) & 63, 64);
-      if (lane >= at) top = (lane + 1 < cnt) ? nxt : INT32_MAX;
-      cnt -= 1;
+    __syncthreads();
+    const bool staged = seg_base[NR] <= kLdsCand;
+    if (staged) {
+      for (int rq = 0; rq < NR; ++rq) {
+        const int len = cstart[rq][nspan] - cstart[rq][0];
+        for (int t = threadIdx.x; t < len; t += blockDim.x) cand[seg_base[rq] + t] = cpos[seg_g0[rq] + t];
+      }
+    }
+    __syncthreads();
+    // queries: the particles of the own cells (center row = index NR / 2)
+    const int rc = NR / 2;
+    const int qa = cstart[rc][x0 - xa], qb = cstart[rc][x1 - xa];
+    for (int qi = qa + threadIdx.x; qi < qb; qi += blockDim.x) {
+      const f32x4 me = staged ? cand[seg_base[rc] + (qi - seg_g0[rc])] : cpos[qi];
+      const int i = __float_as_int(me[3]);
+      const int cx = cell_of(me[0], G.lo[0], G.inv_cell, G.g[0]);
+      int top[kMaxCap];
+#pragma unroll
+      for (int s = 0; s < kMaxCap; ++s) top[s] = INT32_MAX;
+      int cnt = 0;
+      for (int rq = 0; rq < NR; ++rq) {
+        const int ca = max(cx - 1, xa) - xa, cb = min(cx + 1, xb) - xa;  // span-relative cells
+        const int ja = cstart[rq][ca] - seg_g0[rq], jb = cstart[rq][cb + 1] - seg_g0[rq];
+        for (int t = ja; t < jb; ++t) {
+          const f32x4 c = staged ? cand[seg_base[rq] + t] : cpos[seg_g0[rq] + t];
+          float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) {
+            const float u = __fsub_rn(c[d], me[d]);
+            s = __fadd_rn(s, __fmul_rn(u, u));
+          }
+          if (s < r2) {
+            const int j = __float_as_int(c[3]);
+            ++cnt;
+            if (j < top[kMaxCap - 1]) sorted_insert(top, j);
+          }
+        }
+      }
+      cnt = min(cnt, cap);
+      int32_t* out = nbr + (int64_t)i * cap;
+      int w = 0;
+      bool self_dropped = false;
+#pragma unroll
+      for (int s = 0; s < kMaxCap; ++s) {
+        if (s < cnt) {
+          const int v = top[s];
+          if (!loop && v == i && !self_dropped) {  // torch_cluster: K+1 first-by-index, then drop self
+            self_dropped = true;
+          } else {
+            out[w] = v;
+            ++w;
+          }
+        }
+      }
+      deg[i] = w;
     }
   }
-  if (lane < cnt) nbr[i * cap + lane] = top;
-  if (lane == 0) deg[i] = cnt;
-  (void)ex_of;
 }
 
 __global__ __launch_bounds__(256) void k_compact(int64_t n, int cap, const int32_t* nbr,
@@ -543,6 +540,7 @@ struct RadiusWs {
   uint32_t nbuckets;  // cell capacity (cells of all examples)
   int32_t *count, *fill, *start, *bucket_of, *ex_of, *order, *nbr, *deg, *partials;
   uint32_t* bbox;
+  f32x4* cpos;  // [n] cell-ordered (x, y, z, id)
   size_t bytes;
 };
 
@@ -570,6 +568,7 @@ RadiusWs radius_layout(int64_t n, int32_t K, int32_t loop, void* base) {
   w.bucket_of = take(n);
   w.ex_of = take(n);
   w.order = take(n);
+  w.cpos = reinterpret_cast<f32x4*>(take(4 * n));
   w.nbr = take(n * cap);
   w.deg = take(n + 1);
   w.partials = take(nparts);
@@ -588,11 +587,9 @@ int scan_exclusive(const int32_t* in, int32_t* out, int64_t len, int32_t* partia
   if (nb > 8192) return set_error(SGNN_ERR_UNSUPPORTED, "scan: more than 16M elements");
   hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(kScanBlock), 0, stream, in, out, len,
                      partials);
-  if (nb > 1) {
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, stream, partials, (int)nb);
+  if (nb > 1)
     hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(kScanBlock), 0, stream, out, len,
                        partials);
-  }
   return check_launch("scan");
 }
 
@@ -645,17 +642,31 @@ extern "C" int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n
   const int64_t max_cells = w.nbuckets;
   const unsigned nblk = (unsigned)((n + 255) / 256);
   (void)hipMemsetAsync(w.count, 0, sizeof(int32_t) * (2 * (size_t)w.nbuckets + 2 + 16), stream);
-  hipLaunchKernelGGL(k_bbox, dim3(std::min<unsigned>(nblk, 128)), dim3(256), 0, stream, pos,
-                     pos_stride, n, dim, n_ex, cell0, max_cells, w.bbox);
-  hipLaunchKernelGGL(k_cell_assign, dim3(nblk), dim3(256), 0, stream, pos, pos_stride, n, dim,
-                     ex_ptr, n_ex, w.bbox, w.bucket_of, w.ex_of, w.count);
+  const unsigned bblk = std::min<unsigned>(nblk, 128);
+#define SGNN_DIM_LAUNCH(K, GRID, ...)                                                                 \
+  do {                                                                                             \
+    if (dim == 1) hipLaunchKernelGGL(K<1>, dim3(GRID), dim3(256), 0, stream, __VA_ARGS__);          \
+    else if (dim == 2) hipLaunchKernelGGL(K<2>, dim3(GRID), dim3(256), 0, stream, __VA_ARGS__);     \
+    else hipLaunchKernelGGL(K<3>, dim3(GRID), dim3(256), 0, stream, __VA_ARGS__);                   \
+  } while (0)
+  SGNN_DIM_LAUNCH(k_bbox, bblk, pos, pos_stride, n, n_ex, cell0, max_cells, w.bbox);
+  SGNN_DIM_LAUNCH(k_cell_assign, nblk, pos, pos_stride, n, ex_ptr, n_ex, w.bbox, w.bucket_of, w.ex_of, w.count);
   int st = scan_exclusive(w.count, w.start, (int64_t)w.nbuckets + 1, w.partials, stream);
   if (st) return st;
-  hipLaunchKernelGGL(k_cell_scatter, dim3(nblk), dim3(256), 0, stream, n, w.bucket_of, w.start,
-                     w.fill, w.order);
-  hipLaunchKernelGGL(k_radius_query, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, pos,
-                     pos_stride, n, dim, r2, w.bbox, w.bucket_of, w.ex_of,
-                     w.start, w.order, cap, loop, w.nbr, w.deg);
+  SGNN_DIM_LAUNCH(k_cell_scatter, nblk, n, w.bucket_of, w.start, w.fill, w.order, pos, pos_stride, w.cpos);
+#undef SGNN_DIM_LAUNCH
+  // LDS-binned query over cell tiles (persistent grid: the tile count lives on the device)
+  // about one tile per workgroup at lattice densities (~1.5 particles per cell, 64-cell tiles)
+  const unsigned qgrid = (unsigned)std::min<int64_t>(std::max<int64_t>((n + 63) / 64, 1), 4096);
+  if (dim == 1)
+    hipLaunchKernelGGL(k_radius_query_lds<1>, dim3(qgrid), dim3(kQBlock), 0, stream, w.cpos, w.start, w.bbox,
+                       n_ex, r2, cap, loop, w.nbr, w.deg, n);
+  else if (dim == 2)
+    hipLaunchKernelGGL(k_radius_query_lds<2>, dim3(qgrid), dim3(kQBlock), 0, stream, w.cpos, w.start, w.bbox,
+                       n_ex, r2, cap, loop, w.nbr, w.deg, n);
+  else
+    hipLaunchKernelGGL(k_radius_query_lds<3>, dim3(qgrid), dim3(kQBlock), 0, stream, w.cpos, w.start, w.bbox,
+                       n_ex, r2, cap, loop, w.nbr, w.deg, n);
   st = scan_exclusive(w.deg, rowptr, n + 1, w.partials, stream);
   if (st) return st;
   const int64_t tot = n * cap;
