@@ -734,7 +734,9 @@ static int node_layer_common(NodeLayerArgs& a, const sgnn_mlp* node_fn, int mode
       return set_error(SGNN_ERR_INVALID, "node_layer: saves");
     a.sv = *saves;
   }
-  if (!train && H == 64) {  // inference: 16-node tiles, output units split over 4 waves (fwd16.hip)
+  // inference, small graphs: 16-node tiles, output units split over 4 waves (fwd16.hip); from ~10k
+  // nodes up the 32-node one-wave tiles below are faster (C2 50k: 36 vs 45 us per layer)
+  if (!train && H == 64 && a.n <= 8192) {
     sgnn::Node16Args b{a.x_in, a.agg, a.cin, a.cout, a.rowptr, a.n, a.w1, a.b1, a.wm, a.bm, a.w2, a.b2,
                        a.g, a.bb, a.we, a.be, a.u, a.v, a.wd1, a.bd1, a.wdm, a.bdm, a.wd2, a.bd2,
                        a.pos_seq, a.T, a.dim, a.acc_mean, a.acc_std, a.pred, a.next_pos,
