@@ -191,6 +191,19 @@ int sgnn_interaction_layer_decode(const float* x_in, const float* u_in, const fl
                                   int32_t dim, const float* acc_mean, const float* acc_std,
                                   float* pred, float* next_pos, float* window_out, void* stream);
 
+/* sgnn_interaction_layer for the FIRST layer with Encoder.edge_fn folded in
+ * (graph_network.py:92-96, learned_simulator.py:299-312; nmlp_layers 1): e0 of
+ * every edge is computed from the positions (most recent frame at pos + i *
+ * pos_stride) inside the layer, used at once, and written to e0t for the
+ * later layers -- replaces sgnn_encode_edges + sgnn_interaction_layer(k = 0). */
+int sgnn_interaction_layer_encode(const float* pos, int64_t pos_stride, int32_t dim, float radius,
+                                  const sgnn_mlp* enc_edge, float* e0t, const float* x_in,
+                                  const float* u_in, const float* v_in, const int32_t* rowptr,
+                                  const int32_t* send, const int32_t* recv, int64_t n,
+                                  const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
+                                  const sgnn_mlp* next_edge, float* x_out, float* u_out, float* v_out,
+                                  void* stream);
+
 /* ---------------------------------------------------------------------------
  * Whole-step drivers.  One call = one LearnedSimulator.predict_positions
  * (learned_simulator.py:413-438: radius graph, encoders, L interaction

@@ -102,6 +102,10 @@ SIGNATURES = {
                                                      c_void_p, c_void_p, c_void_p, c_int64, P_MLP, P_MLP,
                                                      P_MLP, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                                      c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sgnn_interaction_layer_encode": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_float, P_MLP, c_void_p,
+                                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                     c_int64, P_MLP, P_MLP, P_MLP, c_void_p, c_void_p, c_void_p,
+                                                     c_void_p]),
     "sgnn_coo_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64]),
     "sgnn_coo_to_csr": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -854,7 +854,7 @@ extern "C" int sgnn_encode_edge_features(const float* e, int32_t fe, const int32
 // + node update in one launch (fwd16.hip k_layer16).  Nodes per workgroup
 // tile: enough tiles for two workgroups per CU, at most 16.
 static int layer_common(sgnn::Layer16Args& L, const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn, int mode,
-                        int dec_nlin, void* stream) {
+                        int dec_nlin, void* stream, bool first = false) {
   using namespace sgnn;
   const int H = node_fn ? node_fn->hidden : 0;
   int st = check_mlp(node_fn, 2 * H, H, H, true, "interaction_layer: node MLP shape");
@@ -869,7 +869,7 @@ static int layer_common(sgnn::Layer16Args& L, const sgnn_mlp* edge_fn, const sgn
   L.ewe = edge_fn->w1 + 2 * H; L.ewm = mid_w(edge_fn); L.ebm = mid_b(edge_fn);
   L.ew2 = last_w(edge_fn); L.eb2 = last_b(edge_fn); L.eg = edge_fn->ln_g; L.ebb = edge_fn->ln_b;
   L.nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, (a.n + 511) / 512));
-  return layer16_launch(L, mode, node_fn->nlin, static_cast<hipStream_t>(stream));
+  return layer16_launch(L, mode, node_fn->nlin, static_cast<hipStream_t>(stream), first);
 }
 
 extern "C" int sgnn_interaction_layer(const float* x_in, const float* u_in, const float* v_in,
@@ -921,3 +921,30 @@ extern "C" int sgnn_interaction_layer_decode(const float* x_in, const float* u_i
   return layer_common(L, edge_fn, node_fn, 1, decoder->nlin, stream);
 }
 
+extern "C" int sgnn_interaction_layer_encode(const float* pos, int64_t pos_stride, int32_t dim, float radius,
+                                             const sgnn_mlp* enc_edge, float* e0t, const float* x_in,
+                                             const float* u_in, const float* v_in, const int32_t* rowptr,
+                                             const int32_t* send, const int32_t* recv, int64_t n,
+                                             const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
+                                             const sgnn_mlp* next_edge, float* x_out, float* u_out,
+                                             float* v_out, void* stream) {
+  using namespace sgnn;
+  if (n <= 0) return SGNN_OK;
+  if (!pos || dim < 1 || dim > 3 || !(radius > 0.0f) || !e0t || !x_in || !u_in || !v_in || !rowptr || !send ||
+      !recv || !x_out || !u_out || !v_out || !next_edge || u_out == u_in || v_out == v_in)
+    return set_error(SGNN_ERR_INVALID, "interaction_layer_encode: bad arguments");
+  const int H = node_fn ? node_fn->hidden : 0;
+  int st = check_mlp(enc_edge, dim + 1, H, H, true, "interaction_layer_encode: edge encoder MLP shape");
+  if (!st) st = check_mlp(next_edge, 3 * H, H, H, true, "interaction_layer_encode: next edge MLP shape");
+  if (st) return st;
+  if (enc_edge->nlin != 2 || node_fn->nlin != 2)
+    return set_error(SGNN_ERR_UNSUPPORTED, "interaction_layer_encode: nmlp_layers 1 only");
+  Layer16Args L{};
+  L.nd.x_in = x_in; L.nd.rowptr = rowptr; L.nd.n = n; L.nd.we = next_edge->w1; L.nd.be = next_edge->b1;
+  L.nd.u = u_out; L.nd.v = v_out; L.nd.x_out = x_out;
+  L.u_in = u_in; L.v_in = v_in; L.e0t = e0t; L.e_scale = 1.0f; L.send = send; L.recv = recv;
+  L.pos = pos; L.pos_stride = pos_stride; L.dim = dim; L.radius = radius;
+  L.xw1 = enc_edge->w1; L.xb1 = enc_edge->b1; L.xw2 = enc_edge->w2; L.xb2 = enc_edge->b2;
+  L.xg = enc_edge->ln_g; L.xbb = enc_edge->ln_b; L.e0t_out = e0t;
+  return layer_common(L, edge_fn, node_fn, 0, 0, stream, true);
+}

@@ -42,9 +42,19 @@ struct Layer16Args {
   const int32_t *send, *recv;
   const float *ewe, *ewm, *ebm, *ew2, *eb2, *eg, *ebb;  // edge MLP (ewe = W1 + 2H, ld 3H)
   int nt;
+  // first layer only (first = true): Encoder.edge_fn fused in -- e0 of every
+  // edge from the positions (learned_simulator.py:299-312, graph_network.py:
+  // 92-96; nmlp_layers = 1), used at once and written to e0t_out for the
+  // later layers
+  const float* pos;  // most recent frame, particle i at pos + i * pos_stride
+  int64_t pos_stride;
+  int dim;
+  float radius;
+  const float *xw1, *xb1, *xw2, *xb2, *xg, *xbb;
+  float* e0t_out;
 };
 
-int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t stream);
+int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t stream, bool first = false);
 
 // Encoder, node side (learned_simulator.py:256-290 features -> Encoder.node_fn,
 // graph_network.py:86-90) + the first layer's u/v; nd carries the encoder's

@@ -356,16 +356,19 @@ SGNN_DEV void stage_w64_store(float* dst, const f32x4 (&v)[kStagePer], float sca
   }
 }
 
-template <int NL, int MODE>
+template <int NL, int MODE, bool FIRST>
 __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) void k_layer16(sgnn::Layer16Args a) {
   // LDS: edge MLP weights (W1e pre-scaled by 2^k, exact) and per-wave
   // receiver sums; the node phase's exchange buffers alias the sums (barriers
-  // separate the phases)
+  // separate the phases).  FIRST adds the edge encoder's last Linear.
   constexpr int NW = NL == 3 ? 3 : 2;
+  constexpr int NB = (NL == 3 || MODE == 1) ? kBufs : 4;  // node_tail touches buffers 0, 2, 3 at NL 2, mode 0
   __shared__ float sw[NW][H * LDX];
   __shared__ float svec[4][H];                    // b2, gamma, beta, bm
-  __shared__ float scratch[kBufs * 16 * LDX];  // per-wave receiver sums; = xb in the node phase
-  static_assert(kBufs >= kWaves16, "the per-wave sums fit the node buffers");
+  __shared__ float scratch[NB * 16 * LDX];  // per-wave receiver sums; = xb in the node phase
+  __shared__ float sxw[FIRST ? H * LDX : 4];      // encoder W2 (FIRST)
+  __shared__ float sxv[FIRST ? 4 : 1][H];         // encoder b1, b2, gamma, beta (FIRST)
+  static_assert(NB >= kWaves16, "the per-wave sums fit the node buffers");
   float* sums_all = scratch;
   auto xb = reinterpret_cast<float (*)[16 * LDX]>(scratch);
   const Node16Args& nd = a.nd;
@@ -377,13 +380,23 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) v
   int32_t ea = 0, eb = 0;
   int r_n = 0, s_n = 0;
   f32x4 x_n[KQ], uv_n[KQ];
-  auto load_half = [&](int32_t hs) {  // indices, e0 row, u[recv] + v[send] of edge hs + j
+  float ps_n[3] = {0.0f, 0.0f, 0.0f}, pr_n[3] = {0.0f, 0.0f, 0.0f};
+  auto load_half = [&](int32_t hs) {  // indices, e0 row (FIRST: both positions), u[recv] + v[send]
     const int32_t e = hs + j;
     const int32_t ec = e < eb ? e : eb - 1;
     r_n = a.recv[ec];
     s_n = a.send[ec];
+    if constexpr (FIRST) {
 #pragma unroll
-    for (int q = 0; q < KQ; ++q) x_n[q] = ld_e0_edge(a.e0t, ec, q, g);
+      for (int c = 0; c < 3; ++c)
+        if (c < a.dim) {
+          ps_n[c] = a.pos[(int64_t)s_n * a.pos_stride + c];
+          pr_n[c] = a.pos[(int64_t)r_n * a.pos_stride + c];
+        }
+    } else {
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) x_n[q] = ld_e0_edge(a.e0t, ec, q, g);
+    }
 #pragma unroll
     for (int t = 0; t < KQ; ++t)
       uv_n[t] = ld4(a.u_in + (int64_t)r_n * H + 16 * t + 4 * g) + ld4(a.v_in + (int64_t)s_n * H + 16 * t + 4 * g);
@@ -406,6 +419,18 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) v
   stage_vec(svec[1], a.eg, H, H);
   stage_vec(svec[2], a.ebb, H, H);
   stage_vec(svec[3], a.ebm, H, H);
+  float xw1[KQ] = {0.0f, 0.0f, 0.0f, 0.0f};  // FIRST: encoder W1 [H][dim + 1], unit 16 t + j, k = g
+  if constexpr (FIRST) {
+    f32x4 sx[kStagePer];
+    stage_w64_load(sx, a.xw2, H);
+    stage_w64_store(sxw, sx, 1.0f);
+    stage_vec(sxv[0], a.xb1, H, H);
+    stage_vec(sxv[1], a.xb2, H, H);
+    stage_vec(sxv[2], a.xg, H, H);
+    stage_vec(sxv[3], a.xbb, H, H);
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) xw1[t] = g <= a.dim ? a.xw1[(16 * t + j) * (a.dim + 1) + g] : 0.0f;
+  }
   NodeW<NL, MODE> NWt;
   NWt.load(nd, b, j, g);
   float* sums = sums_all + b * 16 * LDX;
@@ -424,12 +449,54 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) v
       const bool ev = hs + j < eb;
       const int r = r_n;
       f32x4 x[KQ], acc[KQ];
+      float ps[3], pr[3];
 #pragma unroll
       for (int q = 0; q < KQ; ++q) {
         x[q] = x_n[q];
         acc[q] = uv_n[q];
       }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        ps[c] = ps_n[c];
+        pr[c] = pr_n[c];
+      }
       if (hs + 16 * kWaves16 < eb) load_half(hs + 16 * kWaves16);
+      if constexpr (FIRST) {
+        // edge features (p_s - p_r) / R and their norm (learned_simulator.py:299-312)
+        float f[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ss = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          if (c < a.dim) {
+            const float dd = __fdiv_rn(__fsub_rn(ps[c], pr[c]), a.radius);
+            f[c] = dd;
+            ss = __fadd_rn(ss, __fmul_rn(dd, dd));
+          }
+        const float nrm = sqrtf(ss);
+        if (a.dim == 1) f[1] = nrm; else if (a.dim == 2) f[2] = nrm; else f[3] = nrm;
+        const float fg = g == 0 ? f[0] : g == 1 ? f[1] : g == 2 ? f[2] : f[3];
+        // Encoder.edge_fn: Linear(dim + 1, H) -> ReLU -> Linear(H, H) -> LayerNorm
+        f32x4 hx[KQ], y[KQ];
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) {
+          hx[t] = relu4(mfma16(xw1[t], fg, ld4(sxv[0] + 16 * t + 4 * g)));
+          y[t] = ld4(sxv[1] + 16 * t + 4 * g);
+        }
+        mm_full(y, sxw, hx, j, g);
+        float mu, rs;
+        ln_stats(y, mu, rs);
+        const int32_t e = hs + j;
+        float* et = a.e0t_out + (int64_t)(e >> 5) * (32 * H);
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) {
+          const f32x4 ga = ld4(sxv[2] + 16 * t + 4 * g), be = ld4(sxv[3] + 16 * t + 4 * g);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) x[t][c] = (y[t][c] - mu) * rs * ga[c] + be[c];
+          if (ev) {  // e0 for the later layers, 32-edge tiled layout (ld_e0_edge's address)
+            const int tt = t >> 1, gg = 2 * (t & 1) + (g >> 1), hh = g & 1;
+            st4(et + (tt * 4 + gg) * 256 + ((e & 31) + 32 * hh) * 4, x[t]);
+          }
+        }
+      }
       // first Linear: u[recv] + v[send] + 2^k W1_e e0 (graph_network.py:197 on cat[x_i, x_j, e])
       mm_full(acc, sw[0], x, j, g);
 #pragma unroll
@@ -554,15 +621,18 @@ int node16_launch(const Node16Args& a, int mode, int nl, hipStream_t s) {
   return check_launch("node_layer16");
 }
 
-int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t s) {
+int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t s, bool first) {
   if (a.nd.n <= 0) return SGNN_OK;
   if (a.nt < 1 || a.nt > 16) return set_error(SGNN_ERR_INVALID, "layer16: nodes per tile must be 1..16");
+  if (first && (mode != 0 || nl != 2))
+    return set_error(SGNN_ERR_UNSUPPORTED, "layer16: the fused edge encoder needs nmlp_layers 1 and a later layer");
   const int64_t tiles = (a.nd.n + a.nt - 1) / a.nt;
   const unsigned grid = (unsigned)std::min<int64_t>(tiles, 512);
-  if (mode == 0 && nl == 2) hipLaunchKernelGGL((k_layer16<2, 0>), dim3(grid), dim3(kBlock16), 0, s, a);
-  else if (mode == 0) hipLaunchKernelGGL((k_layer16<3, 0>), dim3(grid), dim3(kBlock16), 0, s, a);
-  else if (nl == 2) hipLaunchKernelGGL((k_layer16<2, 1>), dim3(grid), dim3(kBlock16), 0, s, a);
-  else hipLaunchKernelGGL((k_layer16<3, 1>), dim3(grid), dim3(kBlock16), 0, s, a);
+  if (first) hipLaunchKernelGGL((k_layer16<2, 0, true>), dim3(grid), dim3(kBlock16), 0, s, a);
+  else if (mode == 0 && nl == 2) hipLaunchKernelGGL((k_layer16<2, 0, false>), dim3(grid), dim3(kBlock16), 0, s, a);
+  else if (mode == 0) hipLaunchKernelGGL((k_layer16<3, 0, false>), dim3(grid), dim3(kBlock16), 0, s, a);
+  else if (nl == 2) hipLaunchKernelGGL((k_layer16<2, 1, false>), dim3(grid), dim3(kBlock16), 0, s, a);
+  else hipLaunchKernelGGL((k_layer16<3, 1, false>), dim3(grid), dim3(kBlock16), 0, s, a);
   return check_launch("layer16");
 }
 

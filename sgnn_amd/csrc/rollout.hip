@@ -22,18 +22,31 @@ extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in,
                          in->vel_std, in->wall_max, in->wall_div, m->enc_node, &m->edge[0], ws->x_a,
                          ws->u, ws->v, nullptr, stream);
   if (st) return st;
-  st = sgnn_encode_edges(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, d, in->radius, ws->rowptr,
-                         ws->send, ws->recv, n, ws->edge_cap, m->enc_edge, ws->e0t, nullptr, stream);
-  if (st) return st;
+  const float* last = pos_seq + (int64_t)(T - 1) * d;
   float* x_in = ws->x_a;
   float* x_out = ws->x_b;
   float scale = 1.0f;
-  // small graphs (n <= 8192, hidden 64): one fused launch per layer (u/v ping-pong); larger graphs
-  // keep the edge / node kernel pair (more workgroups, no per-workgroup weight staging per node tile)
-  if (ws->u2 && ws->v2 && m->node[0].hidden == 64 && n <= 8192) {
+  // small graphs (n <= 8192, hidden 64): one fused launch per layer (u/v ping-pong), the first one
+  // with the edge encoder folded in (nmlp_layers 1); larger graphs keep the edge / node kernel pair
+  // (more workgroups, no per-workgroup weight staging per node tile)
+  const bool fused = ws->u2 && ws->v2 && m->node[0].hidden == 64 && n <= 8192;
+  const bool enc_in_layer0 = fused && m->nlayers > 1 && m->enc_edge->nlin == 2 && m->node[0].nlin == 2;
+  if (!enc_in_layer0) {
+    st = sgnn_encode_edges(last, (int64_t)T * d, d, in->radius, ws->rowptr, ws->send, ws->recv, n,
+                           ws->edge_cap, m->enc_edge, ws->e0t, nullptr, stream);
+    if (st) return st;
+  }
+  if (fused) {
     float *u_in = ws->u, *v_in = ws->v, *u_out = ws->u2, *v_out = ws->v2;
     for (int k = 0; k < m->nlayers; ++k, scale *= 2.0f) {
-      if (k < m->nlayers - 1) {
+      if (k == 0 && enc_in_layer0) {
+        st = sgnn_interaction_layer_encode(last, (int64_t)T * d, d, in->radius, m->enc_edge, ws->e0t, x_in, u_in,
+                                           v_in, ws->rowptr, ws->send, ws->recv, n, &m->edge[0], &m->node[0],
+                                           &m->edge[1], x_out, u_out, v_out, stream);
+        std::swap(x_in, x_out);
+        std::swap(u_in, u_out);
+        std::swap(v_in, v_out);
+      } else if (k < m->nlayers - 1) {
         st = sgnn_interaction_layer(x_in, u_in, v_in, ws->e0t, scale, ws->rowptr, ws->send, ws->recv, n,
                                     &m->edge[k], &m->node[k], &m->edge[k + 1], x_out, u_out, v_out, stream);
         std::swap(x_in, x_out);

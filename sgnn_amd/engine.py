@@ -290,18 +290,30 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
                               ctypes.byref(pk.enc_node), ctypes.byref(pk.edge[0]),
                               ws.x_a.data_ptr(), ws.u.data_ptr(), ws.v.data_ptr(), None, s),
           "sgnn_encode_nodes")
-    check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius),
-                              ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
-                              ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(), None, s),
-          "sgnn_encode_edges")
-    x_in, x_out = ws.x_a, ws.x_b
     nl = len(pk.edge)
-    if ws.u2 is not None:   # hidden 64: one fused sgnn_interaction_layer launch per layer
+    # same launch sequence as sgnn_predict_positions (rollout.hip)
+    enc_in_layer0 = ws.u2 is not None and nl > 1 and pk.enc_edge.nlin == 2 and pk.node[0].nlin == 2
+    if not enc_in_layer0:
+        check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius),
+                                  ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
+                                  ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(), None, s),
+              "sgnn_encode_edges")
+    x_in, x_out = ws.x_a, ws.x_b
+    if ws.u2 is not None:   # small graphs at hidden 64: one fused launch per layer
         uv_in, uv_out = (ws.u, ws.v), (ws.u2, ws.v2)
         for k in range(nl):
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-            if k < nl - 1:
+            if k == 0 and enc_in_layer0:
+                check(L.sgnn_interaction_layer_encode(
+                    pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius), ctypes.byref(pk.enc_edge),
+                    ws.e0t.data_ptr(), x_in.data_ptr(), uv_in[0].data_ptr(), uv_in[1].data_ptr(),
+                    ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n, ctypes.byref(pk.edge[0]),
+                    ctypes.byref(pk.node[0]), ctypes.byref(pk.edge[1]), x_out.data_ptr(), uv_out[0].data_ptr(),
+                    uv_out[1].data_ptr(), s), "sgnn_interaction_layer_encode")
+                x_in, x_out = x_out, x_in
+                uv_in, uv_out = uv_out, uv_in
+            elif k < nl - 1:
                 check(L.sgnn_interaction_layer(x_in.data_ptr(), uv_in[0].data_ptr(), uv_in[1].data_ptr(),
                                                ws.e0t.data_ptr(), float(2.0 ** k), ws.rowptr.data_ptr(),
                                                ws.send.data_ptr(), ws.recv.data_ptr(), n, ctypes.byref(pk.edge[k]),
