@@ -21,8 +21,9 @@ Extras in the same JSON line (every N):
                   is the north_star's 1/2/4/8-GPU training curve.
   "training_c3"   C3: global batch of 8 real-size graphs (4,800/6,400/8,000
                   particles) split over the N ranks: strong scaling.
-  "rollout_extra" C2 (50k, r = 0.6), C1 at r = 0.6 and C4 (3D 200k, L = 10,
-                  H = 128) rollouts (replicas at N > 1).
+  "rollout_extra" C2 (50k, r = 0.6), C1 at r = 0.6, the real Taylor-bar sizes
+                  (4,800 / 6,400 / 8,000 particles, r = 0.6) and C4 (3D 200k,
+                  L = 10, H = 128) rollouts (replicas at N > 1).
   "multi_scale_c5_train"  C5: multi-scale 3D 1M particles per rank, DDP.
 CPU baselines (rank 0 at N = 1 only): the oracle (plain-torch CPU restatement
 of the reference, test infrastructure) on this box's host cores; >= 20 timed
@@ -58,6 +59,10 @@ WORKLOADS = {
     "c1_r15": ((50, 40), 15.0, 64, 5),     # configs[0] shape at the BASELINE radius (cap binds)
     "c1_r06": ((50, 40), 0.6, 64, 5),      # configs[0] shape at the reference default radius
     "c4": ((100, 50, 40), 0.75, 128, 10),  # configs[3]: 3D 200k particles, 10 layers, H=128
+    # the real Taylor-bar sizes: 60/80/100 mm x 20 mm bars at 0.5 mm, default radius
+    "t4800": ((120, 40), 0.6, 64, 5),
+    "t6400": ((160, 40), 0.6, 64, 5),
+    "t8000": ((200, 40), 0.6, 64, 5),
 }
 MS_WORKLOADS = {
     # name: (lattice dims, num_scales, window, radius_multiplier, hidden, layers, nmlp_layers)
@@ -190,16 +195,20 @@ def cpu_threads() -> dict:
 
 
 def profiled(workload, mode, kernel):
-    """Per-launch HBM bytes and duration of `kernel` from the newest committed
-    rocprofv3 summary (profiles/r*_summary.json: FETCH_SIZE x2 + WRITE_SIZE)."""
+    """Per-launch HBM bytes and duration of `kernel` (all its template
+    variants, weighted by launches) from the newest committed rocprofv3
+    summary (profiles/r*_summary.json: FETCH_SIZE x2 + WRITE_SIZE)."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
         d = json.load(open(path))
         if d.get("workload") != workload or d.get("mode", "rollout") != mode:
             continue
-        for k, v in d["kernels"].items():
-            if k.split("<")[0] == kernel and "hbm_bytes" in v:
-                best = {"bytes": v["hbm_bytes"], "avg_us": v.get("avg_us"), "source": os.path.relpath(path, ROOT)}
+        ks = [v for k, v in d["kernels"].items() if k.split("<")[0] == kernel and "hbm_bytes" in v]
+        if ks:
+            calls = sum(v["calls"] for v in ks)
+            best = {"bytes": sum(v["hbm_bytes"] * v["calls"] for v in ks) / calls,
+                    "avg_us": sum(v["avg_us"] * v["calls"] for v in ks) / calls,
+                    "source": os.path.relpath(path, ROOT)}
     return best
 
 
@@ -318,16 +327,24 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps)
     E = float(np.mean(edges))
     E_all = sum_over_ranks(E, world, device)
     edge_avg_s = float(np.mean([a.elapsed_time(b) for a, b in timers])) * 1e-3
-    flops = E * 4 * H * H            # two H x H Linears per edge (u/v factorised out of the first)
-    # algorithmic bytes of one edge-layer launch: e0 row (4H) + sender/receiver ids (8) per edge,
-    # u/v rows per node (8H), agg row written per node (4H)
-    alg_bytes = E * (4 * H + 8) + n * 12 * H
+    if H == 64 and n <= engine.FUSED_MAX_N:
+        # fused layer (sgnn_interaction_layer): edge MLP (two H x H Linears per edge, u/v factorised
+        # out of the first) + node MLP (2H x H, H x H) + the next layer's u/v (2 x H x H) per node
+        kernel = "k_layer16"
+        flops = E * 4 * H * H + n * 10 * H * H
+        # e0 row (4H) + ids (8) per edge; u/v rows read (8H), x read (4H), x/u/v written (12H) per node
+        alg_bytes = E * (4 * H + 8) + n * 24 * H
+    else:
+        kernel = "k_edge_layer"
+        flops = E * 4 * H * H        # two H x H Linears per edge (u/v factorised out of the first)
+        # e0 row (4H) + sender/receiver ids (8) per edge, u/v rows per node (8H), agg row written (4H)
+        alg_bytes = E * (4 * H + 8) + n * 12 * H
     out = {"workload": f"{workload}: {'x'.join(map(str, dims))} lattice = {n} particles/GPU, "
                        f"r={radius}, L={L}, H={H}, T={T_SEQ}, K=20", "particles": n, "edges": E,
            "value": n * steps * world / dt, "unit": "particle-steps/s",
            "ms_per_step": dt / steps * 1e3,
            "M_edge_messages_per_s": E_all * L * steps / dt / 1e6,
-           "roofline": roofline("k_edge_layer", flops, edge_avg_s, workload, "rollout", alg_bytes)}
+           "roofline": roofline(kernel, flops, edge_avg_s, workload, "rollout", alg_bytes)}
     out["roofline"]["share_of_step"] = edge_avg_s * L / (dt / steps)
     if cpu_steps > 0 and rank == 0 and world == 1:
         out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps, workload)
@@ -637,7 +654,7 @@ def main(argv=None):
             res["training"] = bench_train("train", 10, 3, world, rank, device, args.seed, cs)
             res["training_c3"] = bench_train("train-c3", 10, 3, world, rank, device, args.seed, 0)
             res["rollout_extra"] = {}
-            for wl, st in (("c2", 20), ("c1_r06", 20), ("c4", 10)):
+            for wl, st in (("c2", 20), ("c1_r06", 20), ("t4800", 20), ("t6400", 20), ("t8000", 20), ("c4", 10)):
                 res["rollout_extra"][wl] = bench_rollout(wl, st, 3, world, rank, device, args.seed, cs)
             res["multi_scale_c5_train"] = bench_ms_train("c5", 3, 1, world, rank, device, args.seed, cs)
     if rank == 0:

@@ -27,10 +27,13 @@ def call():
                                        ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
                                        ctypes.byref(pk.edge[1]), ctypes.byref(pk.node[1]), ctypes.byref(pk.edge[2]),
                                        ws.x_b.data_ptr(), ws.u2.data_ptr(), ws.v2.data_ptr(), s), "layer")
-for _ in range(20): call()
-torch.cuda.synchronize()
-a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-a.record()
-for _ in range(100): call()
-b.record(); torch.cuda.synchronize()
-print(f"{wl}: {a.elapsed_time(b) / 100 * 1e3:.2f} us/launch (no instrumentation)")
+for nt in (sys.argv[2:] or [""]):
+    if nt:
+        os.environ["SGNN_NT"] = nt
+    for _ in range(20): call()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(100): call()
+    b.record(); torch.cuda.synchronize()
+    print(f"{wl} nt={nt or 'auto'}: {a.elapsed_time(b) / 100 * 1e3:.2f} us/launch")
