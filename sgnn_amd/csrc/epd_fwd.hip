@@ -287,10 +287,16 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
   float* ml = mbuf + w * 32 * ldh;
   const int64_t E = a.rowptr[a.n];
   const int64_t ntiles = (E + 31) / 32;
-  // contiguous tile range per wave: neighbouring tiles share sender rows
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + w;
-  const int64_t nw = (int64_t)gridDim.x * kWaves;
-  const int64_t t_begin = ntiles * gw / nw, t_end = ntiles * (gw + 1) / nw;
+  // Tile order: XCD-aware grid stride.  Workgroups are dealt round-robin over
+  // the 8 XCDs (blocks b and b + 8 share one L2); the logical id
+  // (b % 8) * (nwg / 8) + b / 8 gives each XCD's waves a contiguous band of
+  // consecutive tiles per round, so the u[recv] / v[send] rows a band gathers
+  // (receivers and their lattice neighbours) stay in that XCD's L2 instead of
+  // being fetched by all eight.  (Needs nwg % 8 == 0; the host rounds the grid.)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int lg = (nwg % 8 == 0) ? (bid % 8) * (nwg / 8) + bid / 8 : bid;
+  const int64_t nw = (int64_t)nwg * kWaves;
+  const int64_t t_begin = (int64_t)lg * kWaves + w, t_end = ntiles;
   // H = 64 software pipeline: the next tile's indices and e0 are loaded while
   // this tile computes, and this tile's u[recv] / v[send] gathers are issued
   // before its W1e e0 product and added after it (the gather latency hides
@@ -310,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     for (int q = 0; q < TH * 4; ++q) xg_n[q] = ld4(src + q * 256);
   };
   if (PF && t_begin < t_end) fetch(t_begin);
-  for (int64_t tile = t_begin; tile < t_end; ++tile) {
+  for (int64_t tile = t_begin; tile < t_end; tile += nw) {
     const int64_t base = tile * 32;
     const int64_t e = base + j;
     const bool valid = e < E;
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
       f32x16 ur[TH], vr[TH];
       load_row_clayout<TH>(ur, a.u + (int64_t)rv * H);
       load_row_clayout<TH>(vr, a.v + (int64_t)s * H);
-      if (tile + 1 < t_end) fetch(tile + 1);
+      if (tile + nw < t_end) fetch(tile + nw);
       zero_acc_regs<TH>(hacc);
       mfma_from_groups<TH, TH, false>(hacc, We, ldh, 0, xg, 1.0f);
 #pragma unroll
@@ -708,7 +714,8 @@ extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t,
     a.sv = *saves;
   }
   const size_t lds = sizeof(float) * (size_t)((H == 64 ? 2 : 1) * H * (H + 4) + 4 * H + kWaves * 32 * (H + 4));
-  const unsigned grid = persistent_grid(edge_cap, 32 * kWaves, H == 64 ? 2 : 1);  // workgroups per CU LDS allows
+  unsigned grid = persistent_grid(edge_cap, 32 * kWaves, H == 64 ? 2 : 1);  // workgroups per CU LDS allows
+  if (grid >= 8) grid &= ~7u;  // a multiple of 8 for the XCD-aware tile order
   hipStream_t s = static_cast<hipStream_t>(stream);
   SGNN_DISPATCH_H_NL(H, edge_fn->nlin, (go_edge_layer<TH_, NL_>(train, grid, lds, s, a)));
   return check_launch("edge_layer");
@@ -869,6 +876,7 @@ static int layer_common(sgnn::Layer16Args& L, const sgnn_mlp* edge_fn, const sgn
   L.ewe = edge_fn->w1 + 2 * H; L.ewm = mid_w(edge_fn); L.ebm = mid_b(edge_fn);
   L.ew2 = last_w(edge_fn); L.eb2 = last_b(edge_fn); L.eg = edge_fn->ln_g; L.ebb = edge_fn->ln_b;
   L.nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, (a.n + 511) / 512));
+  if (const char* e = getenv("SGNN_NT")) L.nt = atoi(e);  // experiment override (tools/exp_layer16.py)
   return layer16_launch(L, mode, node_fn->nlin, static_cast<hipStream_t>(stream), first);
 }
 
