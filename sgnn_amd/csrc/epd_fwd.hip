@@ -858,8 +858,7 @@ extern "C" int sgnn_encode_edge_features(const float* e, int32_t fe, const int32
 
 // ---------------------------------------------------------------------------
 // Fused InteractionNetwork layer (inference, H = 64): edge MLP + receiver sums
-// + node update in one launch (fwd16.hip k_layer16).  Nodes per workgroup
-// tile: enough tiles for two workgroups per CU, at most 16.
+// + node update in one launch (fwd16.hip k_layer16).
 static int layer_common(sgnn::Layer16Args& L, const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn, int mode,
                         int dec_nlin, void* stream, bool first = false) {
   using namespace sgnn;
@@ -875,7 +874,11 @@ static int layer_common(sgnn::Layer16Args& L, const sgnn_mlp* edge_fn, const sgn
   a.wm = mid_w(node_fn); a.bm = mid_b(node_fn); a.g = node_fn->ln_g; a.bb = node_fn->ln_b;
   L.ewe = edge_fn->w1 + 2 * H; L.ewm = mid_w(edge_fn); L.ebm = mid_b(edge_fn);
   L.ew2 = last_w(edge_fn); L.eb2 = last_b(edge_fn); L.eg = edge_fn->ln_g; L.ebb = edge_fn->ln_b;
-  L.nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, (a.n + 511) / 512));
+  // nodes per workgroup tile: ~400 workgroups, 8..16 nodes each -- fewer, fatter workgroups pay
+  // the per-workgroup weight loads less often, and more than 512 (two per CU) would run in two
+  // rounds (measured, tools/exp_layer16.py: C1 r = 15 21.4 -> 18.6-19.9 us at 8 nodes vs 4,
+  // r = 0.6 17.9 -> 11.8 us; 4,800 particles best at 12, 8,000 at 16)
+  L.nt = (int)std::min<int64_t>(16, std::max<int64_t>(8, (a.n + 399) / 400));
   if (const char* e = getenv("SGNN_NT")) L.nt = atoi(e);  // experiment override (tools/exp_layer16.py)
   return layer16_launch(L, mode, node_fn->nlin, static_cast<hipStream_t>(stream), first);
 }
