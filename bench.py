@@ -94,6 +94,8 @@ def parse(argv=None):
     ap.add_argument("--workload", choices=sorted(WORKLOADS) + sorted(MS_WORKLOADS), default=None)
     ap.add_argument("--cpu-steps", type=int, default=20,
                     help="timed oracle rollout steps for cpu_baseline (0: skip); training legs use fewer")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="the headline cpu_baseline keeps stepping until this much CPU work (<= 20x --cpu-steps)")
     ap.add_argument("--no-extras", "--no-rollout-extras", dest="no_extras", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--selftest-launch", action="store_true",
@@ -255,10 +257,11 @@ def quiet_decoder(sim):
 CPU_SAMPLE_DIMS = {"c4": (20, 20, 20)}   # bounded CPU sample (same spacing / radius / model)
 
 
-def cpu_rollout_baseline(sim, window, radius, L, steps, workload):
+def cpu_rollout_baseline(sim, window, radius, L, steps, workload, min_seconds=0.0):
     """Oracle (test infrastructure: CPU restatement of the reference) rollout:
-    one warm-up step, then `steps` timed autoregressive steps (graph build +
-    features + EPD + integration all inside the timed region)."""
+    one warm-up step, then at least `steps` timed autoregressive steps, more
+    until `min_seconds` of CPU work (at most 20x steps) -- graph build +
+    features + EPD + integration all inside the timed region."""
     from oracle import sgnn_oracle as O
     info = cpu_threads()
     state = {k: v.detach().cpu() for k, v in sim.state_dict().items()}
@@ -275,10 +278,13 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload):
         nxt, _ = osim.predict_positions(cur, [n], types_)
         cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
         t0 = time.perf_counter()
-        for _ in range(steps):
+        done = 0
+        while done < steps or (time.perf_counter() - t0 < min_seconds and done < 20 * steps):
             nxt, _ = osim.predict_positions(cur, [n], types_)
             cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
+            done += 1
         dt = time.perf_counter() - t0
+        steps = done
         edges = int(O.radius_graph(cur[:, -1], [n], radius)[0].shape[0])
     return {"value": n * steps / dt, "unit": "particle-steps/s", **info, "seconds": dt,
             "M_edge_messages_per_s": edges * L * steps / dt / 1e6,
@@ -286,7 +292,7 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload):
                       f"restatement of the reference ops + C cell-list radius search), {n} particles{sample}"}
 
 
-def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps):
+def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps, cpu_seconds=0.0):
     """Timed region: `steps` autoregressive steps issued as ONE sgnn_rollout
     call (evaluate.rollout's device path: the C driver launches every kernel of
     every step; no host round trip).  Warm-up: full untimed rollouts.  The
@@ -347,7 +353,7 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps)
            "roofline": roofline(kernel, flops, edge_avg_s, workload, "rollout", alg_bytes)}
     out["roofline"]["share_of_step"] = edge_avg_s * L / (dt / steps)
     if cpu_steps > 0 and rank == 0 and world == 1:
-        out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps, workload)
+        out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps, workload, cpu_seconds)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
     return out
 
@@ -648,7 +654,8 @@ def main(argv=None):
         res = bench_train(args.mode, args.steps, args.warmup, world, rank, device, args.seed, cs)
         res["higher_is_better"], res["vs_baseline"] = True, None
     else:
-        r = bench_rollout(args.workload, args.steps, args.warmup, world, rank, device, args.seed, cs)
+        r = bench_rollout(args.workload, args.steps, args.warmup, world, rank, device, args.seed, cs,
+                          args.cpu_seconds)
         res = headline(r, args, world, "particle-steps/sec (2D Taylor-impact rollout)", parallel)
         if not args.no_extras:
             res["training"] = bench_train("train", 10, 3, world, rank, device, args.seed, cs)
