@@ -282,6 +282,79 @@ SGNN_DEV void store_row_clayout(float* row, const f32x16 (&x)[TH]) {
     }
 }
 
+// Predicated stores without branches: lanes that must not write get a
+// buffer offset past num_records and the hardware drops their write.  A loop
+// whose stores are all of this kind issues the same number of memory
+// instructions on every path, so the compiler's wait counts for loads
+// prefetched before them stay exact (a data-dependent number of stores makes
+// every later wait a full drain).
+constexpr uint32_t kBufRecords = 0x7ffffff0u;   // bytes addressable from a resource base
+constexpr int kBufDrop = 0x7ffffff0;            // voffset of a dropped lane
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+SGNN_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, kBufRecords, 0x00020000);
+}
+
+// row + (units of an items-on-lanes register tile): store_row_clayout where
+// `on`, a dropped write elsewhere.  voff = the row's byte offset from rs.
+template <int TH>
+SGNN_DEV void store_row_clayout_if(__amdgpu_buffer_rsrc_t rs, int voff, bool on, const f32x16 (&x)[TH]) {
+  const int h = lane_id() >> 5;
+  const int v0 = on ? voff + 16 * h : kBufDrop;
+#pragma unroll
+  for (int t = 0; t < TH; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x4 d;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) d[c] = __float_as_uint(x[t][4 * g + c]);
+      __builtin_amdgcn_raw_buffer_store_b128(d, rs, on ? v0 + 4 * (32 * t + 8 * g) : kBufDrop, 0, 0);
+    }
+}
+
+template <int CTRL, int ROWS = 0xf>
+SGNN_DEV int dpp_i(int v, int fill) { return __builtin_amdgcn_update_dpp(fill, v, CTRL, ROWS, 0xf, false); }
+
+// Receiver segment sums of one 32-edge tile held items on lanes (lane (j, h)
+// = edge j of the tile, units 32t + 8g + 4h + c; recv sorted, rv = recv of
+// lane's edge, valid = edge < E), with segment_sum_store's carry contract:
+// a run that starts and ends in the tile -> rows[recv]; one that starts here
+// and continues (nxt == recv of edge 31) -> cout[tile]; one that began in an
+// earlier tile (prv == its recv) -> cin[tile].  The sums come from a
+// segmented inclusive scan along the edges with DPP (row shifts 1-8 inside
+// the 16-lane rows, then row_bcast:15 into the second row of each half; the
+// sortedness makes "same receiver d edges back" the whole segment test), and
+// the last edge of each run stores (branch-free, see store_row_clayout_if).
+// x is overwritten by the scan.
+template <int TH>
+SGNN_DEV void segment_sum_rows(f32x16 (&x)[TH], int rv, bool valid, int prv, int nxt, int64_t tile,
+                               float* rows, float* cin, float* cout) {
+  constexpr int H = 32 * TH;
+  const int l = lane_id(), j = l & 31;
+  const int rk = valid ? rv : -1 - j;  // invalid edges: runs of their own
+  auto step = [&](int pr, auto shift) {
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = __int_as_float(shift(__float_as_int(x[t][r])));
+        x[t][r] = pr == rk ? x[t][r] + pv : x[t][r];
+      }
+  };
+  step(dpp_i<0x111>(rk, INT32_MIN), [](int v) { return dpp_i<0x111>(v, 0); });
+  step(dpp_i<0x112>(rk, INT32_MIN), [](int v) { return dpp_i<0x112>(v, 0); });
+  step(dpp_i<0x114>(rk, INT32_MIN), [](int v) { return dpp_i<0x114>(v, 0); });
+  step(dpp_i<0x118>(rk, INT32_MIN), [](int v) { return dpp_i<0x118>(v, 0); });
+  step(dpp_i<0x142, 0xa>(rk, INT32_MIN), [](int v) { return dpp_i<0x142, 0xa>(v, 0); });
+  const int rn = __builtin_amdgcn_ds_bpermute(((l + 1) & 63) << 2, rk);
+  const bool writer = valid && (j == 31 || rn != rk);
+  const bool starts = rv != prv, cont = j == 31 && nxt == rv;
+  store_row_clayout_if<TH>(buf_rsrc(rows), rv * (4 * H), writer && starts && !cont, x);
+  store_row_clayout_if<TH>(buf_rsrc(cout + tile * H), 0, writer && starts && cont, x);
+  store_row_clayout_if<TH>(buf_rsrc(cin + tile * H), 0, writer && !starts, x);
+}
+
 // LayerNorm that also returns the normalised value yhat and 1/std per item
 // (saved by the training forward for the LayerNorm backward).
 template <int TH>
@@ -448,6 +521,29 @@ SGNN_DEV void wave_lds_sync() {
 SGNN_DEV void stage_matrix_t(float* lds, int ld, const float* g, int ldg, int rows_valid,
                              int cols_valid, int rows_pad, int cols_pad, float scale = 1.0f) {
   const int total = rows_pad * cols_pad;
+  if (rows_valid == rows_pad && cols_valid == cols_pad && (cols_pad & 3) == 0 && (ldg & 3) == 0 &&
+      (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    // unpadded, 16-B aligned weights: float4 loads, four per thread in flight
+    // (the scalar loop below waits on one load per element)
+    const int q4 = cols_pad >> 2, nq = rows_pad * q4, B = blockDim.x;
+    for (int b = threadIdx.x; b < nq; b += 4 * B) {
+      f32x4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = b + i * B, r = idx / q4, c4 = idx - r * q4;
+        if (idx < nq) v[i] = ld4(g + (int64_t)r * ldg + 4 * c4) * scale;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = b + i * B, r = idx / q4, c4 = idx - r * q4;
+        if (idx < nq) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) lds[(4 * c4 + c) * ld + r] = v[i][c];
+        }
+      }
+    }
+    return;
+  }
   for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
     const int r = idx / cols_pad, c = idx - r * cols_pad;
     float v = 0.0f;

@@ -350,29 +350,59 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
   LANEVEC(s_db);
   const int64_t E = a.rowptr[a.n];
   const int64_t nchunks = (E + kChunk - 1) / kChunk;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+  const int64_t G = gridDim.x;
+  // The chunk's inputs are loaded one chunk ahead (its receiver ids two
+  // ahead, so the d agg row gather never waits on them): the gathers and the
+  // tiled saves of chunk c + G are in flight while chunk c computes.
+  auto recv_of = [&](int64_t c) -> int {
+    const int64_t base = (c * kWaves + w) * 32, e = base + j;
+    return (c < nchunks && base < E) ? a.recv[e < E ? e : E - 1] : 0;
+  };
+  auto fetch = [&](int64_t c, int rv, f32x16 (&dm)[TH], f32x16 (&yh)[TH], f32x16 (&h1)[TH],
+                   f32x16 (&h2)[TH], float& rs, int& prv, int& nxt) {
     const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
-    const int nvalid = clamp_items(E - base);
-    const bool valid = e < E;
-    const int64_t ec = valid ? e : E - 1;
-    f32x16 dm[TH], yh[TH], h1[TH], h2[TH];
-    float rs = 0.0f;
-    int rv = 0;
-    const int prv = (nvalid > 0 && base > 0) ? a.recv[base - 1] : -1;  // receivers around the tile
-    const int nxt = base + 32 < E ? a.recv[base + 32] : -1;
-    if (nvalid > 0) {  // tiles past the last valid one are not allocated
-      rv = a.recv[ec];
+    if (c < nchunks && base < E) {  // tiles past the last valid one are not allocated
       load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
       load_tiled<TH>(yh, a.yh + tile * (32 * H));
       load_tiled<TH>(h1, a.hs + tile * (32 * H));
       if (NL == 3) load_tiled<TH>(h2, a.hs2 + tile * (32 * H));
-      rs = a.rstd[ec];
+      rs = a.rstd[e < E ? e : E - 1];
+      // receivers around the tile: lane 0 reads the one before, lane 1 the
+      // one after, as one divergent load (a uniform-address load would be
+      // read into an SGPR at once -- a wait on every prefetch in flight);
+      // segment_sum_store takes them with readlane
+      const int64_t q = j == 0 ? base - 1 : base + 32;
+      const bool has = j == 0 ? base > 0 : base + 32 < E;
+      prv = has ? a.recv[has ? q : base] : -1;
+      nxt = prv;
     } else {
       zero<TH>(dm);
       zero<TH>(yh);
       zero<TH>(h1);
       if (NL == 3) zero<TH>(h2);
+      rs = 0.0f;
+      prv = nxt = -1;
     }
+  };
+  f32x16 dm[TH], yh[TH], h1[TH], h2[TH];
+  float rs;
+  int prv, nxt;
+  int rv = recv_of(blockIdx.x);
+  fetch(blockIdx.x, rv, dm, yh, h1, h2, rs, prv, nxt);
+  int rv_n = recv_of(blockIdx.x + G);
+  // drain the first chunk's loads: the waitcnt pass merges this preheader
+  // state into the loop header and would otherwise make every iteration wait
+  // for its own freshly issued prefetch
+  __builtin_amdgcn_s_waitcnt(0);
+  for (int64_t c = blockIdx.x; c < nchunks; c += G) {
+    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+    const int nvalid = clamp_items(E - base);
+    const bool valid = e < E;
+    f32x16 dm_n[TH], yh_n[TH], h1_n[TH], h2_n[TH];
+    float rs_n;
+    int prv_n, nxt_n;
+    fetch(c + G, rv_n, dm_n, yh_n, h1_n, h2_n, rs_n, prv_n, nxt_n);
+    const int rv_n2 = recv_of(c + 2 * G);
     zero_if<TH>(h1, !valid);
     if (NL == 3) zero_if<TH>(h2, !valid);
     f32x16 dh[TH];
@@ -403,23 +433,33 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
     }
     // !W1E: sgnn_edge_latent_grad forms dE0 and dW1e of this layer
     constexpr bool w1e_here = W1E;
-    if (nvalid > 0) {
-      if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
-      if (w1e_here) {
+    store_row_clayout_if<TH>(buf_rsrc(a.dh_rows + base * H), j * (4 * H), valid, dh);
+    if (w1e_here) {
+      if (nvalid > 0) {
         load_tiled<TH>(e0, a.e0t + tile * (32 * H));
         zero_if<TH>(e0, !valid);
       }
-    }
-    lds_store_items<TH>(im.sA, ldh, j, dh);
-    if (w1e_here) lds_store_items<TH>(im.sB, ldh, j, e0);
-    wave_lds_sync();
-    if (nvalid > 0)
-      segment_sum_store<TH>(im.sA, ldh, rv, nvalid, base, tile, prv, nxt, a.du, a.cin, a.cout);
-    if (w1e_here) {
+      lds_store_items<TH>(im.sA, ldh, j, dh);
+      lds_store_items<TH>(im.sB, ldh, j, e0);
       __syncthreads();
       outer_tiles<NT>(acc_w1, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1e = sum dh (x) e0
       __syncthreads();
     }
+    // dU: receiver segment sums of dh (overwrites dh)
+    segment_sum_rows<TH>(dh, rv, valid, __builtin_amdgcn_readlane(prv, 0), __builtin_amdgcn_readlane(nxt, 1),
+                         tile, a.du, a.cin, a.cout);
+#pragma unroll
+    for (int t = 0; t < TH; ++t) {
+      dm[t] = dm_n[t];
+      yh[t] = yh_n[t];
+      h1[t] = h1_n[t];
+      if (NL == 3) h2[t] = h2_n[t];
+    }
+    rs = rs_n;
+    prv = prv_n;
+    nxt = nxt_n;
+    rv = rv_n;
+    rv_n = rv_n2;
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
   store_outer<NT>(slab, H, TH, TH, acc_wl);
@@ -430,6 +470,207 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
   store_lane_vec<TH>(v + kWaves * H, s_dg);
   store_lane_vec<TH>(v + 2 * kWaves * H, s_db);
   if (NL == 3) store_lane_vec<TH>(v + 3 * kWaves * H, s_dbm);
+}
+
+// ---------------------------------------------------------------------------
+// The single-scale training variant at H = 64 (NL = 2, dE0 / dW1e left to the
+// latent pass), sized for TWO workgroups per CU: LDS = Wl^T (16 KB) + the two
+// [128 items][64] item images (32 KB each) = 80 KB, with no row padding --
+// rows are XOR-swizzled in 16-B groups instead (swz) -- and LayerNorm gamma
+// read from L2; <= 256 VGPRs.  Two independent workgroups per CU interleave
+// one's MFMA phases with the other's LayerNorm / gather / segment-sum phases,
+// which a single 4-wave workgroup (1 wave per SIMD) runs back to back.
+SGNN_DEV int swz(int r, int u) { return r * 64 + (u ^ ((r & 15) << 2)); }
+
+// scale * W^T of a [64 out k][64 in u] block (leading dim ldw, 16-B aligned)
+// into a swizzled [u][k] image: four float4 loads per thread issued
+// together, then written transposed.
+SGNN_DEV void swz_stage_wt(float* wt, const float* w, int ldw, float scale) {
+  static_assert(kBlock == 256, "W staging: 16 floats per thread");
+  const int t = threadIdx.x, u0 = 4 * (t & 15), k0 = t >> 4;
+  f32x4 wv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) wv[i] = ld4(w + (k0 + 16 * i) * ldw + u0) * scale;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wt[swz(u0 + c, k0 + 16 * i)] = wv[i][c];
+}
+
+// Item-on-lane register tile -> swizzled [item][64] image row `item`.
+SGNN_DEV void swz_store_items(float* img, int item, const f32x16 (&x)[2]) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 v;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = x[t][4 * g + c];
+      st4(img + swz(item, 32 * t + 8 * g + 4 * h), v);
+    }
+}
+
+// Column sums of a wave's 32 swizzled image rows (rows past nvalid hold
+// zeros) with 16-B reads: lane L reads unit group L & 15 of rows
+// (L >> 4) + 4k, then a butterfly over the four row phases.  Every lane ends
+// with units 4 (L & 15) + c.  Row (L >> 4) + 4k has XOR term
+// 4 (L >> 4) + 16 (k & 3): four per-lane offsets, the row in the immediate.
+SGNN_DEV f32x4 swz_col_sums(const float* slice) {
+  const int L = lane_id(), ug = L & 15, ro = L >> 4;
+  const int cc = ro * 64 + ((4 * ug) ^ (4 * ro));
+  f32x4 s0 = {0.0f, 0.0f, 0.0f, 0.0f}, s1 = s0;
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+    s0 += ld4(slice + (cc ^ (16 * (k & 3))) + 256 * k);
+    s1 += ld4(slice + (cc ^ (16 * ((k + 1) & 3))) + 256 * (k + 1));
+  }
+  s0 += s1;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    s0[c] += __shfl_xor(s0[c], 16, 64);
+    s0[c] += __shfl_xor(s0[c], 32, 64);
+  }
+  return s0;
+}
+
+// mfma_outer over the 128 items of two swizzled images (one 32x32 tile).
+// Row 2s + h has (row & 15) = 2(s & 7) + h, so its XOR term is 8(s & 7) ^ 4h:
+// eight per-lane column offsets per operand, the row in the immediate.
+SGNN_DEV void swz_outer(f32x16& acc, const float* A, int ua, const float* B, int vb) {
+  constexpr int G = 4, NS = kChunk / 2;
+  const int l = lane_id() & 31, h = lane_id() >> 5;
+  const int ca = h * 64 + ((ua + l) ^ (4 * h)), cb = h * 64 + ((vb + l) ^ (4 * h));
+  auto ra = [&](int s) { return A[(ca ^ (8 * (s & 7))) + 128 * s]; };
+  auto rb = [&](int s) { return B[(cb ^ (8 * (s & 7))) + 128 * s]; };
+  float a0[G], b0[G], a1[G], b1[G];
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    a0[i] = ra(i);
+    b0[i] = rb(i);
+  }
+#pragma unroll
+  for (int s = 0; s < NS; s += 2 * G) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      a1[i] = ra(s + G + i);
+      b1[i] = rb(s + G + i);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < G; ++i) acc = mfma32(a0[i], b0[i], acc);
+    if (s + 2 * G < NS) {
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        a0[i] = ra(s + 2 * G + i);
+        b0[i] = rb(s + 2 * G + i);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < G; ++i) acc = mfma32(a1[i], b1[i], acc);
+  }
+}
+
+// acc[t][u] += sum_k W[k][u] x[k] with W^T staged swizzled ([u][k] image)
+SGNN_DEV void swz_matvec_t(f32x16 (&acc)[2], const float* wt, const f32x16 (&x)[2]) {
+  const int l = lane_id() & 31, h = lane_id() >> 5;
+#pragma unroll
+  for (int tk = 0; tk < 2; ++tk)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 w[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) w[t] = ld4(wt + swz(32 * t + l, 32 * tk + 8 * g + 4 * h));
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[t] = mfma32(w[t][c], x[tk][4 * g + c], acc[t]);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+void k_edge_bwd64(EdgeBwdArgs a) {
+  constexpr int TH = 2, H = 64;
+  extern __shared__ float lds[];
+  float* wt = lds;                  // Wl^T [u][k]
+  float* bufA = wt + H * H;         // [128 items][64]
+  float* bufB = bufA + kChunk * H;
+  swz_stage_wt(wt, a.wl, H, 1.0f);
+  __syncthreads();
+  const int w = wave_id(), l = lane_id(), j = l & 31;
+  float* sA = bufA + w * 32 * H;    // this wave's rows (w*32 + j; (row & 15) == (j & 15))
+  float* sB = bufB + w * 32 * H;
+  const int tu = w >> 1, tv = w & 1;   // the wave's dWl tile
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  f32x4 s_dbl = {0.0f, 0.0f, 0.0f, 0.0f}, s_dg = s_dbl, s_db = s_dbl;   // units 4 (lane & 15) + c
+  const int64_t E = a.rowptr[a.n];
+  const int64_t nchunks = (E + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+    const int nvalid = clamp_items(E - base);
+    const bool valid = e < E;
+    f32x16 dm[TH], yh[TH], h1[TH];
+    float rs = 0.0f;
+    int rv = 0, nb = -1;
+    if (nvalid > 0) {  // tiles past the last valid one are not allocated
+      const int64_t ec = valid ? e : E - 1;
+      rv = a.recv[ec];
+      load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
+      load_tiled<TH>(yh, a.yh + tile * (32 * H));
+      load_tiled<TH>(h1, a.hs + tile * (32 * H));
+      rs = a.rstd[ec];
+      // receivers around the tile: lane 0 the one before, lane 1 the one after
+      const int64_t q = j == 0 ? base - 1 : base + 32;
+      const bool has = j == 0 ? base > 0 : base + 32 < E;
+      nb = has ? a.recv[has ? q : base] : -1;
+    } else {
+      zero<TH>(dm);
+      zero<TH>(yh);
+      zero<TH>(h1);
+    }
+    zero_if<TH>(dm, !valid);
+    zero_if<TH>(h1, !valid);
+    // LayerNorm backward (graph_network.py:148), its affine sums
+    f32x16 dy[TH];
+    acc_layernorm_bwd<TH>(dm, yh, rs, a.gamma, dy);
+    zero_if<TH>(dy, !valid);
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];   // dgamma terms (dm = 0 off the edges)
+    swz_store_items(sA, j, dm);
+    swz_store_items(sB, j, yh);
+    wave_lds_sync();
+    s_db += swz_col_sums(sA);
+    s_dg += swz_col_sums(sB);
+    wave_lds_sync();
+    // last Linear: dWl += dy (x) h1, dbl += dy, dh = (Wl^T dy) * [h1 > 0]
+    swz_store_items(sA, j, dy);
+    swz_store_items(sB, j, h1);
+    wave_lds_sync();
+    s_dbl += swz_col_sums(sA);
+    __syncthreads();
+    swz_outer(acc, bufA, 32 * tu, bufB, 32 * tv);
+    __syncthreads();
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    swz_matvec_t(dh, wt, dy);
+    relu_mask<TH>(dh, h1, valid);
+    store_row_clayout_if<TH>(buf_rsrc(a.dh_rows + base * H), j * (4 * H), valid, dh);
+    segment_sum_rows<TH>(dh, rv, valid, __builtin_amdgcn_readlane(nb, 0), __builtin_amdgcn_readlane(nb, 1),
+                         tile, a.du, a.cin, a.cout);
+  }
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  store_tile_rowmajor(slab + (32 * tu) * H + 32 * tv, H, acc);
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, 2);
+  if (l < 16) {
+    st4(v + w * H + 4 * l, s_dbl);
+    st4(v + kWaves * H + w * H + 4 * l, s_dg);
+    st4(v + 2 * kWaves * H + w * H + 4 * l, s_db);
+  }
 }
 
 // ===========================================================================
@@ -1466,23 +1707,23 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const sgnn_reduce_desc* de
   const int64_t total = (int64_t)d.nrows * d.ncols;
   const int e = threadIdx.x & 31, q = threadIdx.x >> 5;
   const int64_t idx = (int64_t)(blockIdx.x - block_start[lo]) * 32 + e;
-  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+  // eight independent chains per thread: with 512 slabs per kind the loads in
+  // flight, not the bytes, set the rate
+  float s[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   if (idx < total) {
     const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
     const float* base = d.src + d.offset + (int64_t)r * d.src_ld + cc;
     for (int k = 0; k < d.nrep; ++k) {
       const float* p = base + (int64_t)k * d.rep_stride;
       int g = q;
-      for (; g + 24 < d.nslab; g += 32) {
-        s0 += p[(int64_t)g * d.slab_stride];
-        s1 += p[(int64_t)(g + 8) * d.slab_stride];
-        s2 += p[(int64_t)(g + 16) * d.slab_stride];
-        s3 += p[(int64_t)(g + 24) * d.slab_stride];
+      for (; g + 56 < d.nslab; g += 64) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] += p[(int64_t)(g + 8 * u) * d.slab_stride];
       }
-      for (; g < d.nslab; g += 8) s0 += p[(int64_t)g * d.slab_stride];
+      for (; g < d.nslab; g += 8) s[0] += p[(int64_t)g * d.slab_stride];
     }
   }
-  part[q][e] = (s0 + s1) + (s2 + s3);
+  part[q][e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   if (q == 0 && idx < total) {
     float t = 0.0f;
@@ -1639,6 +1880,8 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
   if (st) return st;
   if (edge_fn->nlin == 3 && !saves->h2) return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: saves->h2");
   const int H = edge_fn->hidden;
+  if (H == 64 && n * H * 4 >= (int64_t)kBufRecords)
+    return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer_bwd: at most 8M nodes per launch at H = 64");
   EdgeBwdArgs a{dagg, rowptr, send, recv, n, saves->h, saves->h2, saves->yhat, saves->rstd, e0t,
                 e_scale, last_w(edge_fn), mid_w(edge_fn), edge_fn->w1 + 2 * H, edge_fn->ln_g, du,
                 cin, cout, dh_rows, de0t, de0_accumulate, slab,
@@ -1658,6 +1901,10 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
     if (nl == 3)
       run_wgrad<4, 4>(wg(p.d2_out, 1, 0, saves->h, 1, 0, slab, 2 * H * H, H, vb + 3 * W * H, ss, 0, Edev),
                       nslab, stream);
+    return check_launch("edge_layer_bwd");
+  }
+  if (H == 64 && edge_fn->nlin == 2 && !de0t) {  // single-scale training: two workgroups per CU
+    launch_bwd(k_edge_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
     return check_launch("edge_layer_bwd");
   }
   const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin) - (de0t ? 0 : 4 * (size_t)H * (H + 4));
@@ -2007,6 +2254,103 @@ __global__ __launch_bounds__(kBlock) void k_edge_latent_grad(EdgeLatentGradArgs 
   }
 }
 
+// dW1e_k = sum_e dh_k[e] (x) e0[e] for one layer (H = 64), streamed: every
+// wave's next 32 edges (dh_k rows and the e0 tile, both contiguous) load into
+// registers while the current chunk's outer product runs, so the launch is
+// one HBM stream under the MFMAs instead of load -> barrier -> MFMA rounds.
+// (Folding this layer's dE0 term in as well -- dE0 += 2^k W1e_k^T dh_k per
+// layer on the side stream -- measured slower: the W1e^T image keeps it at
+// one workgroup per CU and the dE0 read-modify-write per layer moves more
+// bytes than k_edge_de0's single pass.)
+template <int TH>
+__global__ __launch_bounds__(kBlock) void k_edge_w1e_grad(EdgeLatentGradArgs a) {
+  constexpr int H = 32 * TH, ldh = H + 4;
+  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
+  extern __shared__ float lds[];
+  float* bufA = lds;                  // dh_k item image
+  float* bufB = bufA + kChunk * ldh;  // e0 item image
+  const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
+  const int w = wave_id(), j = im.j;
+  f32x16 acc[NT];
+  zero_acc<NT>(acc);
+  const int64_t E = a.rowptr[a.n];
+  const int64_t nchunks = (E + kChunk - 1) / kChunk, G = gridDim.x;
+  auto fetch = [&](int64_t c, f32x16 (&e0)[TH], f32x16 (&dh)[TH]) {
+    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+    if (c < nchunks && base < E) {  // tiles past the last valid one are not allocated
+      load_tiled<TH>(e0, a.e0t + tile * (32 * H));
+      load_row_clayout<TH>(dh, a.dh[0] + (e < E ? e : E - 1) * H);
+    } else {
+      zero<TH>(e0);
+      zero<TH>(dh);
+    }
+  };
+  f32x16 e0[TH], dh[TH];
+  fetch(blockIdx.x, e0, dh);
+  // drain the first chunk's loads here: the waitcnt pass merges this
+  // preheader state into the loop header and would otherwise make every
+  // iteration wait for its own freshly issued prefetch
+  __builtin_amdgcn_s_waitcnt(0);
+  for (int64_t c = blockIdx.x; c < nchunks; c += G) {
+    f32x16 e0n[TH], dhn[TH];
+    fetch(c + G, e0n, dhn);
+    const bool valid = (c * kWaves + w) * 32 + j < E;
+    zero_if<TH>(e0, !valid);
+    zero_if<TH>(dh, !valid);
+    lds_store_items<TH>(im.sA, ldh, j, dh);
+    lds_store_items<TH>(im.sB, ldh, j, e0);
+    __syncthreads();
+    outer_tiles<NT>(acc, TH, TH, bufA, ldh, 0, bufB, ldh, 0);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TH; ++t) {
+      e0[t] = e0n[t];
+      dh[t] = dhn[t];
+    }
+  }
+  store_outer<NT>(a.slab[0] + blockIdx.x * a.slab_stride + H * H, H, TH, TH, acc);
+}
+
+// dE0 = sum_k 2^k W1e_k^T dh_k over L <= 5 layers (H = 64): the L swizzled
+// 64x64 images of 2^k W1e_k^T fill exactly 80 KB of LDS, so two 8-wave
+// workgroups share a CU (4 waves per SIMD); no item images and no barriers in
+// the loop -- every wave owns whole 32-edge tiles (grid-stride over waves)
+// and prefetches layer k+1's dh rows under layer k's 64 MFMAs.
+constexpr int kDe0Waves = 8;   // 512-thread workgroups: 4 waves per SIMD at <= 128 VGPRs
+
+template <int L>
+__global__ __launch_bounds__(64 * kDe0Waves) __attribute__((amdgpu_waves_per_eu(4)))
+void k_edge_de0(EdgeLatentGradArgs a) {
+  constexpr int TH = 2, H = 64;
+  extern __shared__ float lds[];
+  if (threadIdx.x < kBlock) {
+#pragma unroll
+    for (int k = 0; k < L; ++k) swz_stage_wt(lds + k * H * H, a.we[k], 3 * H, a.scale[k]);
+  }
+  __syncthreads();
+  const int j = lane_id() & 31;
+  const int64_t E = a.rowptr[a.n];
+  const int64_t ntiles = (E + 31) / 32, nw = (int64_t)gridDim.x * kDe0Waves;
+  for (int64_t tile = (int64_t)blockIdx.x * kDe0Waves + wave_id(); tile < ntiles; tile += nw) {
+    const int64_t e = tile * 32 + j, ec = e < E ? e : E - 1;
+    f32x16 de[TH], cur[TH], nxt[TH];
+    zero<TH>(de);
+    load_row_clayout<TH>(cur, a.dh[0] + ec * H);
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      if (k + 1 < L) load_row_clayout<TH>(nxt, a.dh[k + 1] + ec * H);
+      zero_if<TH>(cur, e >= E);
+      swz_matvec_t(de, lds + k * H * H, cur);
+      if (k + 1 < L) {
+#pragma unroll
+        for (int t = 0; t < TH; ++t) cur[t] = nxt[t];
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one layer's rows in flight, not all L
+    }
+    store_tiled<TH>(a.de0t + tile * (32 * H), de);
+  }
+}
+
 // DE / DW: both halves (one pass), dE0 only (no item images), or dW1e only
 // (L = 1, one layer per launch).
 template <int L, bool DE, bool DW>
@@ -2020,6 +2364,14 @@ void launch_latent(const EdgeLatentGradArgs& a, int nslab, void* stream) {
 template <int L>
 void launch_latent(const EdgeLatentGradArgs& a, int nslab, void* stream, bool dw) {
   if (dw) return launch_latent<L, true, true>(a, nslab, stream);
+  if constexpr (L <= 5) {   // dE0 only: the 80 KB two-workgroups-per-CU pass
+    const size_t lds = 4 * (size_t)L * 64 * 64;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_edge_de0<L>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_edge_de0<L>, dim3((unsigned)nslab), dim3(64 * kDe0Waves), lds,
+                       static_cast<hipStream_t>(stream), a);
+    return;
+  }
   launch_latent<L, true, false>(a, nslab, stream);
 }
 }  // namespace
@@ -2060,7 +2412,7 @@ extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp
       b.slab[0] = a.slab[k];
       b.scale[0] = a.scale[k];
       b.nlayers = 1;
-      launch_latent<1, false, true>(b, nslab, stream);
+      launch_bwd(k_edge_w1e_grad<2>, nslab, 4 * (size_t)(2 * kChunk * (H + 4)), stream, b);
     }
     return check_launch("edge_latent_grad");
   }
@@ -2078,3 +2430,4 @@ extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp
   }
   return check_launch("edge_latent_grad");
 }
+

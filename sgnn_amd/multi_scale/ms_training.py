@@ -24,7 +24,7 @@ import torch
 from .. import _hip, engine
 from .._hip import check, lib, stream_ptr
 from ..train import DataParallel, device_random_walk_noise
-from ..training import (DEFAULT_NSLAB, Adam, FlatParams, SlabArena, _saves, _Timer, emb_args,
+from ..training import (MS_NSLAB, Adam, FlatParams, SlabArena, _saves, _Timer, emb_args,
                         embedding_backward, nslab_table)
 from . import ms_engine
 from .ms_engine import EDGE_TYPES
@@ -46,7 +46,7 @@ class MSTrainWorkspace:
     """Saved activations, backward buffers and slabs for one (n, T, static graph)."""
 
     def __init__(self, gnn, n: int, T: int, dim: int, graphs: Dict[str, engine.CsrGraph],
-                 device: torch.device, nslab: int = DEFAULT_NSLAB):
+                 device: torch.device, nslab: int = MS_NSLAB):
         L = lib()
         H = gnn.latent_dim
         self.H, self.n, self.T, self.dim = H, n, T, dim
@@ -260,7 +260,7 @@ class MultiScaleTrainer:
     def __init__(self, simulator, lr_init: float = 1e-3, lr_decay: float = 0.1,
                  lr_decay_steps: int = 15000, noise_std: float = 0.02,
                  loss_weight_position: float = 1.0, loss_weight_strain: float = 1.0,
-                 group=None, nslab: int = DEFAULT_NSLAB):
+                 group=None, nslab: int = MS_NSLAB):
         check_trainable(simulator)
         self.sim = simulator
         self.gnn = simulator._multi_scale_gnn

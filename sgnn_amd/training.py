@@ -20,7 +20,8 @@ import torch.nn as nn
 from . import _hip, engine
 from ._hip import SgnnReduceDesc, SgnnSaves, check, lib, stream_ptr
 
-DEFAULT_NSLAB = 256  # persistent workgroups (one per CU) for the edge backward kernels
+DEFAULT_NSLAB = 512  # persistent edge-backward workgroups: two per CU (k_edge_bwd64 sizes its LDS for that)
+MS_NSLAB = 256      # multi-scale (H = 128 items / weight-gradient kernels, one workgroup per CU)
 NODE_NSLAB = 256     # node-level backward kernels (128 measured slower: fewer CUs busy)
 
 

@@ -35,7 +35,7 @@ print(f"nslab={ns}: kernel span {t[:, 31].max() - t0:.0f} cycles; wave start spr
       f"{np.percentile(t[:, 0] - t0, [0, 50, 90, 100]).round()} ; end spread "
       f"{np.percentile(t[:, 31] - t0, [0, 50, 90, 100]).round()}")
 print(f"prologue {np.mean(t[:, 1] - t[:, 0]):.0f}")
-names = ["issue", "LN+sums", "dy img+sync", "outer+sync", "matvec", "tail+latch"]
+names = ["loads+LN", "LN sums", "dy img+sync", "outer+sync", "matvec", "dh st+segsum"]
 rows = []
 for ci in range(4):
     sl = 2 + 7 * ci
