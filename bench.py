@@ -337,7 +337,10 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps,
         # fused layer (sgnn_interaction_layer): edge MLP (two H x H Linears per edge, u/v factorised
         # out of the first) + node MLP (2H x H, H x H) + the next layer's u/v (2 x H x H) per node
         kernel = "k_layer16"
-        flops = E * 4 * H * H + n * 10 * H * H
+        # per launch, averaged over the L launches: layer 0 also runs Encoder.edge_fn on its edges
+        # (dim+1 -> H -> H) and the last layer the decoder (H -> H -> dim+1) instead of the next u/v
+        flops = (L * E * 4 * H * H + E * 2 * (H * H + (dim + 1) * H)
+                 + (L - 1) * n * 10 * H * H + n * (8 * H * H + 2 * H * (dim + 1))) / L
         # e0 row (4H) + ids (8) per edge; u/v rows read (8H), x read (4H), x/u/v written (12H) per node
         alg_bytes = E * (4 * H + 8) + n * 24 * H
     else:
