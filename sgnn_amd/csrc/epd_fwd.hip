@@ -258,7 +258,8 @@ struct EdgeLayerArgs {
 };
 
 template <int TH, bool TRAIN, int NL>
-__global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TH > 2 ? 1 : 2)))
+void k_edge_layer(EdgeLayerArgs a) {
   // W1e always sits in LDS (67.6 KB at H = 128, next to the per-wave sum
   // buffers); the last (and middle) Linear is an LDS image at H = 64 and
   // read from L2 at H = 128.
@@ -297,31 +298,39 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
   const int lg = (nwg % 8 == 0) ? (bid % 8) * (nwg / 8) + bid / 8 : bid;
   const int64_t nw = (int64_t)nwg * kWaves;
   const int64_t t_begin = (int64_t)lg * kWaves + w, t_end = ntiles;
-  // H = 64 software pipeline: the next tile's indices and e0 are loaded while
-  // this tile computes, and this tile's u[recv] / v[send] gathers are issued
-  // before its W1e e0 product and added after it (the gather latency hides
-  // behind 64 MFMAs).  H = 128 keeps the in-order form (registers).
-  constexpr bool PF = TH == 2;
-  int rv_n = 0, s_n = 0, prv_n = -1, nxt_n = -1;  // int32: no widening right after the load
+  // Software pipeline: the next tile's indices and e0 are loaded while this
+  // tile computes, and this tile's u[recv] / v[send] gathers are issued before
+  // its W1e e0 product and added after it (the gather latency hides behind
+  // its MFMAs).  H = 128 runs one workgroup per CU (LDS), so the wave may use
+  // the whole register file for the prefetched operands.
+  constexpr bool PF = true;
+  int rv_n = 0, s_n = 0, nb_n = -1;  // int32: no widening right after the load
   f32x4 xg_n[TH * 4];
   auto fetch = [&](int64_t t) {
     const int64_t b = t * 32, ee = b + j;
     const int64_t ecc = ee < E ? ee : E - 1;
     rv_n = a.recv[ecc];
     s_n = a.send[ecc];
-    prv_n = b > 0 ? a.recv[b - 1] : -1;  // receivers around the tile
-    nxt_n = b + 32 < E ? a.recv[b + 32] : -1;
+    // receivers around the tile: lane 0 reads the one before, lane 1 the one
+    // after, as one divergent load (a uniform-address load goes to an SGPR at
+    // once -- a wait on every gather in flight); read back with readlane
+    const bool has = j == 0 ? b > 0 : b + 32 < E;
+    nb_n = has ? a.recv[j == 0 ? b - 1 : b + 32] : -1;
     const float* src = a.e0t + t * (32 * H) + l * 4;
 #pragma unroll
     for (int q = 0; q < TH * 4; ++q) xg_n[q] = ld4(src + q * 256);
   };
   if (PF && t_begin < t_end) fetch(t_begin);
+  // drain the first tile's loads: the waitcnt pass merges this preheader
+  // state into the loop header and would otherwise make every iteration wait
+  // for its own freshly issued prefetch
+  __builtin_amdgcn_s_waitcnt(0);
   for (int64_t tile = t_begin; tile < t_end; tile += nw) {
     const int64_t base = tile * 32;
     const int64_t e = base + j;
     const bool valid = e < E;
     if (!PF) fetch(tile);
-    const int rv = rv_n, prv = prv_n, nxt = nxt_n;
+    const int rv = rv_n, nb = nb_n;
     const int s = s_n;
     f32x4 xg[TH * 4];
 #pragma unroll
@@ -369,7 +378,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_layer(EdgeLayerArgs a) {
     wave_lds_sync();
     // wave-segmented sum over the receiver-sorted CSR: lane = latent unit
     const int nvalid = (E - base) < 32 ? (int)(E - base) : 32;
-    segment_sum_store<TH>(ml, ldh, rv, nvalid, base, tile, prv, nxt, a.agg, a.cin, a.cout);
+    segment_sum_store<TH>(ml, ldh, rv, nvalid, base, tile, __builtin_amdgcn_readlane(nb, 0),
+                          __builtin_amdgcn_readlane(nb, 1), a.agg, a.cin, a.cout);
     wave_lds_sync();
   }
 }
