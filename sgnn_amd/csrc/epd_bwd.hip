@@ -1426,8 +1426,9 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
     const bool valid = e < E;
     const int64_t ec = valid ? e : E - 1;
     const int rv = a.recv[ec];
-    const int prv = base > 0 ? a.recv[base - 1] : -1;  // receivers around the tile
-    const int nxt = base + 32 < E ? a.recv[base + 32] : -1;
+    // receivers around the tile (lane 0: before, lane 1: after; one divergent load, readlane at use)
+    const bool has = j == 0 ? base > 0 : base + 32 < E;
+    const int nb = has ? a.recv[j == 0 ? base - 1 : base + 32] : -1;
     f32x16 dy[TH];
     {
       f32x16 dm[TH], yh[TH];
@@ -1485,7 +1486,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
     if (valid) store_row_clayout<TH>(a.dh_rows + e * H, dh);
     lds_store_items<TH>(sl, ldh, j, dh);
     wave_lds_sync();
-    segment_sum_store<TH>(sl, ldh, rv, nvalid, base, tile, prv, nxt, a.du, a.cin, a.cout);
+    segment_sum_store<TH>(sl, ldh, rv, nvalid, base, tile, __builtin_amdgcn_readlane(nb, 0),
+                          __builtin_amdgcn_readlane(nb, 1), a.du, a.cin, a.cout);
     wave_lds_sync();
   }
   float* v = a.slab + blockIdx.x * a.slab_stride + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, NL);

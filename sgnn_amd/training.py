@@ -327,13 +327,19 @@ class TrainWorkspace:
             return
         pre = "_encode_process_decode."
         g = lambda name: grads[pre + name]
+        dev = self.arena.device
+        # one table per interaction layer (reduced on the side stream as soon
+        # as that layer's backward is done) + one for the encoders / decoder
+        self._reduce_layer = []
+        for k in range(self.L):
+            lay = self.slabs.layout(self.H, self.nlin, self.feat, self.dim)
+            lay.interaction(g, f"_processor.gnn_stacks.{k}.", k, 2.0 ** k)
+            self._reduce_layer.append(lay.upload(dev))
         lay = self.slabs.layout(self.H, self.nlin, self.feat, self.dim)
         lay.enc_node(g, "_encoder.node_fn.", self.emb_g if use_emb else None)
         lay.enc_edge(g, "_encoder.edge_fn.")
-        for k in range(self.L):
-            lay.interaction(g, f"_processor.gnn_stacks.{k}.", k, 2.0 ** k)
         lay.decoder(g, "_decoder.node_fn.", self.loss_out)
-        self._descs_dev, self._block_start, self._ndesc, self._nblocks = lay.upload(self.arena.device)
+        self._descs_dev, self._block_start, self._ndesc, self._nblocks = lay.upload(dev)
         self._descs_key = key
 
 
@@ -514,6 +520,13 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                             tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV],
                             tw.scratch.data_ptr(), s),
               "sgnn_uv_bwd")
+        # layer k's slabs (NODE, EDGE + its dW1e on the side stream, UV) are
+        # complete: sum them into the gradients on the side stream, beside the
+        # layers below (HBM-bound, small LDS: it fits next to the main kernels)
+        ev["g"].record(main)
+        side.wait_event(ev["g"])
+        dd, bs, nd, nb = tw._reduce_layer[k]
+        check(L.sgnn_reduce_slabs(dd.data_ptr(), bs.data_ptr(), nd, nb, side.cuda_stream), "sgnn_reduce_slabs")
     # the encoder-node backward needs only g = dL/dx_0: side stream, beside
     # the edge-latent pass and the edge-encoder backward
     ev["g"].record(main)
