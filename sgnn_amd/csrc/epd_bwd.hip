@@ -9,7 +9,7 @@
 //   k_edge_bwd(k)   edge MLP + LayerNorm backward from d agg_k[recv]:
 //                   dh (ReLU-masked) -> segment sums dU (receiver CSR),
 //                   dh rows for dV, dE0 += 2^k W1e^T dh
-//   k_uv_bwd(k)     g_k = dx_k' + W1i^T dU + W1j^T dV  (dV gathered through
+//   k_uv_bwd64(k)   g_k = dx_k' + W1i^T dU + W1j^T dV  (dV gathered through
 //                   the sender-sorted transpose CSR, deterministic)
 //   k_enc_node_bwd, k_enc_edge_bwd   Encoder MLPs
 //   k_reduce_slabs  weight gradients
@@ -805,35 +805,30 @@ struct UvBwdArgs {
   int64_t slab_stride;
 };
 
-template <int TH>
-__global__ __launch_bounds__(kBlock) void k_uv_bwd(UvBwdArgs a) {
-  constexpr bool GW = TH > 2;
-  constexpr int H = 32 * TH, ldh = H + 4, ldw = GW ? 3 * H : ldh;
+// H = 64 variant sized for two workgroups per CU (512 workgroups: every
+// 128-node chunk of a 50k graph resident at once instead of 1.5 rounds at
+// one per CU): Wi^T as a swizzled 16 KB LDS image, Wj^T read from L2, the two
+// unpadded swizzled item images (64 KB) -- 80 KB -- and <= 256 VGPRs.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+void k_uv_bwd64(UvBwdArgs a) {
+  constexpr int TH = 2, H = 64;
   extern __shared__ float lds[];
-  float* p = lds;
-  const float* WiT = a.w1;
-  const float* WjT = a.w1 + H;
-  if (!GW) {
-    stage_matrix_t(p, ldh, a.w1, 3 * H, H, H, H, H);
-    stage_matrix_t(p + H * ldh, ldh, a.w1 + H, 3 * H, H, H, H, H);
-    WiT = p;
-    WjT = p + H * ldh;
-    p += 2 * H * ldh;
-  }
-  float* bufA = p;
-  float* bufB = bufA + kChunk * ldh;
+  float* wi = lds;                  // Wi^T [u][k]
+  float* bufA = wi + H * H;         // [128 items][64]
+  float* bufB = bufA + kChunk * H;
+  swz_stage_wt(wi, a.w1, 3 * H, 1.0f);
   __syncthreads();
-  const Imgs im = make_imgs(bufA, ldh, bufB, ldh);
-  const int j = im.j, w = wave_id();
-  constexpr int NT = (TH * TH + kWaves - 1) / kWaves;
-  f32x16 acc_i[NT], acc_j[NT];
-  zero_acc<NT>(acc_i);
-  zero_acc<NT>(acc_j);
-  LANEVEC(s_db1);
+  const int w = wave_id(), l = lane_id(), j = l & 31;
+  float* sA = bufA + w * 32 * H;
+  float* sB = bufB + w * 32 * H;
+  const int tu = w >> 1, tv = w & 1;
+  f32x16 acc_i, acc_j;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc_i[r] = acc_j[r] = 0.0f;
+  f32x4 s_db1 = {0.0f, 0.0f, 0.0f, 0.0f};   // units 4 (lane & 15) + c
   const int64_t nchunks = (a.n + kChunk - 1) / kChunk;
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const int64_t i = c * kChunk + w * 32 + j;
-    const int nvalid = clamp_items(a.n - (c * kChunk + w * 32));
     const bool valid = i < a.n;
     const int64_t ic = valid ? i : a.n - 1;
     f32x16 du[TH], dv[TH], xx[TH], gg[TH];
@@ -846,25 +841,26 @@ __global__ __launch_bounds__(kBlock) void k_uv_bwd(UvBwdArgs a) {
     load_row_clayout<TH>(xx, a.x + ic * H);
     zero_if<TH>(xx, !valid);
     load_row_clayout<TH>(gg, a.dxp + ic * H);
-    matvec_t<TH, TH, GW>(gg, WiT, ldw, du);
-    matvec_t<TH, TH, GW>(gg, WjT, ldw, dv);
+    // g = dx' + W1i^T dU + W1j^T dV  (graph_network.py:197 on cat[x_i, x_j, e])
+    swz_matvec_t(gg, wi, du);
+    matvec_t<TH, TH, true>(gg, a.w1 + H, 3 * H, dv);
     if (valid) store_row_clayout<TH>(a.g + i * H, gg);
-    lds_store_items<TH>(im.sA, ldh, j, du);
-    lds_store_items<TH>(im.sB, ldh, j, xx);
+    swz_store_items(sA, j, du);
+    swz_store_items(sB, j, xx);
     wave_lds_sync();
-    lane_sums<TH>(s_db1, im.sA, ldh, nvalid);
+    s_db1 += swz_col_sums(sA);
     __syncthreads();
-    outer_tiles<NT>(acc_i, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, 0:H] = dU (x) x
+    swz_outer(acc_i, bufA, 32 * tu, bufB, 32 * tv);   // dW1[:, 0:H] = dU (x) x
     __syncthreads();
-    lds_store_items<TH>(im.sA, ldh, j, dv);
+    swz_store_items(sA, j, dv);
     __syncthreads();
-    outer_tiles<NT>(acc_j, TH, TH, bufA, ldh, 0, bufB, ldh, 0);  // dW1[:, H:2H] = dV (x) x
+    swz_outer(acc_j, bufA, 32 * tu, bufB, 32 * tv);   // dW1[:, H:2H] = dV (x) x
     __syncthreads();
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
-  store_outer<NT>(slab, 2 * H, TH, TH, acc_i);
-  store_outer<NT>(slab + H, 2 * H, TH, TH, acc_j);
-  store_lane_vec<TH>(slab + 2 * H * H, s_db1);
+  store_tile_rowmajor(slab + (32 * tu) * 2 * H + 32 * tv, 2 * H, acc_i);
+  store_tile_rowmajor(slab + H + (32 * tu) * 2 * H + 32 * tv, 2 * H, acc_j);
+  if (l < 16) st4(slab + 2 * H * H + w * H + 4 * l, s_db1);
 }
 
 // ===========================================================================
@@ -1813,7 +1809,6 @@ size_t bwd_lds(int kind, int H, int tkf, int nl) {
   switch (kind) {
     case SGNN_SLAB_EDGE: return 4 * (2 * img + mid + H + bufs);
     case SGNN_SLAB_NODE: return 4 * (3 * img + mid + H + bufs);
-    case SGNN_SLAB_UV: return 4 * (2 * img + bufs);
     case SGNN_SLAB_DECODER: return 4 * (H * 36 + img + mid + bufs);
     case SGNN_SLAB_ENC_NODE: {
       const size_t ldb = std::max<size_t>(ldh, 32 * tkf + 4);
@@ -1976,8 +1971,7 @@ extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, 
     run_wgrad<4, 4>(wg(p.dv_out, 0, H, x_in, 0, H, slab, H, 2 * H, -1, ss, n, nullptr), nslab, stream);
     return check_launch("uv_bwd");
   }
-  const size_t lds = bwd_lds(SGNN_SLAB_UV, H, 0, 2);
-  launch_bwd(k_uv_bwd<2>, nslab, lds, stream, a);
+  launch_bwd(k_uv_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
   return check_launch("uv_bwd");
 }
 
