@@ -482,6 +482,15 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
 // which a single 4-wave workgroup (1 wave per SIMD) runs back to back.
 SGNN_DEV int swz(int r, int u) { return r * 64 + (u ^ ((r & 15) << 2)); }
 
+// 0 from an opaque move: per-lane offsets derived from it are recomputed at
+// each use instead of being hoisted out of the caller's chunk loop, where the
+// unrolled helpers below would otherwise keep dozens of address VGPRs live.
+SGNN_DEV int opaque_zero() {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+
 // scale * W^T of a [64 out k][64 in u] block (leading dim ldw, 16-B aligned)
 // into a swizzled [u][k] image: four float4 loads per thread issued
 // together, then written transposed.
@@ -539,7 +548,7 @@ SGNN_DEV f32x4 swz_col_sums(const float* slice) {
 // eight per-lane column offsets per operand, the row in the immediate.
 SGNN_DEV void swz_outer(f32x16& acc, const float* A, int ua, const float* B, int vb) {
   constexpr int G = 4, NS = kChunk / 2;
-  const int l = lane_id() & 31, h = lane_id() >> 5;
+  const int l = (lane_id() & 31) + opaque_zero(), h = lane_id() >> 5;
   const int ca = h * 64 + ((ua + l) ^ (4 * h)), cb = h * 64 + ((vb + l) ^ (4 * h));
   auto ra = [&](int s) { return A[(ca ^ (8 * (s & 7))) + 128 * s]; };
   auto rb = [&](int s) { return B[(cb ^ (8 * (s & 7))) + 128 * s]; };
@@ -861,6 +870,134 @@ void k_uv_bwd64(UvBwdArgs a) {
   store_tile_rowmajor(slab + (32 * tu) * 2 * H + 32 * tv, 2 * H, acc_i);
   store_tile_rowmajor(slab + H + (32 * tu) * 2 * H + 32 * tv, 2 * H, acc_j);
   if (l < 16) st4(slab + 2 * H * H + w * H + 4 * l, s_db1);
+}
+
+// matvec_t's global (L2) mode at H = 64 with one 16-unit k-group of weights
+// in flight at a time (the unbatched form keeps all 64 loads live: spills at
+// the 256-register budget of two waves per SIMD).
+SGNN_DEV void gw_matvec_t64(f32x16 (&acc)[2], const float* w, int ld, const f32x16 (&x)[2]) {
+  const int l = (lane_id() & 31) + opaque_zero(), h = lane_id() >> 5;
+  const __amdgpu_buffer_rsrc_t rs = weight_rsrc(w);
+  const int voff = 4 * (4 * h * ld + l);
+#pragma unroll
+  for (int tk = 0; tk < 2; ++tk)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float wv[4][2];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          wv[c][t] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 128 * t, 4 * (32 * tk + 8 * g + c) * ld, 0));
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[t] = mfma32(wv[c][t], x[tk][4 * g + c], acc[t]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Node MLP backward at H = 64, NL = 2, sized for two workgroups per CU like
+// k_edge_bwd64 / k_uv_bwd64: Wl^T swizzled in LDS (16 KB), W1^T's agg and x
+// halves read from L2, two unpadded swizzled item images (64 KB) -- 80 KB --
+// and <= 256 VGPRs (g is read again for dx' instead of kept live).
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+void k_node_bwd64(NodeBwdArgs a) {
+  constexpr int TH = 2, H = 64;
+  extern __shared__ float lds[];
+  float* wl = lds;                  // Wl^T [u][k]
+  float* bufA = wl + H * H;
+  float* bufB = bufA + kChunk * H;
+  swz_stage_wt(wl, a.wl, H, 1.0f);
+  __syncthreads();
+  const int w = wave_id(), l = lane_id(), j = l & 31;
+  float* sA = bufA + w * 32 * H;
+  float* sB = bufB + w * 32 * H;
+  const int tu = w >> 1, tv = w & 1;
+  f32x16 acc_wl, acc_wa, acc_wx;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc_wl[r] = acc_wa[r] = acc_wx[r] = 0.0f;
+  f32x4 s_db1 = {0.0f, 0.0f, 0.0f, 0.0f}, s_dbl = s_db1, s_dg = s_db1, s_db = s_db1;
+  const int64_t nchunks = (a.n + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t i = c * kChunk + w * 32 + j;
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : a.n - 1;
+    f32x16 dy[TH], h1[TH];
+    {
+      f32x16 gi[TH], yh[TH];
+      load_row_clayout<TH>(gi, a.g + ic * H);
+      zero_if<TH>(gi, !valid);
+      load_row_clayout<TH>(yh, a.yh + ic * H);
+      // LayerNorm backward (graph_network.py:219 LayerNorm) and its affine sums
+      acc_layernorm_bwd<TH>(gi, yh, a.rstd[ic], a.gamma, dy);
+      zero_if<TH>(dy, !valid);
+#pragma unroll
+      for (int t = 0; t < TH; ++t) yh[t] *= gi[t];
+      swz_store_items(sA, j, gi);
+      swz_store_items(sB, j, yh);
+      wave_lds_sync();
+      s_db += swz_col_sums(sA);
+      s_dg += swz_col_sums(sB);
+      wave_lds_sync();
+    }
+    load_row_clayout<TH>(h1, a.hn + ic * H);   // after the LayerNorm part: fewer rows live at once
+    zero_if<TH>(h1, !valid);
+    // last Linear: dWl += dy (x) h1, dbl += dy, dh = (Wl^T dy) * [h1 > 0]
+    swz_store_items(sA, j, dy);
+    swz_store_items(sB, j, h1);
+    wave_lds_sync();
+    s_dbl += swz_col_sums(sA);
+    __syncthreads();
+    swz_outer(acc_wl, bufA, 32 * tu, bufB, 32 * tv);
+    __syncthreads();
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    swz_matvec_t(dh, wl, dy);
+    relu_mask<TH>(dh, h1, valid);
+    // first Linear on cat[agg, x] (graph_network.py:220): dW1 += dh (x) [agg, x], db1 += dh
+    {
+      f32x16 ag[TH];
+      load_row_clayout<TH>(ag, a.agg + ic * H);
+      zero_if<TH>(ag, !valid);
+      swz_store_items(sA, j, dh);
+      swz_store_items(sB, j, ag);
+      wave_lds_sync();
+      s_db1 += swz_col_sums(sA);
+      __syncthreads();
+      swz_outer(acc_wa, bufA, 32 * tu, bufB, 32 * tv);
+      __syncthreads();
+    }
+    {
+      f32x16 xx[TH];
+      load_row_clayout<TH>(xx, a.x + ic * H);
+      zero_if<TH>(xx, !valid);
+      swz_store_items(sB, j, xx);
+      __syncthreads();
+      swz_outer(acc_wx, bufA, 32 * tu, bufB, 32 * tv);
+      __syncthreads();
+    }
+    // d agg = W1[:, :H]^T dh ; dx' = g + W1[:, H:]^T dh (residual graph_network.py:176)
+    f32x16 o[TH];
+    zero<TH>(o);
+    gw_matvec_t64(o, a.w1, 2 * H, dh);
+    if (valid) store_row_clayout<TH>(a.dagg + i * H, o);
+    load_row_clayout<TH>(o, a.g + ic * H);
+    gw_matvec_t64(o, a.w1 + H, 2 * H, dh);
+    if (valid) store_row_clayout<TH>(a.dxp + i * H, o);
+  }
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  store_tile_rowmajor(slab + (32 * tu) * H + 32 * tv, H, acc_wl);
+  store_tile_rowmajor(slab + H * H + (32 * tu) * 2 * H + 32 * tv, 2 * H, acc_wa);
+  store_tile_rowmajor(slab + H * H + H + (32 * tu) * 2 * H + 32 * tv, 2 * H, acc_wx);
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_NODE, H, 0, 2);
+  if (l < 16) {
+    st4(v + w * H + 4 * l, s_db1);
+    st4(v + kWaves * H + w * H + 4 * l, s_dbl);
+    st4(v + 2 * kWaves * H + w * H + 4 * l, s_dg);
+    st4(v + 3 * kWaves * H + w * H + 4 * l, s_db);
+  }
 }
 
 // ===========================================================================
@@ -1941,6 +2078,10 @@ extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* 
     if (nl == 3)
       run_wgrad<4, 4>(wg(p.d2_out, 0, H, saves->h, 0, H, slab, 3 * H * H, H, vb + 4 * W * H, ss, n, nullptr),
                       nslab, stream);
+    return check_launch("node_layer_bwd");
+  }
+  if (H == 64 && node_fn->nlin == 2) {  // two workgroups per CU
+    launch_bwd(k_node_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
     return check_launch("node_layer_bwd");
   }
   const size_t lds = bwd_lds(SGNN_SLAB_NODE, H, 0, node_fn->nlin);

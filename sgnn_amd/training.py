@@ -218,9 +218,9 @@ class SlabArena:
 
 def nslab_table(nslab: int) -> Dict[int, int]:
     node_ns = max(1, min(nslab, NODE_NSLAB))
-    # edge backward and the uv backward (H = 64: 80 KB kernels, two workgroups per CU) take the
-    # full count; the node-level kernels with larger LDS run one workgroup per CU
-    return {_hip.SLAB_EDGE: nslab, _hip.SLAB_ENC_EDGE: nslab, _hip.SLAB_NODE: node_ns,
+    # the edge, uv and node backward (H = 64: 80 KB kernels, two workgroups per CU) take the full
+    # count; the decoder / encoder-node backward with larger LDS run one workgroup per CU
+    return {_hip.SLAB_EDGE: nslab, _hip.SLAB_ENC_EDGE: nslab, _hip.SLAB_NODE: nslab,
             _hip.SLAB_UV: nslab, _hip.SLAB_DECODER: node_ns, _hip.SLAB_ENC_NODE: node_ns}
 
 
