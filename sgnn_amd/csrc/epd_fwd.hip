@@ -22,6 +22,7 @@
 #include "../../include/sgnn.h"
 #include "sgnn_internal.h"
 #include "fwd16.h"
+#include "radius_small.h"
 
 namespace {
 
@@ -621,13 +622,16 @@ static int check_train(bool train, const sgnn_mlp* m, const sgnn_saves* sv, cons
   return SGNN_OK;
 }
 
-extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int32_t dim,
-                                 const int64_t* types, const float* emb_w, int32_t emb_dim,
-                                 int32_t use_emb, const float* vel_mean, const float* vel_std,
-                                 float wall_max, float wall_div, const sgnn_mlp* enc,
-                                 const sgnn_mlp* edge0, float* x0, float* u, float* v,
-                                 const sgnn_saves* saves, void* stream) {
-  using namespace sgnn;
+namespace sgnn {
+
+// sgnn_encode_nodes; with fuse_radius, the small-graph radius search those
+// arguments describe is launched too (in the same launch as the inference
+// encoder when that takes the 16-node path, else just before it).
+int encode_nodes_impl(const float* pos_seq, int64_t n, int32_t T, int32_t dim, const int64_t* types,
+                      const float* emb_w, int32_t emb_dim, int32_t use_emb, const float* vel_mean,
+                      const float* vel_std, float wall_max, float wall_div, const sgnn_mlp* enc,
+                      const sgnn_mlp* edge0, float* x0, float* u, float* v, const sgnn_saves* saves,
+                      void* stream, const RadiusSmallArgs* fuse_radius) {
   if (n <= 0) return SGNN_OK;
   if (!pos_seq || !vel_mean || !vel_std || !x0 || !u || !v || T < 2 || dim < 1 || dim > 3)
     return set_error(SGNN_ERR_INVALID, "encode_nodes: bad arguments");
@@ -656,8 +660,10 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
     b.pos_seq = pos_seq; b.T = T; b.dim = dim; b.types = types; b.emb_w = emb_w; b.emb_dim = emb_dim;
     b.use_emb = use_emb; b.vel_mean = vel_mean; b.vel_std = vel_std; b.wall_max = wall_max;
     b.wall_div = wall_div; b.feat = feat; b.w1 = enc->w1; b.b1 = enc->b1;
+    if (fuse_radius) return sgnn::radius_enc16_launch(*fuse_radius, b, enc->nlin, static_cast<hipStream_t>(stream));
     return sgnn::enc_node16_launch(b, enc->nlin, static_cast<hipStream_t>(stream));
   }
+  if (fuse_radius && (st = radius_small_launch(*fuse_radius, static_cast<hipStream_t>(stream)))) return st;
   const unsigned grid = persistent_grid(n, 32 * kWaves, 2);
   const int tkf = (feat + 31) / 32;
   const size_t lds = sizeof(float) * (size_t)(H * (32 * tkf + 4) + (H == 64 ? 3 * H * (H + 4) : 0) + 6 * H);
@@ -672,6 +678,18 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
     else go_encode_nodes<2, 3, 3>(train, grid, lds, s, a);
   }
   return check_launch("encode_nodes");
+}
+
+}  // namespace sgnn
+
+extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int32_t dim,
+                                 const int64_t* types, const float* emb_w, int32_t emb_dim,
+                                 int32_t use_emb, const float* vel_mean, const float* vel_std,
+                                 float wall_max, float wall_div, const sgnn_mlp* enc,
+                                 const sgnn_mlp* edge0, float* x0, float* u, float* v,
+                                 const sgnn_saves* saves, void* stream) {
+  return sgnn::encode_nodes_impl(pos_seq, n, T, dim, types, emb_w, emb_dim, use_emb, vel_mean, vel_std, wall_max,
+                                 wall_div, enc, edge0, x0, u, v, saves, stream, nullptr);
 }
 
 extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t dim, float radius,

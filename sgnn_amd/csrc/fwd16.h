@@ -6,6 +6,8 @@
 
 namespace sgnn {
 
+struct RadiusSmallArgs;  // radius_small.h
+
 // One InteractionNetwork node update (graph_network.py:201-222) + residual
 // (:176), followed by the NEXT layer's edge-MLP node halves u, v (mode 0) or
 // the decoder + Euler integrator (mode 1, learned_simulator.py:381-411).
@@ -72,5 +74,8 @@ struct EncNode16Args {
   const float *w1, *b1;  // encoder first Linear [H][feat]
 };
 int enc_node16_launch(const EncNode16Args& a, int nl, hipStream_t stream);
+// The small-graph radius search and this encoder in one launch (they are
+// independent), followed by the radius graph's CSR launch.
+int radius_enc16_launch(const RadiusSmallArgs& r, const EncNode16Args& a, int nl, hipStream_t stream);
 
 }  // namespace sgnn

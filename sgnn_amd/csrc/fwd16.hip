@@ -23,6 +23,7 @@
 // blocks through LDS ([16 items][H + 4]) with one barrier.
 #include "common.h"
 #include "fwd16.h"
+#include "radius_small.h"
 #include "sgnn_internal.h"
 
 namespace {
@@ -560,50 +561,89 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) v
 // ---------------------------------------------------------------------------
 // Encoders (inference).
 
+// The encoder's weights of one wave's 16 output rows (resident for the launch).
 template <int NL, int KQF>
-__global__ __launch_bounds__(kBlock16) void k_enc_node16(sgnn::EncNode16Args a) {
-  __shared__ float xb[kBufs][16 * LDX];
-  const Node16Args& nd = a.nd;
-  const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
-  const int urow = 16 * b + j, ucol = 16 * b + 4 * g;
+struct EncNodeW {
   NodeW<NL, 0> W;
-  W.load_tail(nd, b, j, g);
   f32x4 w1f[KQF];  // first Linear [H][feat] (feat not a multiple of 4: scalar loads)
-#pragma unroll
-  for (int q = 0; q < KQF; ++q)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int f = 16 * q + 4 * g + c;
-      w1f[q][c] = f < a.feat ? a.w1[(int64_t)urow * a.feat + f] : 0.0f;
-    }
-  const f32x4 vb1 = ld4(a.b1 + ucol);
-  const int D = a.dim, nvel = (a.T - 1) * D;
-  for (int64_t tile = blockIdx.x; tile * 16 < nd.n; tile += gridDim.x) {
-    const int64_t i = tile * 16 + j;
-    const bool valid = i < nd.n;
-    const int64_t ic = valid ? i : nd.n - 1;
-    const float* p = a.pos_seq + ic * a.T * D;
-    f32x4 xf[KQF];
+  f32x4 vb1;
+  SGNN_DEV void load(const sgnn::EncNode16Args& a, int b, int j, int g) {
+    const int urow = 16 * b + j, ucol = 16 * b + 4 * g;
+    W.load_tail(a.nd, b, j, g);
 #pragma unroll
     for (int q = 0; q < KQF; ++q)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int f = 16 * q + 4 * g + c;
-        float val = 0.0f;
-        if (f < nvel) {  // learned_simulator.py:258,272-278 normalised velocity history
-          const int t = f / D, cc = f - t * D;
-          const float vel = __fsub_rn(p[(t + 1) * D + cc], p[t * D + cc]);
-          val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[cc]), a.vel_std[cc]);
-        } else if (f == nvel) {  // :282-284 wall distance
-          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(p[(a.T - 1) * D], 2.0f), 0.0f), a.wall_max), a.wall_div);
-        } else if (a.use_emb && f < nvel + 1 + a.emb_dim) {  // :287-290 type embedding
-          val = a.emb_w[a.types[ic] * a.emb_dim + (f - nvel - 1)];
-        }
-        xf[q][c] = val;
+        w1f[q][c] = f < a.feat ? a.w1[(int64_t)urow * a.feat + f] : 0.0f;
       }
-    const f32x4 h = relu4(mm(vb1, w1f, xf));
-    node_tail<NL, 0>(nd, W, xb, i, valid, h, zero4(), b, j, g);
+    vb1 = ld4(a.b1 + ucol);
   }
+};
+
+// Node features -> Encoder.node_fn -> x0, u, v of the 16 nodes of `tile`
+// (a tile past the end runs with every row invalid: the barriers of node_tail
+// stay matched across the waves that share `xb`).
+template <int NL, int KQF>
+SGNN_DEV void enc_node16_tile(const sgnn::EncNode16Args& a, const EncNodeW<NL, KQF>& E, float (*xb)[16 * LDX],
+                              int64_t tile, int b, int j, int g) {
+  const Node16Args& nd = a.nd;
+  const int D = a.dim, nvel = (a.T - 1) * D;
+  const int64_t i = tile * 16 + j;
+  const bool valid = i < nd.n;
+  const int64_t ic = valid ? i : nd.n - 1;
+  const float* p = a.pos_seq + ic * a.T * D;
+  f32x4 xf[KQF];
+#pragma unroll
+  for (int q = 0; q < KQF; ++q)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int f = 16 * q + 4 * g + c;
+      float val = 0.0f;
+      if (f < nvel) {  // learned_simulator.py:258,272-278 normalised velocity history
+        const int t = f / D, cc = f - t * D;
+        const float vel = __fsub_rn(p[(t + 1) * D + cc], p[t * D + cc]);
+        val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[cc]), a.vel_std[cc]);
+      } else if (f == nvel) {  // :282-284 wall distance
+        val = __fdiv_rn(fminf(fmaxf(__fadd_rn(p[(a.T - 1) * D], 2.0f), 0.0f), a.wall_max), a.wall_div);
+      } else if (a.use_emb && f < nvel + 1 + a.emb_dim) {  // :287-290 type embedding
+        val = a.emb_w[a.types[ic] * a.emb_dim + (f - nvel - 1)];
+      }
+      xf[q][c] = val;
+    }
+  const f32x4 h = relu4(mm(E.vb1, E.w1f, xf));
+  node_tail<NL, 0>(nd, E.W, xb, i, valid, h, zero4(), b, j, g);
+}
+
+template <int NL, int KQF>
+__global__ __launch_bounds__(kBlock16) void k_enc_node16(sgnn::EncNode16Args a) {
+  __shared__ float xb[kBufs][16 * LDX];
+  const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
+  EncNodeW<NL, KQF> E;
+  E.load(a, b, j, g);
+  for (int64_t tile = blockIdx.x; tile * 16 < a.nd.n; tile += gridDim.x) enc_node16_tile<NL, KQF>(a, E, xb, tile, b, j, g);
+}
+
+// The small-graph radius search (radius_small.h) and the node encoder in ONE
+// launch: the two are independent (the encoder reads only the position
+// window), and each alone is a few microseconds of latency on a fraction of
+// the chip.  Workgroups [0, rgrid) run the radius body; the others run the
+// encoder with two 16-node tiles per workgroup (waves 0-3 and 4-7, each half
+// with its own exchange buffers).
+template <int DIM, int NL, int KQF>
+__global__ __launch_bounds__(sgnn::kSmallBlock) void k_radius_enc16(sgnn::RadiusSmallArgs r, sgnn::EncNode16Args a,
+                                                                    int rgrid) {
+  extern __shared__ float lds[];
+  if ((int)blockIdx.x < rgrid) {
+    sgnn::radius_small_body<DIM>(r, lds, blockIdx.x, rgrid);
+    return;
+  }
+  const int l = lane_id(), j = l & 15, g = l >> 4, w = wave_id(), half = w >> 2, b = w & 3;
+  auto xb = reinterpret_cast<float (*)[16 * LDX]>(lds) + half * kBufs;
+  EncNodeW<NL, KQF> E;
+  E.load(a, b, j, g);
+  const int64_t pairs = gridDim.x - rgrid;
+  for (int64_t pr = blockIdx.x - rgrid; pr * 32 < a.nd.n; pr += pairs) enc_node16_tile<NL, KQF>(a, E, xb, 2 * pr + half, b, j, g);
 }
 
 }  // namespace
@@ -649,6 +689,42 @@ int enc_node16_launch(const EncNode16Args& a, int nl, hipStream_t s) {
   }
 #undef SGNN_ENC16
   return check_launch("encode_nodes16");
+}
+
+int radius_enc16_launch(const RadiusSmallArgs& r, const EncNode16Args& a, int nl, hipStream_t s) {
+  const int kqf = (a.feat + 15) / 16;
+  if (kqf > 3) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes16: more than 48 node features");
+  if (r.n != a.nd.n) return set_error(SGNN_ERR_INVALID, "radius_enc16: particle counts differ");
+  // one workgroup per CU: at ~186 VGPRs (the encoder's resident weights) a CU holds one 8-wave
+  // workgroup, so a grid past 256 would run a second round; the radius queries (cheap next to the
+  // position staging every workgroup pays) take the CUs the encoder's 32-node pairs leave
+  const int egrid = (int)std::min<int64_t>((a.nd.n + 31) / 32, 64);
+  const int rgrid = (int)std::max<int64_t>(1, std::min<int64_t>((r.n + 7) / 8, 256 - egrid));
+  const size_t lds = std::max(radius_small_lds(r.n, r.dim), sizeof(float) * 2 * kBufs * 16 * LDX);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)std::max(radius_small_lds(kSmallN, 3), sizeof(float) * 2 * kBufs * 16 * LDX));
+    hipLaunchKernelGGL(kern, dim3((unsigned)(rgrid + egrid)), dim3(kSmallBlock), lds, s, r, a, rgrid);
+  };
+#define SGNN_RE16(D_)                                                   \
+  do {                                                                  \
+    if (nl == 2) {                                                      \
+      if (kqf == 1) go(k_radius_enc16<D_, 2, 1>);                       \
+      else if (kqf == 2) go(k_radius_enc16<D_, 2, 2>);                  \
+      else go(k_radius_enc16<D_, 2, 3>);                                \
+    } else {                                                            \
+      if (kqf == 1) go(k_radius_enc16<D_, 3, 1>);                       \
+      else if (kqf == 2) go(k_radius_enc16<D_, 3, 2>);                  \
+      else go(k_radius_enc16<D_, 3, 3>);                                \
+    }                                                                   \
+  } while (0)
+  if (r.dim == 1) SGNN_RE16(1);
+  else if (r.dim == 2) SGNN_RE16(2);
+  else SGNN_RE16(3);
+#undef SGNN_RE16
+  int st = check_launch("radius_enc16");
+  if (st) return st;
+  return radius_small_csr(r, s);
 }
 
 }  // namespace sgnn

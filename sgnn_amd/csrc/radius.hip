@@ -23,6 +23,7 @@
 #include "common.h"
 #include "../../include/sgnn.h"
 #include "sgnn_internal.h"
+#include "radius_small.h"
 
 namespace {
 
@@ -420,73 +421,14 @@ __global__ __launch_bounds__(256) void k_compact(int64_t n, int cap, const int32
 
 // ---------------------------------------------------------------------------
 // Small-graph path (n <= kSmallN, e.g. the 2k-particle Taylor bar): two
-// launches instead of the cell pipeline's eleven.  Every workgroup stages the
-// whole position array in LDS (coalesced, SoA), and one wave per query walks
-// the candidates of the query's example IN ASCENDING INDEX, 64 per step,
-// straight out of LDS; it keeps the in-range ones in order and stops as soon
-// as it holds `cap` of them -- torch_cluster's CUDA rule (first K in ascending
-// index, strict <) needs no sort and no merge in this order.
-constexpr int kSmallN = 8192;
-constexpr int kSmallBlock = 512;  // 8 query waves per workgroup
+// launches instead of the cell pipeline's eleven (body in radius_small.h).
+using sgnn::kSmallBlock;
+using sgnn::kSmallN;
 
 template <int DIM>
-__global__ __launch_bounds__(kSmallBlock) void k_radius_small(
-    const float* pos, int64_t stride, int n, const int64_t* ex_ptr, int n_ex, float r2, int cap,
-    int loop, int32_t* nbr, int32_t* deg) {
+__global__ __launch_bounds__(kSmallBlock) void k_radius_small(sgnn::RadiusSmallArgs a) {
   extern __shared__ float lds[];
-  float* sp = lds;                       // [DIM][n] SoA
-  __shared__ int32_t kept[kSmallBlock / 64][32];
-  for (int t = threadIdx.x; t < n * DIM; t += blockDim.x) {
-    const int i = t / DIM, d = t - i * DIM;
-    sp[d * n + i] = pos[(int64_t)i * stride + d];
-  }
-  __syncthreads();
-  const int lane = lane_id(), w = wave_id();
-  int32_t* kw = kept[w];
-  for (int i = blockIdx.x * (kSmallBlock / 64) + w; i < n; i += gridDim.x * (kSmallBlock / 64)) {
-    int lo = 0, hi = n_ex - 1;  // example of i: largest b with ex_ptr[b] <= i
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (ex_ptr[mid] <= i) lo = mid; else hi = mid - 1;
-    }
-    const int jb = (int)ex_ptr[lo], je = (int)ex_ptr[lo + 1];
-    float pi[DIM];
-#pragma unroll
-    for (int d = 0; d < DIM; ++d) pi[d] = sp[d * n + i];
-    int cnt = 0;
-    for (int base = jb; base < je && cnt < cap; base += 64) {
-      const int j = base + lane;
-      bool in = false;
-      if (j < je) {
-        float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
-#pragma unroll
-        for (int d = 0; d < DIM; ++d) {
-          const float t = __fsub_rn(sp[d * n + j], pi[d]);
-          s = __fadd_rn(s, __fmul_rn(t, t));
-        }
-        in = s < r2;
-      }
-      const uint64_t bal = __ballot(in);
-      const int slot = cnt + (int)__popcll(bal & ((1ull << lane) - 1ull));
-      if (in && slot < cap) kw[slot] = j;
-      cnt += (int)__popcll(bal);
-    }
-    wave_lds_sync();
-    cnt = min(cnt, cap);
-    int top = lane < cnt ? kw[lane] : INT32_MAX;
-    if (!loop) {  // torch_cluster: K+1 first-by-index, then drop the self loop
-      const uint64_t self = __ballot(lane < cnt && top == i);
-      if (self) {
-        const int at = __ffsll((long long)self) - 1;
-        const int nxt = __shfl(top, (lane + 1) & 63, 64);
-        if (lane >= at) top = (lane + 1 < cnt) ? nxt : INT32_MAX;
-        cnt -= 1;
-      }
-    }
-    if (lane < cnt) nbr[(int64_t)i * cap + lane] = top;
-    if (lane == 0) deg[i] = cnt;
-    wave_lds_sync();
-  }
+  sgnn::radius_small_body<DIM>(a, lds, blockIdx.x, gridDim.x);
 }
 
 // deg -> rowptr (exclusive scan, rowptr[n] = E) and the padded lists ->
@@ -595,6 +537,44 @@ int scan_exclusive(const int32_t* in, int32_t* out, int64_t len, int32_t* partia
 
 }  // namespace sgnn
 
+namespace sgnn {
+
+int radius_small_csr(const RadiusSmallArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_csr_small, dim3((unsigned)((a.n + 31) / 32)), dim3(1024), 0, s, a.n, a.cap, a.nbr,
+                     a.deg, a.rowptr, a.send, a.recv);
+  return check_launch("radius_graph(small csr)");
+}
+
+int radius_small_launch(const RadiusSmallArgs& a, hipStream_t s) {
+  const unsigned grid = (unsigned)std::min<int64_t>((a.n + 7) / 8, 512);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)radius_small_lds(kSmallN, 3));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kSmallBlock), radius_small_lds(a.n, a.dim), s, a);
+  };
+  if (a.dim == 1) go(k_radius_small<1>);
+  else if (a.dim == 2) go(k_radius_small<2>);
+  else go(k_radius_small<3>);
+  return radius_small_csr(a, s);
+}
+
+// The small path's arguments (workspace layout included) when sgnn_radius_graph
+// would take it with these arguments; false otherwise (validation left to it).
+bool radius_small_plan(const float* pos, int64_t pos_stride, int64_t n, int32_t dim, const int64_t* ex_ptr,
+                       int32_t n_ex, float radius, int32_t K, int32_t loop, void* workspace, int32_t* rowptr,
+                       int32_t* send, int32_t* recv, int64_t edge_cap, RadiusSmallArgs* out) {
+  const int cap = K + (loop ? 0 : 1);
+  if (n < 1 || n > kSmallN || dim < 1 || dim > 3 || n_ex < 1 || K < 1 || !(radius > 0.0f) || cap > 32 ||
+      edge_cap < n * cap || !pos || !ex_ptr || !workspace || !rowptr || !send || !recv)
+    return false;
+  RadiusWs w = radius_layout(n, K, loop, workspace);
+  *out = RadiusSmallArgs{pos, pos_stride, (int)n, dim, ex_ptr, n_ex, radius * radius, cap, loop, w.nbr, w.deg,
+                         rowptr, send, recv};
+  return true;
+}
+
+}  // namespace sgnn
+
 extern "C" size_t sgnn_radius_workspace_bytes(int64_t n, int32_t K, int32_t loop) {
   return radius_layout(n, K, loop, nullptr).bytes;
 }
@@ -620,21 +600,9 @@ extern "C" int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n
   RadiusWs w = radius_layout(n, K, loop, workspace);
   const float r2 = radius * radius;
   if (n <= kSmallN) {  // small graphs: brute force over LDS in index order, two launches
-    const unsigned grid = (unsigned)std::min<int64_t>((n + 7) / 8, 512);
-    const size_t lds = sizeof(float) * (size_t)n * dim;
-    const int nn = (int)n;
-    auto go = [&](auto kern) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(float) * kSmallN * 3));
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(kSmallBlock), lds, stream, pos, pos_stride, nn, ex_ptr, n_ex,
-                         r2, cap, loop, w.nbr, w.deg);
-    };
-    if (dim == 1) go(k_radius_small<1>);
-    else if (dim == 2) go(k_radius_small<2>);
-    else go(k_radius_small<3>);
-    hipLaunchKernelGGL(k_csr_small, dim3((unsigned)((n + 31) / 32)), dim3(1024), 0, stream, nn, cap, w.nbr,
-                       w.deg, rowptr, send, recv);
-    return check_launch("radius_graph(small)");
+    const RadiusSmallArgs a{pos, pos_stride, (int)n, dim, ex_ptr, n_ex, r2, cap, loop, w.nbr, w.deg,
+                            rowptr, send, recv};
+    return radius_small_launch(a, stream);
   }
   if ((int64_t)n_ex > (int64_t)w.nbuckets)
     return set_error(SGNN_ERR_UNSUPPORTED, "radius_graph: more examples than cell capacity (2n)");

@@ -4,6 +4,7 @@
 // host is a hipLaunchKernel (~µs) instead of a Python ctypes round trip.
 #include "../../include/sgnn.h"
 #include "sgnn_internal.h"
+#include "radius_small.h"
 
 extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq,
                                       const sgnn_step_ws* ws, float* pred, float* next_pos,
@@ -13,14 +14,25 @@ extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in,
     return set_error(SGNN_ERR_INVALID, "predict_positions: bad arguments");
   const int64_t n = in->n;
   const int T = in->T, d = in->dim;
-  // radius graph on the most recent frame (learned_simulator.py:116-117)
-  int st = sgnn_radius_graph(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, n, d, in->ex_ptr, in->n_ex,
-                             in->radius, in->K, 1, ws->radius_ws, ws->rowptr, ws->send, ws->recv,
-                             ws->edge_cap, stream);
-  if (st) return st;
-  st = sgnn_encode_nodes(pos_seq, n, T, d, in->types, in->emb_w, in->emb_dim, in->use_emb, in->vel_mean,
-                         in->vel_std, in->wall_max, in->wall_div, m->enc_node, &m->edge[0], ws->x_a,
-                         ws->u, ws->v, nullptr, stream);
+  // radius graph on the most recent frame (learned_simulator.py:116-117); graphs of <= 2,560
+  // particles launch its search together with the node encoder (independent work, one launch whose
+  // grid fits the 256 CUs once: C1 0.1275 -> 0.1239 ms/step; measured slower at 4,800 / 8,000
+  // particles, 0.156 -> 0.167 / 0.217 -> 0.268, where the radius search needs more workgroups)
+  constexpr int64_t kMergeMaxN = 2560;
+  RadiusSmallArgs ra{};
+  const bool small = n <= kMergeMaxN && radius_small_plan(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, n, d, in->ex_ptr,
+                                       in->n_ex, in->radius, in->K, 1, ws->radius_ws, ws->rowptr, ws->send,
+                                       ws->recv, ws->edge_cap, &ra);
+  int st = SGNN_OK;
+  if (!small) {
+    st = sgnn_radius_graph(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, n, d, in->ex_ptr, in->n_ex,
+                           in->radius, in->K, 1, ws->radius_ws, ws->rowptr, ws->send, ws->recv,
+                           ws->edge_cap, stream);
+    if (st) return st;
+  }
+  st = encode_nodes_impl(pos_seq, n, T, d, in->types, in->emb_w, in->emb_dim, in->use_emb, in->vel_mean,
+                         in->vel_std, in->wall_max, in->wall_div, m->enc_node, &m->edge[0], ws->x_a, ws->u,
+                         ws->v, nullptr, stream, small ? &ra : nullptr);
   if (st) return st;
   const float* last = pos_seq + (int64_t)(T - 1) * d;
   float* x_in = ws->x_a;

@@ -11,6 +11,14 @@ namespace sgnn {
 
 int set_error(int status, const char* msg);
 int check_launch(const char* where);
+struct RadiusSmallArgs;  // radius_small.h
+// sgnn_encode_nodes, optionally with the small-graph radius search launched
+// alongside (epd_fwd.hip).
+int encode_nodes_impl(const float* pos_seq, int64_t n, int32_t T, int32_t dim, const int64_t* types,
+                      const float* emb_w, int32_t emb_dim, int32_t use_emb, const float* vel_mean,
+                      const float* vel_std, float wall_max, float wall_div, const sgnn_mlp* enc,
+                      const sgnn_mlp* edge0, float* x0, float* u, float* v, const sgnn_saves* saves,
+                      void* stream, const RadiusSmallArgs* fuse_radius);
 int scan_exclusive(const int32_t* in, int32_t* out, int64_t len, int32_t* partials,
                    hipStream_t stream);
 

@@ -1,7 +1,7 @@
 """Host orchestration of the HIP kernels: parameter packing, HBM workspaces,
 and the per-step launch sequence.  Everything here launches on the current
-torch stream through the C-ABI (no host synchronisation inside a step, so a
-step or a whole rollout can be captured in a HIP graph).
+torch stream through the C-ABI (no host synchronisation inside a step; a
+whole rollout is one sgnn_rollout call).
 
 Data layout in HBM (per graph of n particles, hidden H, cap K):
   rowptr[n+1], send[n*K], recv[n*K]   int32 receiver-sorted CSR (E = rowptr[n])
@@ -14,7 +14,6 @@ Data layout in HBM (per graph of n particles, hidden H, cap K):
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -270,7 +269,9 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
     """One LearnedSimulator.predict_positions (learned_simulator.py:413-438):
     radius graph -> encoder -> L interaction layers -> decoder -> Euler.
     Issued as ONE sgnn_predict_positions call (the launch sequence runs in C);
-    with `timers`, launched kernel by kernel so the edge layers can be timed."""
+    with `timers`, launched kernel by kernel so the edge layers can be timed
+    (one event pair per edge layer; small graphs: one pair around all L fused
+    layers)."""
     L = lib()
     pk = ParamPack.get(epd)
     if timers is None:
@@ -301,9 +302,11 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
     x_in, x_out = ws.x_a, ws.x_b
     if ws.u2 is not None:   # small graphs at hidden 64: one fused launch per layer
         uv_in, uv_out = (ws.u, ws.v), (ws.u2, ws.v2)
+        # one event pair around the L back-to-back fused launches (events between them would add
+        # their own cost to every launch); the caller divides by L
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
         for k in range(nl):
-            ev0 = torch.cuda.Event(enable_timing=True)
-            ev0.record()
             if k == 0 and enc_in_layer0:
                 check(L.sgnn_interaction_layer_encode(
                     pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius), ctypes.byref(pk.enc_edge),
@@ -329,9 +332,9 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
                     ctypes.byref(pk.node[k]), ctypes.byref(pk.dec), pos.data_ptr(), T, d, inp.acc_mean.data_ptr(),
                     inp.acc_std.data_ptr(), pred.data_ptr(), next_pos.data_ptr(), _ptr(window_out), s),
                     "sgnn_interaction_layer_decode")
-            ev1 = torch.cuda.Event(enable_timing=True)
-            ev1.record()
-            timers.append((ev0, ev1))
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        timers.append((ev0, ev1))
         return
     for k in range(nl):
         if timers is not None:
@@ -468,65 +471,3 @@ class DeviceRollout:
                                  self.out_pos.data_ptr(), self.out_pred.data_ptr(),
                                  stream_ptr(self.win[0].device)), "sgnn_rollout")
         return self.out_pos[:self.nsteps], self.out_pred[:self.nsteps, :, -1]
-
-
-class RolloutRunner:
-    """Autoregressive rollout on the device (evaluate.py:117-145 with the
-    window shift fused into the decoder kernel), optionally replayed from a
-    captured HIP graph: two steps (window A -> B -> A) per graph, each followed
-    by a copy of the step's prediction into the output slot selected by a
-    device-side counter, so one captured graph serves the whole rollout with
-    no host round trip and no per-kernel launch cost."""
-
-    def __init__(self, step_fn, window: torch.Tensor, n: int, dim: int, nsteps: int,
-                 use_graph: bool = True):
-        dev = window.device
-        self.step_fn, self.n, self.dim, self.nsteps = step_fn, n, dim, nsteps
-        self.win = [window.to(torch.float32).contiguous().clone(), torch.empty_like(window, dtype=torch.float32)]
-        self.pred = torch.empty(n, dim + 1, dtype=torch.float32, device=dev)
-        self.nxt = torch.empty(n, dim, dtype=torch.float32, device=dev)
-        self.out_pos = torch.empty(max(nsteps, 1), n, dim, dtype=torch.float32, device=dev)
-        self.out_strain = torch.empty(max(nsteps, 1), n, dtype=torch.float32, device=dev)
-        self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.graph = None
-        # HIP-graph replay is opt-in: at the 2k-particle / r = 15 shape a replay
-        # hit an illegal address that the eager loop does not (under study).
-        self.use_graph = use_graph and bool(os.environ.get("SGNN_ROLLOUT_GRAPH"))
-
-    def _one(self, k: int) -> None:
-        self.step_fn(self.win[k % 2], self.pred, self.nxt, self.win[(k + 1) % 2])
-        self.out_pos.index_copy_(0, self.counter, self.nxt[None])
-        self.out_strain.index_copy_(0, self.counter, self.pred[None, :, -1])
-        self.counter += 1
-
-    def _capture(self) -> None:
-        s = torch.cuda.Stream(device=self.win[0].device)
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):       # warm-up (workspaces, kernel attributes)
-            self._one(0)
-            self._one(1)
-        torch.cuda.current_stream().wait_stream(s)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self._one(0)
-            self._one(1)
-
-    def run(self, window: Optional[torch.Tensor] = None):
-        """Returns (positions [nsteps, n, dim], strain [nsteps, n]) on the device."""
-        if window is not None:
-            self.win[0].copy_(window)
-        if self.use_graph and self.nsteps >= 4:
-            if self.graph is None:
-                init = self.win[0].clone()
-                self._capture()          # its warm-up steps advance the window: restore it
-                self.win[0].copy_(init)
-            self.counter.zero_()
-            for _ in range(self.nsteps // 2):
-                self.graph.replay()
-            if self.nsteps % 2:
-                self._one(0)
-        else:
-            self.counter.zero_()
-            for k in range(self.nsteps):
-                self._one(k)
-        return self.out_pos[:self.nsteps], self.out_strain[:self.nsteps]

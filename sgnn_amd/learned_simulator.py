@@ -191,26 +191,15 @@ class LearnedSimulator(nn.Module):
                             self._connectivity_radius, inp, ws, pred, next_pos)
         return next_pos, pred[:, -1]
 
-    def rollout_runner(self, window: torch.Tensor, nparticles_per_example, particle_types, nsteps: int,
-                       use_graph: bool = False):
+    def rollout_runner(self, window: torch.Tensor, nparticles_per_example, particle_types, nsteps: int):
         """Device-resident autoregressive rollout of `nsteps` predict_positions
-        steps from `window` (evaluate.py:117-145): one sgnn_rollout call
-        (use_graph=True: the older Python-driven loop replayed from a HIP graph)."""
+        steps from `window` (evaluate.py:117-145): one sgnn_rollout call."""
         inp, use_emb = self._step_inputs(window, nparticles_per_example, particle_types)
         n, T, d = inp.pos_seq.shape
         ws = self._workspace(n, T, inp.pos_seq.device)
-        epd, emb_w, radius = self._encode_process_decode, self._particle_type_embedding.weight, \
-            self._connectivity_radius
-        if not use_graph:
-            pk = engine.ParamPack.get(epd)
-            sin = engine.step_in(inp, ws, radius, emb_w, use_emb)
-            return engine.DeviceRollout(pk.epd, sin, ws, inp.pos_seq, n, d, nsteps, keep=(pk, inp))
-
-        def step(win_in, pred, nxt, win_out):
-            inp.pos_seq = win_in
-            engine.forward_step(epd, emb_w, use_emb, radius, inp, ws, pred, nxt, window_out=win_out)
-
-        return engine.RolloutRunner(step, inp.pos_seq, n, d, nsteps, use_graph)
+        pk = engine.ParamPack.get(self._encode_process_decode)
+        sin = engine.step_in(inp, ws, self._connectivity_radius, self._particle_type_embedding.weight, use_emb)
+        return engine.DeviceRollout(pk.epd, sin, ws, inp.pos_seq, n, d, nsteps, keep=(pk, inp))
 
     def predict_accelerations(self, next_positions: torch.Tensor, position_sequence_noise: torch.Tensor,
                               position_sequence: torch.Tensor, nparticles_per_example,

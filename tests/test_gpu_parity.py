@@ -183,7 +183,7 @@ def test_device_rollout_runner(nsteps):
     sim = product_sim(z)
     types_ = torch.zeros(n, dtype=torch.long, device="cuda")
     win = torch.from_numpy(seq[:, :T]).cuda()
-    pos, strain = sim.rollout_runner(win, [n], types_, nsteps, use_graph=False).run()
+    pos, strain = sim.rollout_runner(win, [n], types_, nsteps).run()
     torch.cuda.synchronize()
     osim = oracle_sim(z)
     ref_pos, ref_str = O.rollout(osim, torch.from_numpy(seq), torch.zeros(n, dtype=torch.long), n, nsteps, T)
