@@ -631,7 +631,8 @@ int encode_nodes_impl(const float* pos_seq, int64_t n, int32_t T, int32_t dim, c
                       const float* emb_w, int32_t emb_dim, int32_t use_emb, const float* vel_mean,
                       const float* vel_std, float wall_max, float wall_div, const sgnn_mlp* enc,
                       const sgnn_mlp* edge0, float* x0, float* u, float* v, const sgnn_saves* saves,
-                      void* stream, const RadiusSmallArgs* fuse_radius) {
+                      void* stream, const RadiusSmallArgs* fuse_radius, bool defer_csr, bool* csr_pending) {
+  if (csr_pending) *csr_pending = false;
   if (n <= 0) return SGNN_OK;
   if (!pos_seq || !vel_mean || !vel_std || !x0 || !u || !v || T < 2 || dim < 1 || dim > 3)
     return set_error(SGNN_ERR_INVALID, "encode_nodes: bad arguments");
@@ -660,7 +661,12 @@ int encode_nodes_impl(const float* pos_seq, int64_t n, int32_t T, int32_t dim, c
     b.pos_seq = pos_seq; b.T = T; b.dim = dim; b.types = types; b.emb_w = emb_w; b.emb_dim = emb_dim;
     b.use_emb = use_emb; b.vel_mean = vel_mean; b.vel_std = vel_std; b.wall_max = wall_max;
     b.wall_div = wall_div; b.feat = feat; b.w1 = enc->w1; b.b1 = enc->b1;
-    if (fuse_radius) return sgnn::radius_enc16_launch(*fuse_radius, b, enc->nlin, static_cast<hipStream_t>(stream));
+    if (fuse_radius) {
+      const bool defer = defer_csr && csr_pending;
+      st = sgnn::radius_enc16_launch(*fuse_radius, b, enc->nlin, static_cast<hipStream_t>(stream), !defer);
+      if (!st && defer) *csr_pending = true;
+      return st;
+    }
     return sgnn::enc_node16_launch(b, enc->nlin, static_cast<hipStream_t>(stream));
   }
   if (fuse_radius && (st = radius_small_launch(*fuse_radius, static_cast<hipStream_t>(stream)))) return st;
@@ -689,7 +695,7 @@ extern "C" int sgnn_encode_nodes(const float* pos_seq, int64_t n, int32_t T, int
                                  const sgnn_mlp* edge0, float* x0, float* u, float* v,
                                  const sgnn_saves* saves, void* stream) {
   return sgnn::encode_nodes_impl(pos_seq, n, T, dim, types, emb_w, emb_dim, use_emb, vel_mean, vel_std, wall_max,
-                                 wall_div, enc, edge0, x0, u, v, saves, stream, nullptr);
+                                 wall_div, enc, edge0, x0, u, v, saves, stream, nullptr, false, nullptr);
 }
 
 extern "C" int sgnn_encode_edges(const float* pos, int64_t pos_stride, int32_t dim, float radius,
@@ -960,15 +966,17 @@ extern "C" int sgnn_interaction_layer_decode(const float* x_in, const float* u_i
   return layer_common(L, edge_fn, node_fn, 1, decoder->nlin, stream);
 }
 
-extern "C" int sgnn_interaction_layer_encode(const float* pos, int64_t pos_stride, int32_t dim, float radius,
-                                             const sgnn_mlp* enc_edge, float* e0t, const float* x_in,
-                                             const float* u_in, const float* v_in, const int32_t* rowptr,
-                                             const int32_t* send, const int32_t* recv, int64_t n,
-                                             const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
-                                             const sgnn_mlp* next_edge, float* x_out, float* u_out,
-                                             float* v_out, void* stream) {
-  using namespace sgnn;
+namespace sgnn {
+
+int interaction_layer_encode_impl(const float* pos, int64_t pos_stride, int32_t dim, float radius,
+                                  const sgnn_mlp* enc_edge, float* e0t, const float* x_in, const float* u_in,
+                                  const float* v_in, const int32_t* rowptr, const int32_t* send,
+                                  const int32_t* recv, int64_t n, const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
+                                  const sgnn_mlp* next_edge, float* x_out, float* u_out, float* v_out, void* stream,
+                                  const RadiusSmallArgs* lists) {
   if (n <= 0) return SGNN_OK;
+  if (lists && (lists->n != n || lists->rowptr != rowptr || lists->send != send || lists->recv != recv))
+    return set_error(SGNN_ERR_INVALID, "interaction_layer_encode: lists describe another graph");
   if (!pos || dim < 1 || dim > 3 || !(radius > 0.0f) || !e0t || !x_in || !u_in || !v_in || !rowptr || !send ||
       !recv || !x_out || !u_out || !v_out || !next_edge || u_out == u_in || v_out == v_in)
     return set_error(SGNN_ERR_INVALID, "interaction_layer_encode: bad arguments");
@@ -985,5 +993,23 @@ extern "C" int sgnn_interaction_layer_encode(const float* pos, int64_t pos_strid
   L.pos = pos; L.pos_stride = pos_stride; L.dim = dim; L.radius = radius;
   L.xw1 = enc_edge->w1; L.xb1 = enc_edge->b1; L.xw2 = enc_edge->w2; L.xb2 = enc_edge->b2;
   L.xg = enc_edge->ln_g; L.xbb = enc_edge->ln_b; L.e0t_out = e0t;
+  if (lists) {
+    L.l_deg = lists->deg; L.l_nbr = lists->nbr; L.l_cap = lists->cap;
+    L.rowptr_out = lists->rowptr; L.send_out = lists->send; L.recv_out = lists->recv;
+  }
   return layer_common(L, edge_fn, node_fn, 0, 0, stream, true);
+}
+
+}  // namespace sgnn
+
+extern "C" int sgnn_interaction_layer_encode(const float* pos, int64_t pos_stride, int32_t dim, float radius,
+                                             const sgnn_mlp* enc_edge, float* e0t, const float* x_in,
+                                             const float* u_in, const float* v_in, const int32_t* rowptr,
+                                             const int32_t* send, const int32_t* recv, int64_t n,
+                                             const sgnn_mlp* edge_fn, const sgnn_mlp* node_fn,
+                                             const sgnn_mlp* next_edge, float* x_out, float* u_out,
+                                             float* v_out, void* stream) {
+  return sgnn::interaction_layer_encode_impl(pos, pos_stride, dim, radius, enc_edge, e0t, x_in, u_in, v_in, rowptr,
+                                             send, recv, n, edge_fn, node_fn, next_edge, x_out, u_out, v_out,
+                                             stream, nullptr);
 }

@@ -54,6 +54,13 @@ struct Layer16Args {
   float radius;
   const float *xw1, *xb1, *xw2, *xb2, *xg, *xbb;
   float* e0t_out;
+  // first layer, optional: the radius search's padded lists (l_deg [n], l_nbr
+  // [n][l_cap]) instead of the CSR -- every workgroup builds its tile's CSR
+  // rows in LDS and writes them (rowptr / send / recv above) for the later
+  // layers; needs one tile per workgroup (tiles <= 512)
+  const int32_t *l_deg, *l_nbr;
+  int l_cap;
+  int32_t *rowptr_out, *send_out, *recv_out;
 };
 
 int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t stream, bool first = false);
@@ -76,6 +83,7 @@ struct EncNode16Args {
 int enc_node16_launch(const EncNode16Args& a, int nl, hipStream_t stream);
 // The small-graph radius search and this encoder in one launch (they are
 // independent), followed by the radius graph's CSR launch.
-int radius_enc16_launch(const RadiusSmallArgs& r, const EncNode16Args& a, int nl, hipStream_t stream);
+int radius_enc16_launch(const RadiusSmallArgs& r, const EncNode16Args& a, int nl, hipStream_t stream,
+                        bool csr = true);
 
 }  // namespace sgnn

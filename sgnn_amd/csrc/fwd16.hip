@@ -369,6 +369,8 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) v
   __shared__ float scratch[NB * 16 * LDX];  // per-wave receiver sums; = xb in the node phase
   __shared__ float sxw[FIRST ? H * LDX : 4];      // encoder W2 (FIRST)
   __shared__ float sxv[FIRST ? 4 : 1][H];         // encoder b1, b2, gamma, beta (FIRST)
+  __shared__ int32_t lsend[FIRST ? 16 * 32 : 1], lrecv[FIRST ? 16 * 32 : 1];  // lists mode: the tile's CSR
+  __shared__ int32_t lpre[FIRST ? 17 : 1], lred[FIRST ? kWaves16 : 1];
   static_assert(NB >= kWaves16, "the per-wave sums fit the node buffers");
   float* sums_all = scratch;
   auto xb = reinterpret_cast<float (*)[16 * LDX]>(scratch);
@@ -382,11 +384,17 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) v
   int r_n = 0, s_n = 0;
   f32x4 x_n[KQ], uv_n[KQ];
   float ps_n[3] = {0.0f, 0.0f, 0.0f}, pr_n[3] = {0.0f, 0.0f, 0.0f};
+  const bool lists = FIRST && a.l_deg != nullptr;
   auto load_half = [&](int32_t hs) {  // indices, e0 row (FIRST: both positions), u[recv] + v[send]
     const int32_t e = hs + j;
     const int32_t ec = e < eb ? e : eb - 1;
-    r_n = a.recv[ec];
-    s_n = a.send[ec];
+    if (FIRST && lists) {
+      r_n = lrecv[ec - ea];
+      s_n = lsend[ec - ea];
+    } else {
+      r_n = a.recv[ec];
+      s_n = a.send[ec];
+    }
     if constexpr (FIRST) {
 #pragma unroll
       for (int c = 0; c < 3; ++c)
@@ -402,10 +410,58 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(2))) v
     for (int t = 0; t < KQ; ++t)
       uv_n[t] = ld4(a.u_in + (int64_t)r_n * H + 16 * t + 4 * g) + ld4(a.v_in + (int64_t)s_n * H + 16 * t + 4 * g);
   };
+  // lists mode (FIRST, one tile per workgroup): the tile's CSR rows from the
+  // radius search's padded lists -- row start = sum of deg over the earlier
+  // rows (a workgroup reduction), the rows compacted into LDS and written out
+  auto build_tile_csr = [&](int64_t i0) {
+    const int cnt = (int)min<int64_t>(NT, nd.n - i0);
+    int part = 0;
+    for (int64_t k = threadIdx.x; k < i0; k += kBlock16) part += a.l_deg[k];
+    const int dg = b == 0 && l < cnt ? a.l_deg[i0 + l] : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (l == 0) lred[b] = part;
+    __syncthreads();
+    if (b == 0) {
+      int base = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves16; ++w) base += lred[w];
+      int incl = dg;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (l >= o) incl += t;
+      }
+      if (l < 16) lpre[l + 1] = base + incl;
+      if (l == 0) lpre[0] = base;
+    }
+    __syncthreads();
+    const int base = lpre[0];
+    for (int t = threadIdx.x; t < cnt * a.l_cap; t += kBlock16) {
+      const int k = t / a.l_cap, q = t - k * a.l_cap;
+      const int r0 = lpre[k];
+      if (q < lpre[k + 1] - r0) {
+        const int32_t sv = a.l_nbr[(i0 + k) * a.l_cap + q];
+        lsend[r0 - base + q] = sv;
+        lrecv[r0 - base + q] = (int32_t)(i0 + k);
+        a.send_out[r0 + q] = sv;
+        a.recv_out[r0 + q] = (int32_t)(i0 + k);
+      }
+    }
+    if (threadIdx.x < cnt) a.rowptr_out[i0 + threadIdx.x] = lpre[threadIdx.x];
+    if (threadIdx.x == 0 && i0 + cnt == nd.n) a.rowptr_out[nd.n] = lpre[cnt];
+    __syncthreads();
+    ea = base;
+    eb = lpre[cnt];
+  };
   auto start_tile = [&](int64_t tl) {
     const int64_t i0 = tl * NT;
-    ea = nd.rowptr[i0];
-    eb = nd.rowptr[min<int64_t>(i0 + NT, nd.n)];
+    if (FIRST && lists) {
+      build_tile_csr(i0);
+    } else {
+      ea = nd.rowptr[i0];
+      eb = nd.rowptr[min<int64_t>(i0 + NT, nd.n)];
+    }
     if (ea + 16 * b < eb) load_half(ea + 16 * b);
   };
   f32x4 st0[kStagePer], st1[kStagePer], st2[kStagePer];
@@ -668,6 +724,10 @@ int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t s, bool f
     return set_error(SGNN_ERR_UNSUPPORTED, "layer16: the fused edge encoder needs nmlp_layers 1 and a later layer");
   const int64_t tiles = (a.nd.n + a.nt - 1) / a.nt;
   const unsigned grid = (unsigned)std::min<int64_t>(tiles, 512);
+  if (a.l_deg && (!first || tiles > 512 || a.l_cap < 1 || a.l_cap > 32 || !a.l_nbr || !a.rowptr_out ||
+                  !a.send_out || !a.recv_out))
+    return set_error(SGNN_ERR_INVALID, "layer16: CSR from the padded lists needs the first layer, <= 512 tiles, "
+                                       "cap <= 32");
   if (first) hipLaunchKernelGGL((k_layer16<2, 0, true>), dim3(grid), dim3(kBlock16), 0, s, a);
   else if (mode == 0 && nl == 2) hipLaunchKernelGGL((k_layer16<2, 0, false>), dim3(grid), dim3(kBlock16), 0, s, a);
   else if (mode == 0) hipLaunchKernelGGL((k_layer16<3, 0, false>), dim3(grid), dim3(kBlock16), 0, s, a);
@@ -691,7 +751,7 @@ int enc_node16_launch(const EncNode16Args& a, int nl, hipStream_t s) {
   return check_launch("encode_nodes16");
 }
 
-int radius_enc16_launch(const RadiusSmallArgs& r, const EncNode16Args& a, int nl, hipStream_t s) {
+int radius_enc16_launch(const RadiusSmallArgs& r, const EncNode16Args& a, int nl, hipStream_t s, bool csr) {
   const int kqf = (a.feat + 15) / 16;
   if (kqf > 3) return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes16: more than 48 node features");
   if (r.n != a.nd.n) return set_error(SGNN_ERR_INVALID, "radius_enc16: particle counts differ");
@@ -723,7 +783,7 @@ int radius_enc16_launch(const RadiusSmallArgs& r, const EncNode16Args& a, int nl
   else SGNN_RE16(3);
 #undef SGNN_RE16
   int st = check_launch("radius_enc16");
-  if (st) return st;
+  if (st || !csr) return st;
   return radius_small_csr(r, s);
 }
 

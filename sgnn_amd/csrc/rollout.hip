@@ -23,6 +23,12 @@ extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in,
   const bool small = n <= kMergeMaxN && radius_small_plan(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, n, d, in->ex_ptr,
                                        in->n_ex, in->radius, in->K, 1, ws->radius_ws, ws->rowptr, ws->send,
                                        ws->recv, ws->edge_cap, &ra);
+  // small graphs at hidden 64: one fused launch per layer (u/v ping-pong), the first one with the
+  // edge encoder folded in (nmlp_layers 1) -- and, after the merged radius + encoder launch, with the
+  // CSR built from the radius search's padded lists (no separate compaction launch)
+  const bool fused = ws->u2 && ws->v2 && m->node[0].hidden == 64 && n <= 8192;
+  const bool enc_in_layer0 = fused && m->nlayers > 1 && m->enc_edge->nlin == 2 && m->node[0].nlin == 2;
+  bool csr_pending = false;
   int st = SGNN_OK;
   if (!small) {
     st = sgnn_radius_graph(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, n, d, in->ex_ptr, in->n_ex,
@@ -32,17 +38,14 @@ extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in,
   }
   st = encode_nodes_impl(pos_seq, n, T, d, in->types, in->emb_w, in->emb_dim, in->use_emb, in->vel_mean,
                          in->vel_std, in->wall_max, in->wall_div, m->enc_node, &m->edge[0], ws->x_a, ws->u,
-                         ws->v, nullptr, stream, small ? &ra : nullptr);
+                         ws->v, nullptr, stream, small ? &ra : nullptr, small && enc_in_layer0, &csr_pending);
   if (st) return st;
   const float* last = pos_seq + (int64_t)(T - 1) * d;
   float* x_in = ws->x_a;
   float* x_out = ws->x_b;
   float scale = 1.0f;
-  // small graphs (n <= 8192, hidden 64): one fused launch per layer (u/v ping-pong), the first one
-  // with the edge encoder folded in (nmlp_layers 1); larger graphs keep the edge / node kernel pair
-  // (more workgroups, no per-workgroup weight staging per node tile)
-  const bool fused = ws->u2 && ws->v2 && m->node[0].hidden == 64 && n <= 8192;
-  const bool enc_in_layer0 = fused && m->nlayers > 1 && m->enc_edge->nlin == 2 && m->node[0].nlin == 2;
+  // larger graphs keep the edge / node kernel pair (more workgroups, no per-workgroup weight staging
+  // per node tile)
   if (!enc_in_layer0) {
     st = sgnn_encode_edges(last, (int64_t)T * d, d, in->radius, ws->rowptr, ws->send, ws->recv, n,
                            ws->edge_cap, m->enc_edge, ws->e0t, nullptr, stream);
@@ -52,9 +55,9 @@ extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in,
     float *u_in = ws->u, *v_in = ws->v, *u_out = ws->u2, *v_out = ws->v2;
     for (int k = 0; k < m->nlayers; ++k, scale *= 2.0f) {
       if (k == 0 && enc_in_layer0) {
-        st = sgnn_interaction_layer_encode(last, (int64_t)T * d, d, in->radius, m->enc_edge, ws->e0t, x_in, u_in,
+        st = interaction_layer_encode_impl(last, (int64_t)T * d, d, in->radius, m->enc_edge, ws->e0t, x_in, u_in,
                                            v_in, ws->rowptr, ws->send, ws->recv, n, &m->edge[0], &m->node[0],
-                                           &m->edge[1], x_out, u_out, v_out, stream);
+                                           &m->edge[1], x_out, u_out, v_out, stream, csr_pending ? &ra : nullptr);
         std::swap(x_in, x_out);
         std::swap(u_in, u_out);
         std::swap(v_in, v_out);
