@@ -1826,13 +1826,16 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_items(EncEdgeItemsArgs p) {
 
 // ===========================================================================
 // Slab reduction: out[r][c] = scale * sum_g sum_q slab_g[off + q*rep + r*ld + c].
-// Block = 32 consecutive output elements x 8 slab groups; thread q sums slabs
-// g = q, q+8, ... with 4 independent accumulators (coalesced 128-B rows per
-// slab), then the 8 partials are added in a fixed order through LDS:
-// deterministic.
+// Block = 32 consecutive output elements (the C-ABI's block_start unit).
+// Descriptors whose rows are 16-B aligned (ncols, ld, offsets, strides all
+// multiples of 4): 8 lanes x float4 cover the 32 elements and the 256 threads
+// are 32 slab groups, each summing slabs g = q, q+32, ... with 4 independent
+// float4 accumulators (16-B loads: 4x the bytes per load instruction of the
+// scalar form).  Otherwise 32 lanes x 1 float and 8 slab groups.  The group
+// partials are added in a fixed order through LDS: deterministic.
 __global__ __launch_bounds__(256) void k_reduce_slabs(const sgnn_reduce_desc* descs,
                                                       const int32_t* block_start, int ndesc) {
-  __shared__ float part[8][33];
+  __shared__ float part[32][33];
   int lo = 0, hi = ndesc - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -1840,30 +1843,58 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const sgnn_reduce_desc* de
   }
   const sgnn_reduce_desc d = descs[lo];
   const int64_t total = (int64_t)d.nrows * d.ncols;
-  const int e = threadIdx.x & 31, q = threadIdx.x >> 5;
-  const int64_t idx = (int64_t)(blockIdx.x - block_start[lo]) * 32 + e;
-  // eight independent chains per thread: with 512 slabs per kind the loads in
-  // flight, not the bytes, set the rate
-  float s[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  if (idx < total) {
-    const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
-    const float* base = d.src + d.offset + (int64_t)r * d.src_ld + cc;
-    for (int k = 0; k < d.nrep; ++k) {
-      const float* p = base + (int64_t)k * d.rep_stride;
-      int g = q;
-      for (; g + 56 < d.nslab; g += 64) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s[u] += p[(int64_t)(g + 8 * u) * d.slab_stride];
+  const int64_t blk0 = (int64_t)(blockIdx.x - block_start[lo]) * 32;
+  const bool vec = ((d.ncols | d.src_ld | d.offset | d.slab_stride | d.rep_stride) & 3) == 0 &&
+                   (reinterpret_cast<uintptr_t>(d.src) & 15) == 0;
+  int ngroups;
+  if (vec) {
+    ngroups = 32;
+    const int e4 = threadIdx.x & 7, q = threadIdx.x >> 3;
+    const int64_t idx = blk0 + 4 * e4;  // ncols % 4 == 0: a float4 never straddles a row or the end
+    f32x4 s0 = {0.0f, 0.0f, 0.0f, 0.0f}, s1 = s0, s2 = s0, s3 = s0;
+    if (idx < total) {
+      const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
+      const float* base = d.src + d.offset + (int64_t)r * d.src_ld + cc;
+      for (int k = 0; k < d.nrep; ++k) {
+        const float* p = base + (int64_t)k * d.rep_stride;
+        int g = q;
+        for (; g + 96 < d.nslab; g += 128) {
+          s0 += ld4(p + (int64_t)g * d.slab_stride);
+          s1 += ld4(p + (int64_t)(g + 32) * d.slab_stride);
+          s2 += ld4(p + (int64_t)(g + 64) * d.slab_stride);
+          s3 += ld4(p + (int64_t)(g + 96) * d.slab_stride);
+        }
+        for (; g < d.nslab; g += 32) s0 += ld4(p + (int64_t)g * d.slab_stride);
       }
-      for (; g < d.nslab; g += 8) s[0] += p[(int64_t)g * d.slab_stride];
     }
-  }
-  part[q][e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-  __syncthreads();
-  if (q == 0 && idx < total) {
-    float t = 0.0f;
+    const f32x4 t = (s0 + s1) + (s2 + s3);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t += part[k][e];
+    for (int c = 0; c < 4; ++c) part[q][4 * e4 + c] = t[c];
+  } else {
+    ngroups = 8;
+    const int e = threadIdx.x & 31, q = threadIdx.x >> 5;
+    const int64_t idx = blk0 + e;
+    float s[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (idx < total) {
+      const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
+      const float* base = d.src + d.offset + (int64_t)r * d.src_ld + cc;
+      for (int k = 0; k < d.nrep; ++k) {
+        const float* p = base + (int64_t)k * d.rep_stride;
+        int g = q;
+        for (; g + 56 < d.nslab; g += 64) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s[u] += p[(int64_t)(g + 8 * u) * d.slab_stride];
+        }
+        for (; g < d.nslab; g += 8) s[0] += p[(int64_t)g * d.slab_stride];
+      }
+    }
+    part[q][e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  }
+  __syncthreads();
+  const int64_t idx = blk0 + threadIdx.x;
+  if (threadIdx.x < 32 && idx < total) {
+    float t = 0.0f;
+    for (int k = 0; k < ngroups; ++k) t += part[k][threadIdx.x];
     const int r = (int)(idx / d.ncols), cc = (int)(idx - (int64_t)r * d.ncols);
     float* o = d.dst + (int64_t)r * d.dst_ld + cc;
     *o = d.accumulate ? *o + t * d.scale : t * d.scale;
