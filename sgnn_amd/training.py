@@ -414,19 +414,21 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
                               ws.v.data_ptr(), ctypes.byref(sv), side.cuda_stream), "sgnn_encode_nodes")
     ev["encn"].record(side)
     engine.radius_graph(ws, pos, (T - 1) * d, T * d, inp.ex_ptr, inp.n_ex, radius)
-    # sender-sorted transpose of the new graph (for dV) on the side stream,
-    # overlapping the forward layers; train_backward waits for it
     ev["graph"].record(main)
-    side.wait_event(ev["graph"])
-    check(L.sgnn_transpose_csr(ws.rowptr.data_ptr(), ws.send.data_ptr(), n, ws.edge_cap,
-                               tw.tws_ptr(), tw.tptr.data_ptr(), tw.tperm.data_ptr(), side.cuda_stream),
-          "sgnn_transpose_csr")
-    ev["tcsr"].record(side)
+    # the edge encoder is queued on the launch stream before the side-stream
+    # work below, so the GPU has it in hand while the host issues the rest
     sv = _saves(yhat=tw.ee_yh, rstd=tw.ee_rstd, h2=tw.ee_h2)
     check(L.sgnn_encode_edges(pos.data_ptr() + 4 * (T - 1) * d, T * d, d, float(radius),
                               ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
                               ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(),
                               ctypes.byref(sv), s), "sgnn_encode_edges")
+    # sender-sorted transpose of the new graph (for dV) on the side stream,
+    # overlapping the forward layers; train_backward waits for it
+    side.wait_event(ev["graph"])
+    check(L.sgnn_transpose_csr(ws.rowptr.data_ptr(), ws.send.data_ptr(), n, ws.edge_cap,
+                               tw.tws_ptr(), tw.tptr.data_ptr(), tw.tperm.data_ptr(), side.cuda_stream),
+          "sgnn_transpose_csr")
+    ev["tcsr"].record(side)
     nl = len(pk.edge)
     main.wait_event(ev["encn"])          # x0, u, v of layer 0
     for k in range(nl):
