@@ -1409,6 +1409,164 @@ __global__ __launch_bounds__(kBlock) void k_enc_edge_bwd(EncEdgeBwdArgs a) {
   if (NL == 3) store_lane_vec<TH>(v + 4 * kWaves * H, s_dbm);
 }
 
+// Encoder edge MLP backward at H = 64, NL = 2 (the single-scale training
+// configuration), sized like k_edge_bwd64 for TWO workgroups per CU: Wl^T
+// swizzled in LDS (16 KB) + two unpadded swizzled [128 items][64] images
+// (64 KB) = 80 KB, W1 / b1 / gamma read from L2, <= 256 VGPRs.  Per 128-edge
+// chunk: LayerNorm backward from dE0, dWl = sum dy (x) h1 (one 32x32 tile per
+// wave), dh = (Wl^T dy) * [h1 > 0], then dW1 = sum dh (x) f over the edge
+// features f (dim + 1 <= 4 of a 32-column tile; the two 32-unit tiles are
+// split over the waves by item halves and summed once at the end) and
+// db1 = sum dh.  h1 is recomputed from the positions as the forward did.
+SGNN_DEV void swz_store_feat(float* img, int item, f32x4 f) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {  // half h writes column groups 4 (2q + h) .. +3 of columns 0..31
+    const int g = 2 * q + h;
+    st4(img + swz(item, 4 * g), g == 0 ? f : f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+  }
+}
+
+// swz_outer over the item steps [s0, s0 + 32) (items 2 s0 .. 2 s0 + 63).
+SGNN_DEV void swz_outer_half(f32x16& acc, const float* A, int ua, const float* B, int vb, int s0) {
+  constexpr int G = 4, NS = kChunk / 4;
+  const int l = (lane_id() & 31) + opaque_zero(), h = lane_id() >> 5;
+  const int ca = h * 64 + ((ua + l) ^ (4 * h)), cb = h * 64 + ((vb + l) ^ (4 * h));
+  auto ra = [&](int s) { return A[(ca ^ (8 * (s & 7))) + 128 * s]; };
+  auto rb = [&](int s) { return B[(cb ^ (8 * (s & 7))) + 128 * s]; };
+#pragma unroll
+  for (int s = 0; s < NS; s += G) {
+    float a[G], b[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      a[i] = ra(s0 + s + i);
+      b[i] = rb(s0 + s + i);
+    }
+#pragma unroll
+    for (int i = 0; i < G; ++i) acc = mfma32(a[i], b[i], acc);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+void k_enc_edge_bwd64(EncEdgeBwdArgs a) {
+  constexpr int TH = 2, H = 64;
+  extern __shared__ float lds[];
+  float* wt = lds;                  // Wl^T [u][k]
+  float* bufA = wt + H * H;         // [128 items][64]
+  float* bufB = bufA + kChunk * H;
+  swz_stage_wt(wt, a.wl, H, 1.0f);
+  __syncthreads();
+  const int w = wave_id(), l = lane_id(), j = l & 31, h = l >> 5;
+  float* sA = bufA + w * 32 * H;
+  float* sB = bufB + w * 32 * H;
+  const int tu = w >> 1, tv = w & 1;   // the wave's dWl tile
+  const int t1 = w & 1, ih = w >> 1;   // its dW1 tile (units 32 t1 ..) and item half
+  const int nf = a.dim + 1;
+  f32x16 acc, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc[r] = 0.0f;
+    acc1[r] = 0.0f;
+  }
+  f32x4 s_dbl = {0.0f, 0.0f, 0.0f, 0.0f}, s_dg = s_dbl, s_db = s_dbl, s_db1 = s_dbl;
+  const int64_t E = a.rowptr[a.n];
+  const int64_t nchunks = (E + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+    const int nvalid = clamp_items(E - base);
+    const bool valid = e < E;
+    f32x16 dm[TH], yh[TH], h1[TH];
+    float rs = 0.0f;
+    f32x4 fx = {0.0f, 0.0f, 0.0f, 0.0f};
+    zero<TH>(dm);
+    zero<TH>(yh);
+    zero<TH>(h1);
+    if (nvalid > 0) {  // tiles past the last valid one are not allocated
+      const int64_t ec = valid ? e : E - 1;
+      load_tiled<TH>(dm, a.de0t + tile * (32 * H));
+      load_tiled<TH>(yh, a.yh + tile * (32 * H));
+      rs = a.rstd[ec];
+      // edge features (learned_simulator.py:299-312) and the first hidden layer, as the forward
+      const int64_t snd = a.send[ec], rcv = a.recv[ec];
+      float f[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      float ss = 0.0f;
+      for (int cc = 0; cc < a.dim; ++cc) {
+        const float d = __fdiv_rn(__fsub_rn(a.pos[snd * a.stride + cc], a.pos[rcv * a.stride + cc]), a.radius);
+        f[cc] = d;
+        ss = __fadd_rn(ss, __fmul_rn(d, d));
+      }
+      f[a.dim] = sqrtf(ss);
+      acc_bias<TH>(h1, a.b1);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {  // K = 4 in two 32x32x2 steps: k = 2 st + h
+        const int k = 2 * st + h;
+        const float b = st == 0 ? (h ? f[1] : f[0]) : (h ? f[3] : f[2]);
+#pragma unroll
+        for (int t = 0; t < TH; ++t) {
+          const float wv = k < nf ? a.w1[(32 * t + j) * nf + k] : 0.0f;
+          h1[t] = mfma32(wv, b, h1[t]);
+        }
+      }
+      acc_relu<TH>(h1);
+      if (valid) fx = f32x4{f[0], f[1], f[2], f[3]};
+    }
+    zero_if<TH>(dm, !valid);
+    zero_if<TH>(h1, !valid);
+    // LayerNorm backward (graph_network.py:92-96 encoder LN), its affine sums
+    f32x16 dy[TH];
+    acc_layernorm_bwd<TH>(dm, yh, rs, a.gamma, dy);
+    zero_if<TH>(dy, !valid);
+#pragma unroll
+    for (int t = 0; t < TH; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];
+    swz_store_items(sA, j, dm);
+    swz_store_items(sB, j, yh);
+    wave_lds_sync();
+    s_db += swz_col_sums(sA);
+    s_dg += swz_col_sums(sB);
+    wave_lds_sync();
+    // last Linear: dWl += dy (x) h1, dbl += dy, dh = (Wl^T dy) * [h1 > 0]
+    swz_store_items(sA, j, dy);
+    swz_store_items(sB, j, h1);
+    wave_lds_sync();
+    s_dbl += swz_col_sums(sA);
+    __syncthreads();
+    swz_outer(acc, bufA, 32 * tu, bufB, 32 * tv);
+    __syncthreads();
+    f32x16 dh[TH];
+    zero<TH>(dh);
+    swz_matvec_t(dh, wt, dy);
+    relu_mask<TH>(dh, h1, valid);
+    // first Linear: dW1 += dh (x) f, db1 += dh
+    swz_store_items(sA, j, dh);
+    swz_store_feat(sB, j, fx);
+    wave_lds_sync();
+    s_db1 += swz_col_sums(sA);
+    __syncthreads();
+    swz_outer_half(acc1, bufA, 32 * t1, bufB, 0, 32 * ih);
+    __syncthreads();
+  }
+  // the item halves of each dW1 tile: waves 2, 3 hand theirs to waves 0, 1 (fixed order)
+  if (w >= 2) store_tile_rowmajor(bufA + (w - 2) * 32 * 32, 32, acc1);
+  __syncthreads();
+  float* slab = a.slab + blockIdx.x * a.slab_stride;
+  if (w < 2) {
+    const int hh = l >> 5;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc1[r] += bufA[w * 32 * 32 + crow(r, hh) * 32 + j];
+    store_tile_rowmajor(slab + H * H + (32 * t1) * 32, 32, acc1);
+  }
+  store_tile_rowmajor(slab + (32 * tu) * H + 32 * tv, H, acc);
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_ENC_EDGE, H, 0, 2);
+  if (l < 16) {
+    st4(v + w * H + 4 * l, s_db1);
+    st4(v + kWaves * H + w * H + 4 * l, s_dbl);
+    st4(v + 2 * kWaves * H + w * H + 4 * l, s_dg);
+    st4(v + 3 * kWaves * H + w * H + 4 * l, s_db);
+  }
+}
+
 // ===========================================================================
 // Hidden 128: per-item chains and weight-gradient GEMMs in separate launches.
 // In the fused form every wave would hold 3-4 [128 x 128] weight-gradient
@@ -2243,6 +2401,10 @@ extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_
     if (nl == 3)
       run_wgrad<4, 4>(wg(p.d2_out, 1, 0, p.h1_out, 1, 0, slab, H * H + H * 32, H, vb + 4 * W * H, ss, 0, Edev),
                       nslab, stream);
+    return check_launch("encode_edges_bwd");
+  }
+  if (H == 64 && enc->nlin == 2 && dim <= 3) {  // single-scale training: two workgroups per CU
+    launch_bwd(k_enc_edge_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
     return check_launch("encode_edges_bwd");
   }
   const size_t lds = bwd_lds(SGNN_SLAB_ENC_EDGE, H, 0, enc->nlin);
