@@ -121,11 +121,13 @@ def test_gradients_against_oracle_autograd(nx, ny, radius, n_ex):
     print(f"{nx}x{ny} r={radius}: worst relative grad error {worst:.3e}")
 
 
-@pytest.mark.parametrize("dim,H,nmlp,L", [(2, 64, 2, 3), (2, 128, 1, 3), (3, 128, 2, 3), (2, 64, 1, 7)])
+@pytest.mark.parametrize("dim,H,nmlp,L", [(2, 64, 2, 3), (2, 128, 1, 3), (3, 128, 2, 3), (2, 64, 1, 7),
+                                          (3, 64, 1, 3), (1, 64, 1, 3)])
 def test_wide_and_deep_mlp_gradients_against_oracle(dim, H, nmlp, L):
     """H = 128 (weights read from L2) and nmlp_layers = 2 (3-Linear MLPs, middle
     Linear backward) through the fused backward, vs oracle autograd; L = 7 at
-    H = 64 takes the latent pass with the W1e images read from L2."""
+    H = 64 takes the latent pass with the W1e images read from L2; 3D / 1D at
+    H = 64 give the encoder edge backward (k_enc_edge_bwd64) 4 and 2 features."""
     from oracle import sgnn_oracle as O
     from sgnn_amd import synthetic
     from sgnn_amd.learned_simulator import LearnedSimulator
@@ -134,7 +136,8 @@ def test_wide_and_deep_mlp_gradients_against_oracle(dim, H, nmlp, L):
     # at depth 7 the fp32 oracle's own gradient error is 1.2e-3 of max|g|
     # (measured against the same oracle in float64; the HIP path is 3.3e-4 from it)
     rel = 5e-4 if L <= 5 else 2e-3
-    base = synthetic.lattice_2d(30, 20) if dim == 2 else synthetic.lattice_3d(10, 8, 6)
+    base = (synthetic.lattice_2d(30, 20) if dim == 2 else synthetic.lattice_3d(10, 8, 6) if dim == 3
+            else synthetic.lattice_2d(300, 1)[:, :1].copy())
     seq = synthetic.trajectory(base, T + 1, seed=5)
     n = seq.shape[0]
     st = synthetic.normalization_stats(dim, noise_std=0.02)
