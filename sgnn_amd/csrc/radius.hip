@@ -6,7 +6,8 @@
 // and stops at the cap) + k_csr_small (scan + compaction): two launches.
 //
 // Large graphs (no host sync, capturable in a hipGraph):
-//   0. k_bbox             bounding box of the finite coordinates (device atomics)
+//   0. k_bbox             per-block bounding boxes of the finite coordinates; zeroes
+//                         the cell histogram (no memset launch)
 //   1. k_cell_assign      particle -> (example, dense cell of side 1.01 r, grown
 //                         x2 until the grid fits the workspace); histogram
 //   2. scan               cell counts -> cell starts
@@ -107,9 +108,8 @@ SGNN_DEV float ord2f(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
 }
 
-// bbox words: [0..2] = ~ord(min_d) (atomicMax of the complement = min),
-// [3..5] = ord(max_d), [6] = arrival counter, [8..15] = the derived Grid
-// (written by the last-arriving block: agent-scope atomics + fence fan-in).
+// bbox words: [0..2] = ~ord(min_d) (max of the complement = min), [3..5] =
+// ord(max_d) (0: no finite value); the derived Grid lives at bbox + 8.
 
 // Every thread derives the same grid from the bbox (identical float ops).
 SGNN_DEV Grid make_grid(const uint32_t (&bbox)[6], int dim, int n_ex, float cell0, int64_t max_cells) {
@@ -137,16 +137,18 @@ SGNN_DEV Grid make_grid(const uint32_t (&bbox)[6], int dim, int n_ex, float cell
   return G;
 }
 
+// Per-block bounding-box partials (no atomics, nothing to initialise): block
+// b writes its 6 words to bboxp[8 b ..]; k_cell_assign reduces them.  The
+// blocks also zero the cell histogram words (count, fill) the later kernels
+// accumulate into, so the pipeline needs no memset launch.
 template <int DIM>
-__global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, int64_t n,
-                                              int n_ex, float cell0, int64_t max_cells,
-                                              uint32_t* bbox) {
-  constexpr int dim = DIM;
+__global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, int64_t n, uint32_t* bboxp,
+                                              int32_t* zero, int64_t nzero) {
   __shared__ uint32_t red[6][4];
-  __shared__ bool last;
   uint32_t v[6] = {0, 0, 0, 0, 0, 0};
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t gsz = (int64_t)gridDim.x * blockDim.x, gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = gid; i < nzero; i += gsz) zero[i] = 0;
+  for (int64_t i = gid; i < n; i += gsz) {
 #pragma unroll
     for (int d = 0; d < DIM; ++d) {
       const float x = pos[i * stride + d];
@@ -168,23 +170,7 @@ __global__ __launch_bounds__(256) void k_bbox(const float* pos, int64_t stride, 
   if (threadIdx.x < 6) {
     uint32_t a = 0;
     for (int k = 0; k < (int)(blockDim.x >> 6); ++k) a = max(a, red[threadIdx.x][k]);
-    if (a) atomicMax(&bbox[threadIdx.x], a);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint32_t t = __hip_atomic_fetch_add(&bbox[6], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    uint32_t b[6];
-    for (int k = 0; k < 6; ++k)
-      b[k] = __hip_atomic_load(&bbox[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const Grid G = make_grid(b, dim, n_ex, cell0, max_cells);
-    Grid* out = reinterpret_cast<Grid*>(bbox + 8);
-    *out = G;
+    bboxp[8 * blockIdx.x + threadIdx.x] = a;
   }
 }
 
@@ -234,18 +220,36 @@ SGNN_DEV int32_t wave_aggregated_inc(int32_t* counter, int32_t key, bool active)
 // DIM is a template parameter: with a runtime dimension loop the compiler kept
 // the Grid in LDS and issued the coordinate loads one after another (measured
 // 25 us vs 4 us for 50k particles, tools/bench_assign.hip).
+// Every block reduces k_bbox's partials and derives the grid (identical float
+// ops in every block); block 0 also stores it at bbox + 8 for the query.
 template <int DIM>
 __global__ __launch_bounds__(256) void k_cell_assign(const float* pos, int64_t stride, int64_t n,
                                                      const int64_t* ex_ptr, int n_ex,
-                                                     const uint32_t* bbox, int32_t* cell_of_p,
+                                                     const uint32_t* bboxp, int nbb, float cell0,
+                                                     int64_t max_cells, uint32_t* bbox, int32_t* cell_of_p,
                                                      int32_t* ex_of, int32_t* count) {
+  __shared__ Grid sG;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i0 < n;
   const int64_t i = active ? i0 : n - 1;
   float x[DIM];
 #pragma unroll
   for (int d = 0; d < DIM; ++d) x[d] = pos[i * stride + d];
-  const Grid G = *reinterpret_cast<const Grid*>(bbox + 8);
+  if (threadIdx.x < 64) {  // wave 0: lane L takes partials L, L + 64 (nbb <= 128), then a butterfly
+    uint32_t v[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = threadIdx.x; k < nbb; k += 64)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) v[c] = max(v[c], bboxp[8 * k + c]);
+#pragma unroll
+    for (int c = 0; c < 6; ++c)
+      for (int o = 32; o > 0; o >>= 1) v[c] = max(v[c], (uint32_t)__shfl_xor((int)v[c], o, 64));
+    if (threadIdx.x == 0) {
+      sG = make_grid(v, DIM, n_ex, cell0, max_cells);
+      if (blockIdx.x == 0) *reinterpret_cast<Grid*>(bbox + 8) = sG;
+    }
+  }
+  __syncthreads();
+  const Grid G = sG;
   int lo = 0, hi = n_ex - 1;  // largest b with ex_ptr[b] <= i
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -478,10 +482,12 @@ __global__ __launch_bounds__(1024) void k_csr_small(int n, int cap, const int32_
   }
 }
 
+constexpr int kBboxBlocks = 128;
+
 struct RadiusWs {
   uint32_t nbuckets;  // cell capacity (cells of all examples)
   int32_t *count, *fill, *start, *bucket_of, *ex_of, *order, *nbr, *deg, *partials;
-  uint32_t* bbox;
+  uint32_t *bbox, *bboxp;
   f32x4* cpos;  // [n] cell-ordered (x, y, z, id)
   size_t bytes;
 };
@@ -503,9 +509,10 @@ RadiusWs radius_layout(int64_t n, int32_t K, int32_t loop, void* base) {
     off += align_up(sizeof(int32_t) * (size_t)count);
     return r;
   };
-  w.count = take(2 * (int64_t)m + 2 + 16);  // count[m+1], fill[m+1], bbox[16]: one memset
+  w.count = take(2 * (int64_t)m + 2);  // count[m+1], fill[m+1]: zeroed by k_bbox
   w.fill = w.count + m + 1;
-  w.bbox = reinterpret_cast<uint32_t*>(w.fill + m + 1);
+  w.bbox = reinterpret_cast<uint32_t*>(take(16));                 // Grid at + 8
+  w.bboxp = reinterpret_cast<uint32_t*>(take(8 * kBboxBlocks));   // k_bbox per-block partials
   w.start = take(m + 1);
   w.bucket_of = take(n);
   w.ex_of = take(n);
@@ -609,16 +616,16 @@ extern "C" int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n
   const float cell0 = radius * 1.01f;  // margin keeps |dp| < r inside +-1 cell under rounding
   const int64_t max_cells = w.nbuckets;
   const unsigned nblk = (unsigned)((n + 255) / 256);
-  (void)hipMemsetAsync(w.count, 0, sizeof(int32_t) * (2 * (size_t)w.nbuckets + 2 + 16), stream);
-  const unsigned bblk = std::min<unsigned>(nblk, 128);
+  const unsigned bblk = std::min<unsigned>(nblk, kBboxBlocks);
 #define SGNN_DIM_LAUNCH(K, GRID, ...)                                                                 \
   do {                                                                                             \
     if (dim == 1) hipLaunchKernelGGL(K<1>, dim3(GRID), dim3(256), 0, stream, __VA_ARGS__);          \
     else if (dim == 2) hipLaunchKernelGGL(K<2>, dim3(GRID), dim3(256), 0, stream, __VA_ARGS__);     \
     else hipLaunchKernelGGL(K<3>, dim3(GRID), dim3(256), 0, stream, __VA_ARGS__);                   \
   } while (0)
-  SGNN_DIM_LAUNCH(k_bbox, bblk, pos, pos_stride, n, n_ex, cell0, max_cells, w.bbox);
-  SGNN_DIM_LAUNCH(k_cell_assign, nblk, pos, pos_stride, n, ex_ptr, n_ex, w.bbox, w.bucket_of, w.ex_of, w.count);
+  SGNN_DIM_LAUNCH(k_bbox, bblk, pos, pos_stride, n, w.bboxp, w.count, 2 * (int64_t)w.nbuckets + 2);
+  SGNN_DIM_LAUNCH(k_cell_assign, nblk, pos, pos_stride, n, ex_ptr, n_ex, w.bboxp, (int)bblk, cell0, max_cells,
+                  w.bbox, w.bucket_of, w.ex_of, w.count);
   int st = scan_exclusive(w.count, w.start, (int64_t)w.nbuckets + 1, w.partials, stream);
   if (st) return st;
   SGNN_DIM_LAUNCH(k_cell_scatter, nblk, n, w.bucket_of, w.start, w.fill, w.order, pos, pos_stride, w.cpos);
