@@ -733,6 +733,8 @@ int layer16_launch(const Layer16Args& a, int mode, int nl, hipStream_t s, bool f
                                        "cap <= 32");
   // one workgroup per CU: the whole register file (no spills; C1 r = 15 0.1222 -> 0.1184 ms/step,
   // r = 0.6 0.0845 -> 0.081)
+  // (measured slower past 256 workgroups, one per CU in two rounds: 4,800 particles 0.155 -> 0.173,
+  // 8,000 0.217 -> 0.242 ms/step)
   if (grid <= 256) {
     if (first) hipLaunchKernelGGL((k_layer16<2, 0, true, 1>), dim3(grid), dim3(kBlock16), 0, s, a);
     else if (mode == 0 && nl == 2) hipLaunchKernelGGL((k_layer16<2, 0, false, 1>), dim3(grid), dim3(kBlock16), 0, s, a);
