@@ -104,6 +104,40 @@ int sgnn_encode_edge_features(const float* e, int32_t fe, const int32_t* perm,
                               const sgnn_mlp* enc, float* e0t, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Width-generic blocks (generic.hip): any latent / hidden / edge widths and
+ * nmlp_layers, plain fp32 FMA -- the reference's build_mlp(...) (+ LayerNorm)
+ * (graph_network.py:7-45, :86-96, :139-148, :321-322; multi_scale_gnn.py:26-64)
+ * on rows assembled from up to three sources, the MessagePassing receiver sum
+ * (aggr='add', graph_network.py:136 / multi_scale_gnn.py:67) and the feature
+ * construction of _encoder_preprocessor (learned_simulator.py:231-316).  They
+ * back the reference's per-module forwards (Encoder / InteractionNetwork /
+ * Processor / Decoder, G2M / M2M / M2G blocks) and the shapes the MFMA kernels
+ * are not built for; the hidden-64 / 128 kernels above are the fast path.
+ * ------------------------------------------------------------------------- */
+typedef struct sgnn_rows_src {
+  const float* data;    /* row r of this source: data[(index ? index[r] : r) * ld + c], c < dim */
+  const int32_t* index; /* optional gather (e.g. receivers / senders of every edge) */
+  int64_t ld;
+  int32_t dim;
+  float scale;          /* multiplies every value read (1 = none) */
+} sgnn_rows_src;
+/* out[r] = MLP(cat(src_0[r], .., src_{nsrc-1}[r])) (+ LayerNorm when mlp->ln_g) (+ residual[r]);
+ * out / residual: [n][mlp->out_dim].  1 <= nsrc <= 3; the widths must sum to mlp->in_dim. */
+int sgnn_rows_mlp(const sgnn_rows_src* srcs, int32_t nsrc, int64_t n, const sgnn_mlp* mlp,
+                  const float* residual, float* out, void* stream);
+/* agg[i] = sum of m[perm ? perm[p] : p] over p in [rowptr[i], rowptr[i+1]) (receiver CSR, in order). */
+int sgnn_segment_sum(const float* m, const int32_t* rowptr, const int32_t* perm, int64_t n, int32_t width,
+                     float* agg, void* stream);
+/* Node features [n][(T-1)*dim + 1 (+ emb_dim)] (learned_simulator.py:256-290; wall as sgnn_encode_nodes). */
+int sgnn_node_features(const float* pos_seq, int64_t n, int32_t T, int32_t dim, const int64_t* types,
+                       const float* emb_w, int32_t emb_dim, int32_t use_emb, const float* vel_mean,
+                       const float* vel_std, float wall_max, float wall_div, float* out, void* stream);
+/* Edge features [E][dim+1] in CSR order (learned_simulator.py:299-312), E = rowptr[n]. */
+int sgnn_edge_features(const float* pos, int64_t pos_stride, int32_t dim, float radius,
+                       const int32_t* rowptr, const int32_t* send, const int32_t* recv, int64_t n,
+                       int64_t edge_cap, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Encoder, node side: node features of LearnedSimulator._encoder_preprocessor
  * (learned_simulator.py:256-290: normalised velocity history, wall distance
  * clamp(x+2, 0, wall_max) / wall_div — single scale: (R, 1), learned_simulator.py:
@@ -240,11 +274,25 @@ typedef struct sgnn_step_ws { /* device buffers of one (n, T, dim, H, K) shape *
   float *e0t, *x_a, *x_b, *u, *v, *agg, *cin, *cout;
   float *u2, *v2; /* [n][H] second node-half buffers: with both set, H = 64 and n <= 8192 each
                      layer runs as ONE sgnn_interaction_layer launch (u/v ping-pong); else two */
+  /* Optional, the one-launch step (hidden 64, nmlp_layers 1, n <= 4096, 2 <= nlayers <= 10):
+   * with all three set, a whole step is ONE kernel launch (radius graph, encoders, every layer,
+   * decoder, integrator; sgnn_step_path() says whether it applies).  The radius graph then stays
+   * in the kernel's LDS: rowptr/send/recv are not written, step_deg receives each receiver's
+   * neighbour count. */
+  float* uvl;           /* nlayers*2*n*H + (n+16)*K*(H+4) floats: every layer's node halves u_k, v_k
+                           ([nlayers][2][n][H]), then room for the edge latents of tiles too large for
+                           the kernel's LDS */
+  uint32_t* step_flags; /* [512] per-workgroup phase counters + error word (zeroed per call) */
+  int32_t* step_deg;    /* [n] neighbours kept per receiver */
 } sgnn_step_ws;
 
 int sgnn_predict_positions(const sgnn_epd* model, const sgnn_step_in* in, const float* pos_seq,
                            const sgnn_step_ws* ws, float* pred, float* next_pos, float* window_out,
                            void* stream);
+/* 1 when sgnn_predict_positions / sgnn_rollout run these arguments as the one-launch step, 0 when
+ * they run the per-kernel sequence; (*nt, *grid) = receivers per workgroup and workgroups. */
+int sgnn_step_path(const sgnn_epd* model, const sgnn_step_in* in, const sgnn_step_ws* ws, int32_t* nt,
+                   int32_t* grid);
 /* Steps alternate win_a -> win_b -> win_a ...; step k writes out_pred[k][n][dim+1]
  * (normalised acceleration + strain) and out_pos[k][n][dim]. */
 int sgnn_rollout(const sgnn_epd* model, const sgnn_step_in* in, float* win_a, float* win_b,

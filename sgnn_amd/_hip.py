@@ -55,7 +55,8 @@ class SgnnStepWs(ctypes.Structure):
     _fields_ = [("radius_ws", c_void_p), ("rowptr", c_void_p), ("send", c_void_p), ("recv", c_void_p),
                 ("edge_cap", c_int64), ("e0t", c_void_p), ("x_a", c_void_p), ("x_b", c_void_p),
                 ("u", c_void_p), ("v", c_void_p), ("agg", c_void_p), ("cin", c_void_p), ("cout", c_void_p),
-                ("u2", c_void_p), ("v2", c_void_p)]
+                ("u2", c_void_p), ("v2", c_void_p), ("uvl", c_void_p), ("step_flags", c_void_p),
+                ("step_deg", c_void_p)]
 
 
 class SgnnReduceDesc(ctypes.Structure):
@@ -64,6 +65,11 @@ class SgnnReduceDesc(ctypes.Structure):
                 ("rep_stride", c_int64), ("nslab", c_int32), ("nrep", c_int32), ("src_ld", c_int32),
                 ("nrows", c_int32), ("ncols", c_int32), ("dst_ld", c_int32), ("accumulate", c_int32),
                 ("scale", c_float)]
+
+
+class SgnnRowsSrc(ctypes.Structure):
+    """struct sgnn_rows_src (include/sgnn.h)."""
+    _fields_ = [("data", c_void_p), ("index", c_void_p), ("ld", c_int64), ("dim", c_int32), ("scale", c_float)]
 
 
 P_SAVES = ctypes.POINTER(SgnnSaves)
@@ -145,6 +151,14 @@ SIGNATURES = {
                                              P_MLP, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
     "sgnn_predict_positions": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p, c_void_p]),
+    "sgnn_rows_mlp": (ctypes.c_int, [ctypes.POINTER(SgnnRowsSrc), c_int32, c_int64, P_MLP, c_void_p, c_void_p,
+                                     c_void_p]),
+    "sgnn_segment_sum": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "sgnn_node_features": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                          c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p]),
+    "sgnn_edge_features": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_int64,
+                                          c_int64, c_void_p, c_void_p]),
+    "sgnn_step_path": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sgnn_rollout": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                     c_void_p, c_void_p]),
     "sgnn_random_walk_noise": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_float, ctypes.c_uint64,

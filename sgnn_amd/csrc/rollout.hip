@@ -5,13 +5,112 @@
 #include "../../include/sgnn.h"
 #include "sgnn_internal.h"
 #include "radius_small.h"
+#include "step16.h"
 
-extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq,
-                                      const sgnn_step_ws* ws, float* pred, float* next_pos,
-                                      float* window_out, void* stream) {
+namespace {
+
+// An MLP of nmlp_layers 1 with these widths (and a LayerNorm when `ln`).
+bool mlp16(const sgnn_mlp* m, int in_dim, int out_dim, bool ln) {
+  return m && m->nlin == 2 && m->w1 && m->b1 && m->w2 && m->b2 && m->in_dim == in_dim && m->hidden == 64 &&
+         m->out_dim == out_dim && (!ln || (m->ln_g && m->ln_b));
+}
+
+int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t p{};
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount
+                                                                                              : -1;
+  }
+  return cus;
+}
+
+// The one-launch step's arguments when it applies to this call (step16.hip):
+// hidden 64, nmlp_layers 1 everywhere, 2..10 layers, n <= 4096 particles, a
+// grid of <= one workgroup per CU, and the kernel's LDS under 160 KB.
+bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq, const sgnn_step_ws* ws,
+                 float* pred, float* next_pos, float* window_out, sgnn::Step16Args* out) {
+  using namespace sgnn;
+  if (!m || !in || !ws || !ws->uvl || !ws->step_flags || !ws->step_deg) return false;
+  const int L = m->nlayers;
+  const int64_t n = in->n;
+  const int d = in->dim, T = in->T;
+  const int cap = in->K;  // predict_positions keeps self loops (learned_simulator.py:75,117)
+  if (L < 2 || L > kStep16MaxL || n < 1 || n > kStep16MaxGrid * kStep16MaxNT || d < 1 || d > 3 || T < 2 ||
+      cap < 1 || cap > kStep16MaxCap || in->n_ex < 1 || !in->ex_ptr || !(in->radius > 0.0f))
+    return false;
+  const int feat = (T - 1) * d + 1 + (in->use_emb ? in->emb_dim : 0);
+  if (feat > 48 || !mlp16(m->enc_node, feat, 64, true) || !mlp16(m->enc_edge, d + 1, 64, true) ||
+      !mlp16(m->dec, 64, d + 1, false))
+    return false;
+  for (int k = 0; k < L; ++k)
+    if (!mlp16(&m->edge[k], 3 * 64, 64, true) || !mlp16(&m->node[k], 2 * 64, 64, true)) return false;
+  Step16Args a{};
+  a.n = (int)n; a.T = T; a.dim = d; a.ex_ptr = in->ex_ptr; a.n_ex = in->n_ex;
+  a.radius = in->radius; a.r2 = in->radius * in->radius; a.cap = cap; a.loop = 1;
+  a.types = in->types; a.emb_w = in->emb_w; a.emb_dim = in->emb_dim; a.use_emb = in->use_emb; a.feat = feat;
+  a.vel_mean = in->vel_mean; a.vel_std = in->vel_std; a.acc_mean = in->acc_mean; a.acc_std = in->acc_std;
+  a.wall_max = in->wall_max; a.wall_div = in->wall_div;
+  a.L = L;
+  for (int k = 0; k < L; ++k) {
+    const sgnn_mlp &e = m->edge[k], &v = m->node[k];
+    a.lay[k] = Lay16{e.w1, e.b1, e.w2, e.b2, e.ln_g, e.ln_b, v.w1, v.b1, v.w2, v.b2, v.ln_g, v.ln_b};
+  }
+  const sgnn_mlp *xn = m->enc_node, *xe = m->enc_edge, *dc = m->dec;
+  a.xn_w1 = xn->w1; a.xn_b1 = xn->b1; a.xn_w2 = xn->w2; a.xn_b2 = xn->b2; a.xn_g = xn->ln_g; a.xn_bb = xn->ln_b;
+  a.xe_w1 = xe->w1; a.xe_b1 = xe->b1; a.xe_w2 = xe->w2; a.xe_b2 = xe->b2; a.xe_g = xe->ln_g; a.xe_bb = xe->ln_b;
+  a.d_w1 = dc->w1; a.d_b1 = dc->b1; a.d_w2 = dc->w2; a.d_b2 = dc->b2;
+  a.uvl = ws->uvl; a.flags = ws->step_flags; a.deg_out = ws->step_deg; a.nbr_out = nullptr;
+  a.pos_seq = pos_seq; a.pred = pred; a.next_pos = next_pos; a.window_out = window_out;
+  // receivers per workgroup: 8 up to 2,048 particles (C1: 250 workgroups), then as many as keep
+  // the grid at one workgroup per CU
+  const int64_t cus = std::min<int64_t>(device_cus(), kStep16MaxGrid);
+  if (cus < 1) return false;
+  a.nt = (int)std::max<int64_t>(8, (n + cus - 1) / cus);
+  if (a.nt > kStep16MaxNT || (n + a.nt - 1) / a.nt > cus) return false;
+  a.ecap_t = a.nt * cap;
+  a.e0_hbm = 0;
+  size_t lds = step16_lds_bytes(a);
+  if (lds > kStep16MaxLds) {  // the tile's e0 rows do not fit in LDS: keep them in HBM (ws->uvl's tail)
+    a.e0_hbm = 1;
+    lds = step16_lds_bytes(a);
+  }
+  if (lds == 0 || lds > kStep16MaxLds) return false;
+  *out = a;
+  return true;
+}
+
+constexpr size_t kStepFlagBytes = 512 * sizeof(uint32_t);
+
+}  // namespace
+
+extern "C" int sgnn_step_path(const sgnn_epd* m, const sgnn_step_in* in, const sgnn_step_ws* ws, int32_t* nt,
+                              int32_t* grid) {
+  sgnn::Step16Args a{};
+  float dummy = 0.0f;
+  const bool one = step16_plan(m, in, &dummy, ws, &dummy, &dummy, nullptr, &a);
+  if (nt) *nt = one ? a.nt : 0;
+  if (grid) *grid = one ? (int32_t)((a.n + a.nt - 1) / a.nt) : 0;
+  return one ? 1 : 0;
+}
+
+// One predict_positions; `step` = index of this step within the call (the
+// one-launch step's phase counters are zeroed at step 0 and count on).
+static int predict_impl(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq, const sgnn_step_ws* ws,
+                        float* pred, float* next_pos, float* window_out, void* stream, int32_t step) {
   using namespace sgnn;
   if (!m || !in || !pos_seq || !ws || !pred || !next_pos || m->nlayers < 1 || !m->edge || !m->node)
     return set_error(SGNN_ERR_INVALID, "predict_positions: bad arguments");
+  if (window_out && window_out == pos_seq)
+    return set_error(SGNN_ERR_INVALID, "predict_positions: window_out aliases pos_seq");
+  Step16Args sa{};
+  if (step16_plan(m, in, pos_seq, ws, pred, next_pos, window_out, &sa)) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (step == 0) (void)hipMemsetAsync(ws->step_flags, 0, kStepFlagBytes, s);
+    sa.epoch0 = (uint32_t)step * (uint32_t)(m->nlayers + 1);
+    return step16_launch(sa, s);
+  }
   const int64_t n = in->n;
   const int T = in->T, d = in->dim;
   // radius graph on the most recent frame (learned_simulator.py:116-117); graphs of <= 2,560
@@ -96,6 +195,12 @@ extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in,
   return SGNN_OK;
 }
 
+extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq,
+                                      const sgnn_step_ws* ws, float* pred, float* next_pos,
+                                      float* window_out, void* stream) {
+  return predict_impl(m, in, pos_seq, ws, pred, next_pos, window_out, stream, 0);
+}
+
 extern "C" int sgnn_rollout(const sgnn_epd* m, const sgnn_step_in* in, float* win_a, float* win_b,
                             const sgnn_step_ws* ws, int32_t nsteps, float* out_pos, float* out_pred,
                             void* stream) {
@@ -107,8 +212,8 @@ extern "C" int sgnn_rollout(const sgnn_epd* m, const sgnn_step_in* in, float* wi
   for (int32_t k = 0; k < nsteps; ++k) {
     float* cur = (k & 1) ? win_b : win_a;
     float* nxt = (k & 1) ? win_a : win_b;
-    const int st = sgnn_predict_positions(m, in, cur, ws, out_pred + (int64_t)k * n * (d + 1),
-                                          out_pos + (int64_t)k * n * d, nxt, stream);
+    const int st = predict_impl(m, in, cur, ws, out_pred + (int64_t)k * n * (d + 1), out_pos + (int64_t)k * n * d,
+                                nxt, stream, k);
     if (st) return st;
   }
   return SGNN_OK;

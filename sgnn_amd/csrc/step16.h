@@ -1,0 +1,60 @@
+// One LearnedSimulator.predict_positions step in ONE launch (step16.hip):
+// shared between the step driver (rollout.hip) and the kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sgnn {
+
+constexpr int kStep16MaxL = 10;     // interaction layers carried in the kernel arguments
+constexpr int kStep16MaxNT = 16;    // receivers per workgroup (one 16-item node tile)
+constexpr int kStep16MaxCap = 64;   // neighbour cap (K, +1 without self loops)
+constexpr int kStep16MaxGrid = 256; // one workgroup per CU, every workgroup resident
+constexpr size_t kStep16MaxLds = 160 * 1024;
+
+// Weights of one InteractionNetwork (nmlp_layers 1): edge_fn = Linear(3H, H) ->
+// ReLU -> Linear(H, H) -> LayerNorm, node_fn = Linear(2H, H) -> ReLU ->
+// Linear(H, H) -> LayerNorm (graph_network.py:139-148), torch [out][in].
+struct Lay16 {
+  const float *ew1, *eb1, *ew2, *eb2, *eg, *ebb;
+  const float *nw1, *nb1, *nw2, *nb2, *ng, *nbb;
+};
+
+struct Step16Args {
+  // inputs (learned_simulator.py:413-438): window [n][T][dim], examples
+  const float* pos_seq;
+  int n, T, dim;
+  const int64_t* ex_ptr;
+  int n_ex;
+  float radius, r2;
+  int cap, loop;  // kept neighbours per receiver (K, or K + 1 then the self loop dropped)
+  const int64_t* types;
+  const float* emb_w;
+  int emb_dim, use_emb, feat;
+  const float *vel_mean, *vel_std, *acc_mean, *acc_std;
+  float wall_max, wall_div;
+  // weights
+  int L;
+  Lay16 lay[kStep16MaxL];
+  const float *xn_w1, *xn_b1, *xn_w2, *xn_b2, *xn_g, *xn_bb;  // Encoder.node_fn
+  const float *xe_w1, *xe_b1, *xe_w2, *xe_b2, *xe_g, *xe_bb;  // Encoder.edge_fn
+  const float *d_w1, *d_b1, *d_w2, *d_b2;                    // Decoder
+  // workspace
+  float* uvl;          // [L][2][n][H]: layer k's node halves u_k, v_k (written once per step), then (e0_hbm)
+                       // [grid][ecap_t][H + 4] e0 rows of each tile's edges
+  int e0_hbm;          // e0 rows in HBM instead of LDS (tiles whose edges do not fit next to the weights)
+  uint32_t* flags;     // [grid] per-tile phase counters + [grid] error word, zeroed per call
+  uint32_t epoch0;     // phase counter base of this step within the call
+  int nt;              // receivers per workgroup
+  int ecap_t;          // edge rows per workgroup (nt * cap)
+  int32_t *deg_out, *nbr_out;  // optional: the radius graph as padded lists [n], [n][cap]
+  // outputs
+  float *pred, *next_pos, *window_out;
+};
+
+// LDS bytes the kernel needs for these arguments (0 when it does not apply).
+size_t step16_lds_bytes(const Step16Args& a);
+// Launches the kernel (a.nt / a.ecap_t set by the caller; grid = ceil(n / nt)).
+int step16_launch(const Step16Args& a, hipStream_t s);
+
+}  // namespace sgnn

@@ -1,0 +1,619 @@
+// One whole LearnedSimulator.predict_positions (learned_simulator.py:413-438)
+// in ONE launch, for graphs of up to 4,096 particles at hidden 64 and
+// nmlp_layers 1 (the C1 headline: 2,000 particles, r = 15, L = 5):
+//   radius graph (torch_cluster.radius via radius_graph, :116-117)
+//   -> Encoder (graph_network.py:86-96, features :231-316)
+//   -> L x InteractionNetwork (graph_network.py:150-222, edge-latent doubling)
+//   -> Decoder (:321-333) -> Euler integrator (learned_simulator.py:381-411)
+//   (+ the rollout window shift, evaluate.py:136-139).
+//
+// Why one launch.  At C1 the whole step is ~7 GFLOP of fp32 MFMA work, 45 us
+// of a 256-CU chip's time at the 1/4 MFMA occupancy one wave per SIMD
+// reaches, and the per-layer launch sequence paid, per layer, a kernel
+// boundary, a grid-wide ramp, and a weight staging pass that no other work
+// overlapped.  Here workgroup t owns receivers
+// [t*nt, t*nt + nt) for the whole step and stays resident (grid <= 256, one
+// workgroup per CU by its LDS size).  Layer k of tile t needs only layer k's
+// node halves u_k, v_k of the tiles its senders live in, so instead of a grid
+// barrier every tile publishes a per-tile phase counter after writing its
+// rows and every consumer waits on the counters of ITS sender tiles only
+// (dataflow: a slow tile delays its dependents, not the chip).  While a tile
+// waits, the next layer's weights are already in flight.
+//
+// Hand-off protocol (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md
+// "visibility", table row 1: one workgroup per CU, hipMalloc memory): every
+// handed-off byte (u_k / v_k rows) is stored write-through (sc1) and drained
+// (s_waitcnt vmcnt(0) in every storing wave, then a workgroup barrier); ONE
+// lane then stores the tile's counter with an agent-scope atomic (sc1 store).
+// The consumer's wave 0 polls the counters relaxed (sc1 loads); the other
+// waves pass a workgroup barrier after the match; EVERY load of handed-off
+// rows is an sc1 buffer load (no L1), so no acquire fence is needed.  Each
+// layer's u/v go to their own buffers (written once per step), so there is
+// no write-after-read hazard between tiles at different layers; x and the
+// edge latent e0 of a tile's own edges never leave its LDS.  Counters are
+// zeroed by the driver at the start of every call; phase p of step s is
+// epoch0 + p + 1 with epoch0 = s (L + 1).  Every spin is bounded: a tile that
+// times out records it in an error word and finishes (results are then
+// garbage; the driver's tests read the word).
+#include "common.h"
+#include "fwd16.h"
+#include "sgnn_internal.h"
+#include "step16.h"
+
+#include "fwd16_dev.h"
+
+namespace {
+
+using sgnn::Step16Args;
+using sgnn::Lay16;
+
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+constexpr int kPollLimit = 1 << 21;   // ~1 s of polling: a hang becomes an error word
+constexpr int kMaxGrid = sgnn::kStep16MaxGrid;
+
+SGNN_DEV f32x4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, int voff) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(f32x4, __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 16)));
+}
+SGNN_DEV void st4_sc1(__amdgpu_buffer_rsrc_t rs, int voff, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff, 0, 16);
+}
+
+// LDS carve (floats), shared with the host's size query.
+struct Carve {
+  int sw0, sw1, svec, sxw, sxv, scratch, xs, region, ints, total;  // float offsets / count
+  int region_floats;
+};
+SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
+  Carve c{};
+  int o = 0;
+  c.sw0 = o; o += H * LDX;        // edge W1e (x 2^k), LDS image [H][LDX]
+  c.sw1 = o; o += H * LDX;        // edge W2
+  c.svec = o; o += 4 * H;         // edge b2, gamma, beta
+  c.sxw = o; o += H * LDX;        // Encoder.edge_fn W2
+  c.sxv = o; o += 4 * H;          // Encoder.edge_fn b1, b2, gamma, beta
+  c.scratch = o; o += 4 * 16 * LDX;  // per-wave receiver sums; node-phase exchange buffers
+  c.xs = o; o += 16 * LDX;        // x rows of the tile's nodes (resident for the step)
+  const int e0f = e0g ? 0 : nt * cap * LDX, posf = n * dim;
+  c.region_floats = e0f > posf ? e0f : posf;  // positions (radius phase), then e0 rows (unless in HBM)
+  c.region = o; o += (c.region_floats + 3) & ~3;
+  c.ints = o;                     // lsend, lrecv, nbr [nt*cap] each; deg [16]; pre [20]; mask [8]; kw [4][64]
+  o += 3 * nt * cap + 16 + 20 + 8 + 4 * 64;
+  c.total = (o + 3) & ~3;
+  return c;
+}
+
+// Per-tile counters: wave 0 polls those of the tiles in `mask`, the others wait at the barrier.
+SGNN_DEV void wait_tiles(const uint32_t* mask, uint32_t* flags, int G, uint32_t epoch, int b, int lane) {
+  if (b == 0) {
+    for (int it = 0;; ++it) {
+      bool ok = true;
+      for (int t = lane; t < G; t += 64)
+        if ((mask[t >> 5] >> (t & 31)) & 1u)
+          ok = ok && __hip_atomic_load((gu32*)(flags + t), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+      if (__all(ok)) break;
+      if (it >= kPollLimit) {
+        if (lane == 0)
+          __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+// Every storing wave drains its sc1 stores, then one lane publishes the phase.
+SGNN_DEV void publish(uint32_t* flags, int tile, uint32_t epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store((gu32*)(flags + tile), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Node update of the tile (16 item rows, `valid` rows written) from the first
+// Linear's post-ReLU output h: last Linear, LayerNorm, + residual xo -> x
+// (LDS rows xs), then u, v of the next layer (mode 0, sc1 rows) or decoder +
+// integrator + window shift (mode 1).  Same arithmetic as fwd16.hip node_tail.
+template <int MODE>
+SGNN_DEV void step_tail(const Step16Args& a, const NodeW<2, MODE>& W, float* scratch, float* xs, int64_t i,
+                        bool valid, f32x4 h, f32x4 xo, int b, int j, int g, __amdgpu_buffer_rsrc_t ru,
+                        __amdgpu_buffer_rsrc_t rv) {
+  const int ucol = 16 * b + 4 * g;
+  f32x4 hr[KQ], yr[KQ], xnr[KQ];
+  xchg(scratch, j, ucol, g, h, hr);
+  const f32x4 y = mm(W.vb2, W.w2, hr);
+  xchg(scratch + 16 * LDX, j, ucol, g, y, yr);
+  float mean, rstd;
+  ln_stats(yr, mean, rstd);
+  f32x4 xn;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xn[c] = (y[c] - mean) * rstd * W.vg[c] + W.vbb[c] + xo[c];  // LN (+ :176 residual)
+  xchg(xs, j, ucol, g, xn, xnr);
+  if constexpr (MODE == 0) {
+    const f32x4 u = mm(W.vba, W.wa, xnr);
+    const f32x4 v = mm(zero4(), W.wb, xnr);
+    const int off = valid ? (int)i * (H * 4) + ucol * 4 : kBufDrop;
+    st4_sc1(ru, off, u);
+    st4_sc1(rv, off, v);
+  } else {
+    f32x4 hdr[KQ];
+    xchg(scratch + 2 * 16 * LDX, j, ucol, g, relu4(mm(W.vba, W.wa, xnr)), hdr);
+    const int D = a.dim;
+    if (b == 0) {
+      const f32x4 o = mm(W.vbo, W.wb, hdr);  // lanes g == 0 hold outputs 0..3
+      if (valid && g == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c <= D) a.pred[i * (D + 1) + c] = comp(o, c);
+        const float* p = a.pos_seq + i * a.T * D;  // learned_simulator.py:398-411
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if (c >= D) break;
+          const float acc = __fadd_rn(__fmul_rn(comp(o, c), a.acc_std[c]), a.acc_mean[c]);
+          const float pT = p[(a.T - 1) * D + c], pT1 = p[(a.T - 2) * D + c];
+          const float np = __fadd_rn(pT, __fadd_rn(__fsub_rn(pT, pT1), acc));
+          a.next_pos[i * D + c] = np;
+          if (a.window_out) a.window_out[(i * a.T + a.T - 1) * D + c] = np;
+        }
+      }
+    } else if (b == 1 && g == 0 && valid && a.window_out) {  // evaluate.py:136-139
+      const float* p = a.pos_seq + i * a.T * D;
+      float* w = a.window_out + i * a.T * D;
+      for (int k = 0; k < (a.T - 1) * D; ++k) w[k] = p[k + D];
+    }
+  }
+}
+
+// The edge MLP over the tile's edges (wave b takes the 16-edge halves b, b + 4,
+// ... of the compacted tile CSR), LayerNorm, and the receiver sums (DPP
+// row-segmented scan, per-wave LDS rows, fixed order).  FIRST: the edge
+// features and Encoder.edge_fn run inline and e0 rows are kept in LDS.
+template <bool FIRST>
+SGNN_DEV void step_edges(const Step16Args& a, const float* sw0, const float* sw1, const float* svec,
+                         const float* sxw, const float* sxv, const float (&xw1)[KQ], float* sums, float* e0l,
+                         const int32_t* lsend, const int32_t* lrecv, int Et, int i0,
+                         __amdgpu_buffer_rsrc_t ru, __amdgpu_buffer_rsrc_t rv, int b, int j, int g) {
+  int r_n = 0, s_n = 0;
+  f32x4 x_n[KQ], uv_n[KQ];
+  float ps_n[3] = {0.0f, 0.0f, 0.0f}, pr_n[3] = {0.0f, 0.0f, 0.0f};
+  const float* pos = a.pos_seq + (int64_t)(a.T - 1) * a.dim;
+  const int pstride = a.T * a.dim;
+  auto load_half = [&](int hs) {
+    const int e = hs + j;
+    const int ec = e < Et ? e : Et - 1;
+    r_n = lrecv[ec];
+    s_n = lsend[ec];
+    if constexpr (FIRST) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (c < a.dim) {
+          ps_n[c] = pos[(int64_t)s_n * pstride + c];
+          pr_n[c] = pos[(int64_t)r_n * pstride + c];
+        }
+    } else {
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) x_n[q] = ld4(e0l + ec * LDX + 16 * q + 4 * g);
+    }
+#pragma unroll
+    for (int t = 0; t < KQ; ++t)
+      uv_n[t] = ld4_sc1(ru, r_n * (H * 4) + (16 * t + 4 * g) * 4) + ld4_sc1(rv, s_n * (H * 4) + (16 * t + 4 * g) * 4);
+  };
+  if (16 * b < Et) load_half(16 * b);
+  for (int hs = 16 * b; hs < Et; hs += 16 * kWaves16) {
+    const bool ev = hs + j < Et;
+    const int r = r_n;
+    f32x4 x[KQ], acc[KQ];
+    float ps[3], pr[3];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      x[q] = x_n[q];
+      acc[q] = uv_n[q];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      ps[c] = ps_n[c];
+      pr[c] = pr_n[c];
+    }
+    if (hs + 16 * kWaves16 < Et) load_half(hs + 16 * kWaves16);
+    if constexpr (FIRST) {
+      // edge features (p_s - p_r) / R and their norm (learned_simulator.py:299-312)
+      float f[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ss = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (c < a.dim) {
+          const float dd = __fdiv_rn(__fsub_rn(ps[c], pr[c]), a.radius);
+          f[c] = dd;
+          ss = __fadd_rn(ss, __fmul_rn(dd, dd));
+        }
+      const float nrm = sqrtf(ss);
+      if (a.dim == 1) f[1] = nrm; else if (a.dim == 2) f[2] = nrm; else f[3] = nrm;
+      const float fg = g == 0 ? f[0] : g == 1 ? f[1] : g == 2 ? f[2] : f[3];
+      // Encoder.edge_fn: Linear(dim + 1, H) -> ReLU -> Linear(H, H) -> LayerNorm (graph_network.py:92-96)
+      f32x4 hx[KQ], y[KQ];
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) {
+        hx[t] = relu4(mfma16(xw1[t], fg, ld4(sxv + 16 * t + 4 * g)));
+        y[t] = ld4(sxv + H + 16 * t + 4 * g);
+      }
+      mm_full(y, sxw, hx, j, g);
+      float mu, rs;
+      ln_stats(y, mu, rs);
+      const int e = hs + j;
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) {
+        const f32x4 ga = ld4(sxv + 2 * H + 16 * t + 4 * g), be = ld4(sxv + 3 * H + 16 * t + 4 * g);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[t][c] = (y[t][c] - mu) * rs * ga[c] + be[c];
+        if (ev) st4(e0l + e * LDX + 16 * t + 4 * g, x[t]);  // e0 rows for the later layers
+      }
+    }
+    // first Linear: u[recv] + v[send] + 2^k W1_e e0 (graph_network.py:197 on cat[x_i, x_j, e])
+    mm_full(acc, sw0, x, j, g);
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) x[t] = relu4(acc[t]);
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) acc[t] = ld4(svec + 16 * t + 4 * g);
+    mm_full(acc, sw1, x, j, g);
+    float mu, rs;
+    ln_stats(acc, mu, rs);
+    f32x4 m[KQ];
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) {
+      const f32x4 ga = ld4(svec + H + 16 * t + 4 * g), be = ld4(svec + 2 * H + 16 * t + 4 * g);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) m[t][c] = (acc[t][c] - mu) * rs * ga[c] + be[c];
+    }
+    // receiver runs of the half (recv sorted along the 16-lane rows): segmented
+    // inclusive scan with DPP row shifts; the last lane of each run adds its
+    // total to the receiver's row of this wave's sums
+    const int rk = ev ? r : -1 - j;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const int prv = dpp_row_shr(rk, d, INT32_MIN);
+#pragma unroll
+      for (int t = 0; t < KQ; ++t)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float pv = __int_as_float(dpp_row_shr(__float_as_int(m[t][c]), d, 0));
+          m[t][c] = prv == rk ? m[t][c] + pv : m[t][c];
+        }
+    }
+    const int rn = dpp_row_shl1(rk, INT32_MIN);
+    if (ev && rn != rk) {
+      float* dst = sums + (r - i0) * LDX + 4 * g;
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) st4(dst + 16 * t, ld4(dst + 16 * t) + m[t]);
+    }
+  }
+}
+
+// Stage an edge MLP's LDS images: W1e (columns 2H..3H of W1, x scale) and W2 + vectors.
+struct EdgeStage {
+  f32x4 w1e[kStagePer], w2[kStagePer];
+  SGNN_DEV void load(const Lay16& L) {
+    stage_w64_load(w1e, L.ew1 + 2 * H, 3 * H);
+    stage_w64_load(w2, L.ew2, H);
+  }
+  SGNN_DEV void store(float* sw0, float* sw1, float* svec, const Lay16& L, float scale) const {
+    stage_w64_store(sw0, w1e, scale);
+    stage_w64_store(sw1, w2, 1.0f);
+    stage_vec(svec, L.eb2, H, H);
+    stage_vec(svec + H, L.eg, H, H);
+    stage_vec(svec + 2 * H, L.ebb, H, H);
+  }
+};
+
+// Layer k's weights by a constant index per case: indexing the kernel-argument
+// array with a runtime k would copy the whole argument block to scratch.
+SGNN_DEV Lay16 lay_at(const Step16Args& a, int k) {
+  switch (k) {
+    case 0: return a.lay[0];
+    case 1: return a.lay[1];
+    case 2: return a.lay[2];
+    case 3: return a.lay[3];
+    case 4: return a.lay[4];
+    case 5: return a.lay[5];
+    case 6: return a.lay[6];
+    case 7: return a.lay[7];
+    case 8: return a.lay[8];
+    default: return a.lay[9];
+  }
+}
+static_assert(sgnn::kStep16MaxL == 10, "lay_at covers every layer");
+
+SGNN_DEV Node16Args node_args(const Step16Args& a, const Lay16& L, const Lay16* next) {
+  Node16Args nd{};
+  nd.w1 = L.nw1; nd.b1 = L.nb1; nd.w2 = L.nw2; nd.b2 = L.nb2; nd.g = L.ng; nd.bb = L.nbb;
+  if (next) {
+    nd.we = next->ew1; nd.be = next->eb1;
+  } else {
+    nd.wd1 = a.d_w1; nd.bd1 = a.d_b1; nd.wd2 = a.d_w2; nd.bd2 = a.d_b2;
+  }
+  nd.dim = a.dim;
+  return nd;
+}
+
+// One interaction layer of the tile: wait for the sender tiles' u_k / v_k,
+// edge phase, receiver sums, node phase, publish u_{k+1} / v_{k+1}, stage the
+// next layer's edge weights.
+template <bool FIRST, int MODE, bool E0G>
+SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv, const float (&xw1)[KQ],
+                         const uint32_t* mask, const int32_t* lsend, const int32_t* lrecv, int Et, int i0, int cnt,
+                         int b, int j, int g, int l) {
+  const int tile = blockIdx.x, G = gridDim.x;
+  float* sw0 = lds + cv.sw0;
+  float* sw1 = lds + cv.sw1;
+  float* svec = lds + cv.svec;
+  float* scratch = lds + cv.scratch;
+  float* xs = lds + cv.xs;
+  const int64_t nH = (int64_t)a.n * H;
+  // e0 rows of the tile's edges: LDS, or (graphs whose tile does not fit) a per-tile HBM block behind
+  // the layers' node halves -- written and read by this workgroup only
+  float* e0l = E0G ? a.uvl + 2 * a.L * nH + (int64_t)tile * a.ecap_t * LDX : lds + cv.region;
+  const __amdgpu_buffer_rsrc_t ru = buf_rsrc(a.uvl + (2 * k) * nH), rv = buf_rsrc(a.uvl + (2 * k + 1) * nH);
+  // this layer's node weights (VGPR-resident) are requested before the wait
+  const Lay16 Lk = lay_at(a, k), Ln = lay_at(a, MODE == 0 ? k + 1 : k);
+  NodeW<2, MODE> W;
+  W.load(node_args(a, Lk, MODE == 0 ? &Ln : nullptr), b, j, g);
+  wait_tiles(mask, a.flags, G, a.epoch0 + (uint32_t)k + 1, b, l);
+  float* sums = scratch + b * 16 * LDX;
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) st4(sums + j * LDX + 16 * q + 4 * g, zero4());
+  step_edges<FIRST>(a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, xw1, sums, e0l, lsend, lrecv, Et, i0, ru, rv, b, j,
+                    g);
+  __syncthreads();
+  // the next layer's edge weights: requested now, stored once the node phase is done
+  EdgeStage nxt;
+  if (MODE == 0) nxt.load(Ln);
+  f32x4 ag[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    ag[q] = ld4(scratch + j * LDX + 16 * q + 4 * g);
+#pragma unroll
+    for (int w = 1; w < kWaves16; ++w) ag[q] += ld4(scratch + w * 16 * LDX + j * LDX + 16 * q + 4 * g);
+  }
+  f32x4 xr[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) xr[q] = ld4(xs + j * LDX + 16 * q + 4 * g);
+  const f32x4 xo = ld4(xs + j * LDX + 16 * b + 4 * g);
+  __syncthreads();  // the exchange buffers alias the sums
+  const bool valid = j < cnt;
+  const int64_t i = i0 + j;
+  const f32x4 h = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));  // graph_network.py:220
+  if constexpr (MODE == 0) {
+    const __amdgpu_buffer_rsrc_t ru1 = buf_rsrc(a.uvl + (2 * k + 2) * nH), rv1 = buf_rsrc(a.uvl + (2 * k + 3) * nH);
+    step_tail<0>(a, W, scratch, xs, i, valid, h, xo, b, j, g, ru1, rv1);
+    publish(a.flags, tile, a.epoch0 + (uint32_t)k + 2);
+    nxt.store(sw0, sw1, svec, Ln, (float)(2 << k));  // W1e x 2^(k+1): exact
+  } else {
+    step_tail<1>(a, W, scratch, xs, i, valid, h, xo, b, j, g, ru, rv);
+  }
+}
+
+template <int DIM, int KQF, bool E0G>
+__global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) void k_step16(Step16Args a_) {
+  // every access through the kernel-argument segment itself (scalar loads): binding a reference to
+  // the by-value parameter would copy its 1.3 KB to scratch first
+  (void)a_;
+  const Step16Args& a = *(const Step16Args*)(const __attribute__((address_space(4))) Step16Args*)
+                             __builtin_amdgcn_kernarg_segment_ptr();
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
+  const int tile = blockIdx.x, nt = a.nt, cap = a.cap, n = a.n;
+  const int i0 = tile * nt;
+  const int cnt = min(nt, n - i0);
+  const Carve cv = carve(n, DIM, nt, cap, E0G);
+  int32_t* ints = reinterpret_cast<int32_t*>(lds + cv.ints);
+  int32_t* lsend = ints;
+  int32_t* lrecv = lsend + nt * cap;
+  int32_t* nbr_l = lrecv + nt * cap;
+  int32_t* ldeg = nbr_l + nt * cap;
+  int32_t* lpre = ldeg + 16;
+  uint32_t* mask = reinterpret_cast<uint32_t*>(lpre + 20);
+  int32_t* kw_all = reinterpret_cast<int32_t*>(mask + 8);
+
+  // weights of layer 0's edge MLP and of Encoder.edge_fn, in flight during the radius search
+  EdgeStage st0;
+  st0.load(a.lay[0]);
+  f32x4 sx[kStagePer];
+  stage_w64_load(sx, a.xe_w2, H);
+  if (threadIdx.x < 8) mask[threadIdx.x] = 0u;
+
+  // ---- radius graph of the tile's receivers (torch_cluster's rule: first `cap` in-range senders of
+  // the receiver's example in ascending index, strict <; learned_simulator.py:116-117) --------------
+  float* sp = lds + cv.region;  // [DIM][n] SoA
+  for (int t = threadIdx.x; t < n * DIM; t += kBlock16) {
+    const int i = t / DIM, d = t - i * DIM;
+    sp[d * n + i] = a.pos_seq[((int64_t)i * a.T + a.T - 1) * DIM + d];
+  }
+  __syncthreads();
+  {
+    int32_t* kw = kw_all + b * 64;
+    for (int rl = b; rl < cnt; rl += kWaves16) {
+      const int i = i0 + rl;
+      int lo = 0, hi = a.n_ex - 1;  // example of i: largest e with ex_ptr[e] <= i
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.ex_ptr[mid] <= i) lo = mid; else hi = mid - 1;
+      }
+      const int jb = (int)a.ex_ptr[lo], je = (int)a.ex_ptr[lo + 1];
+      float pi[DIM];
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) pi[d] = sp[d * n + i];
+      int c = 0;
+      for (int base = jb; base < je && c < cap; base += 64) {
+        const int jj = base + l;
+        bool in = false;
+        if (jj < je) {
+          float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) {
+            const float t = __fsub_rn(sp[d * n + jj], pi[d]);
+            s = __fadd_rn(s, __fmul_rn(t, t));
+          }
+          in = s < a.r2;
+        }
+        const uint64_t bal = __ballot(in);
+        const int slot = c + (int)__popcll(bal & ((1ull << l) - 1ull));
+        if (in && slot < cap) kw[slot] = jj;
+        c += (int)__popcll(bal);
+      }
+      wave_lds_sync();
+      c = min(c, cap);
+      int top = l < c ? kw[l] : INT32_MAX;
+      if (!a.loop) {  // torch_cluster: K+1 first-by-index, then the self loop dropped
+        const uint64_t self = __ballot(l < c && top == i);
+        if (self) {
+          const int at = __ffsll((long long)self) - 1;
+          const int nx = __shfl(top, (l + 1) & 63, 64);
+          if (l >= at) top = (l + 1 < c) ? nx : INT32_MAX;
+          c -= 1;
+        }
+      }
+      if (l < c) nbr_l[rl * cap + l] = top;
+      if (l == 0) ldeg[rl] = c;
+      wave_lds_sync();
+    }
+  }
+  // LDS images of the staged weights (the radius phase never touches them)
+  st0.store(lds + cv.sw0, lds + cv.sw1, lds + cv.svec, a.lay[0], 1.0f);
+  stage_w64_store(lds + cv.sxw, sx, 1.0f);
+  stage_vec(lds + cv.sxv, a.xe_b1, H, H);
+  stage_vec(lds + cv.sxv + H, a.xe_b2, H, H);
+  stage_vec(lds + cv.sxv + 2 * H, a.xe_g, H, H);
+  stage_vec(lds + cv.sxv + 3 * H, a.xe_bb, H, H);
+  __syncthreads();
+  // tile CSR (receiver-sorted, senders ascending) from the kept lists; sender-tile mask
+  if (b == 0) {
+    const int dg = l < cnt ? ldeg[l] : 0;
+    int incl = dg;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (l >= o) incl += t;
+    }
+    if (l < 16) lpre[l + 1] = incl;
+    if (l == 0) lpre[0] = 0;
+    if (a.deg_out && l < cnt) a.deg_out[i0 + l] = dg;
+  }
+  __syncthreads();
+  const int Et = lpre[cnt];
+  for (int t = threadIdx.x; t < cnt * cap; t += kBlock16) {
+    const int k = t / cap, q = t - k * cap;
+    if (q < ldeg[k]) {
+      const int32_t sv = nbr_l[k * cap + q];
+      const int e = lpre[k] + q;
+      lsend[e] = sv;
+      lrecv[e] = i0 + k;
+      const int st = sv / nt;
+      atomicOr(&mask[st >> 5], 1u << (st & 31));
+      if (a.nbr_out) a.nbr_out[(int64_t)(i0 + k) * cap + q] = sv;
+    }
+  }
+
+  // ---- Encoder.node_fn of the tile's nodes (features: learned_simulator.py:256-290) -> x0 (LDS),
+  // u_0 / v_0 (published as phase 1) ------------------------------------------------------------
+  float xw1[KQ] = {0.0f, 0.0f, 0.0f, 0.0f};  // Encoder.edge_fn W1 [H][dim + 1]: unit 16 t + j, k = g
+#pragma unroll
+  for (int t = 0; t < KQ; ++t) xw1[t] = g <= DIM ? a.xe_w1[(16 * t + j) * (DIM + 1) + g] : 0.0f;
+  {
+    Node16Args nd{};
+    nd.w2 = a.xn_w2; nd.b2 = a.xn_b2; nd.g = a.xn_g; nd.bb = a.xn_bb;
+    nd.we = a.lay[0].ew1; nd.be = a.lay[0].eb1; nd.dim = DIM;
+    NodeW<2, 0> E;
+    E.load_tail(nd, b, j, g);
+    f32x4 w1f[KQF];
+    const int urow = 16 * b + j;
+#pragma unroll
+    for (int q = 0; q < KQF; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * q + 4 * g + c;
+        w1f[q][c] = f < a.feat ? a.xn_w1[(int64_t)urow * a.feat + f] : 0.0f;
+      }
+    const f32x4 vb1 = ld4(a.xn_b1 + 16 * b + 4 * g);
+    const int64_t i = i0 + j;
+    const bool valid = j < cnt;
+    const int64_t ic = valid ? i : (int64_t)i0;
+    const int nvel = (a.T - 1) * DIM;
+    const float* p = a.pos_seq + ic * a.T * DIM;
+    f32x4 xf[KQF];
+#pragma unroll
+    for (int q = 0; q < KQF; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * q + 4 * g + c;
+        float val = 0.0f;
+        if (f < nvel) {  // learned_simulator.py:258,272-278 normalised velocity history
+          const int t = f / DIM, cc = f - t * DIM;
+          const float vel = __fsub_rn(p[(t + 1) * DIM + cc], p[t * DIM + cc]);
+          val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[cc]), a.vel_std[cc]);
+        } else if (f == nvel) {  // :282-284 wall distance
+          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(p[(a.T - 1) * DIM], 2.0f), 0.0f), a.wall_max), a.wall_div);
+        } else if (a.use_emb && f < nvel + 1 + a.emb_dim) {  // :287-290 type embedding
+          val = a.emb_w[a.types[ic] * a.emb_dim + (f - nvel - 1)];
+        }
+        xf[q][c] = val;
+      }
+    const f32x4 h = relu4(mm(vb1, w1f, xf));
+    const int64_t nH = (int64_t)n * H;
+    step_tail<0>(a, E, lds + cv.scratch, lds + cv.xs, i, valid, h, zero4(), b, j, g, buf_rsrc(a.uvl),
+                 buf_rsrc(a.uvl + nH));
+    publish(a.flags, tile, a.epoch0 + 1);
+  }
+
+  // ---- the interaction layers ------------------------------------------------------------------
+  step_layer<true, 0, E0G>(a, 0, lds, cv, xw1, mask, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+  for (int k = 1; k < a.L - 1; ++k)
+    step_layer<false, 0, E0G>(a, k, lds, cv, xw1, mask, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+  step_layer<false, 1, E0G>(a, a.L - 1, lds, cv, xw1, mask, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+}
+
+}  // namespace
+
+namespace sgnn {
+
+size_t step16_lds_bytes(const Step16Args& a) {
+  if (a.nt < 1 || a.nt > kStep16MaxNT || a.cap < 1 || a.cap > kStep16MaxCap || a.dim < 1 || a.dim > 3) return 0;
+  return sizeof(float) * (size_t)carve(a.n, a.dim, a.nt, a.cap, a.e0_hbm != 0).total;
+}
+
+int step16_launch(const Step16Args& a, hipStream_t s) {
+  const size_t lds = step16_lds_bytes(a);
+  const int64_t grid = ((int64_t)a.n + a.nt - 1) / a.nt;
+  if (lds == 0 || lds > kStep16MaxLds || grid < 1 || grid > kStep16MaxGrid || a.L < 2 || a.L > kStep16MaxL ||
+      a.ecap_t != a.nt * a.cap)
+    return set_error(SGNN_ERR_UNSUPPORTED, "step16: shape outside the one-launch step");
+  const int kqf = (a.feat + 15) / 16;
+  if (kqf < 1 || kqf > 3) return set_error(SGNN_ERR_UNSUPPORTED, "step16: more than 48 node features");
+  // at least 81 KB: one workgroup per CU whatever the shape (the hand-off protocol's measured form)
+  const size_t lds_req = std::max<size_t>(lds, 81 * 1024);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kStep16MaxLds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock16), lds_req, s, a);
+  };
+#define SGNN_S16(D_, G_)                                \
+  do {                                                  \
+    if (kqf == 1) go(k_step16<D_, 1, G_>);              \
+    else if (kqf == 2) go(k_step16<D_, 2, G_>);         \
+    else go(k_step16<D_, 3, G_>);                       \
+  } while (0)
+  if (a.e0_hbm) {
+    if (a.dim == 1) SGNN_S16(1, true);
+    else if (a.dim == 2) SGNN_S16(2, true);
+    else SGNN_S16(3, true);
+  } else {
+    if (a.dim == 1) SGNN_S16(1, false);
+    else if (a.dim == 2) SGNN_S16(2, false);
+    else SGNN_S16(3, false);
+  }
+#undef SGNN_S16
+  return check_launch("step16");
+}
+
+}  // namespace sgnn

@@ -25,6 +25,8 @@ from ._hip import SgnnMlp, check, lib, stream_ptr
 
 MAX_NUM_NEIGHBORS = 20  # learned_simulator.py:117
 FUSED_MAX_N = 8192      # fused per-layer kernel for graphs up to this size (sgnn_predict_positions)
+STEP1_MAX_N = 4096      # one-launch step (sgnn_step_path) for graphs up to this size
+STEP1_MAX_L = 10
 
 
 def _ptr(t: Optional[torch.Tensor]) -> int:
@@ -90,7 +92,7 @@ class StepWorkspace:
     """HBM buffers for one (n, T, dim, H, K, loop) step shape."""
 
     def __init__(self, n: int, T: int, dim: int, hidden: int, K: int, loop: bool,
-                 device: torch.device):
+                 device: torch.device, nlayers: int = 0):
         L = lib()
         self.n, self.T, self.dim, self.H, self.K, self.loop = n, T, dim, hidden, K, loop
         cap = K + (0 if loop else 1)
@@ -116,20 +118,43 @@ class StepWorkspace:
         self.agg = torch.empty(n, hidden, **f32)
         self.cin = torch.empty(ntiles, hidden, **f32)
         self.cout = torch.empty(ntiles, hidden, **f32)
+        # one-launch step (sgnn_step_path decides; the C driver falls back to the kernel sequence):
+        # every layer's node halves, the per-workgroup phase counters, the neighbour counts
+        one = hidden == 64 and n <= STEP1_MAX_N and 2 <= nlayers <= STEP1_MAX_L
+        self.uvl = torch.empty(nlayers * 2 * n * hidden + (n + 16) * K * (hidden + 4), **f32) if one else None
+        self.step_flags = torch.zeros(512, **i32) if one else None
+        self.step_deg = torch.zeros(n, **i32) if one else None
         self.c = _hip.SgnnStepWs(radius_ws=self.radius_ws_ptr(), rowptr=self.rowptr.data_ptr(),
                                  send=self.send.data_ptr(), recv=self.recv.data_ptr(), edge_cap=self.edge_cap,
                                  e0t=self.e0t.data_ptr(), x_a=self.x_a.data_ptr(), x_b=self.x_b.data_ptr(),
                                  u=self.u.data_ptr(), v=self.v.data_ptr(), agg=self.agg.data_ptr(),
                                  cin=self.cin.data_ptr(), cout=self.cout.data_ptr(),
-                                 u2=_ptr(self.u2), v2=_ptr(self.v2))
+                                 u2=_ptr(self.u2), v2=_ptr(self.v2), uvl=_ptr(self.uvl),
+                                 step_flags=_ptr(self.step_flags), step_deg=_ptr(self.step_deg))
 
     def radius_ws_ptr(self) -> int:
         p = self.radius_ws.data_ptr()
         return (p + 255) & ~255
 
     def num_edges(self) -> int:
-        """E (host sync) — only for API/diagnostics, never inside a step."""
+        """E of the CSR the kernel sequence built (host sync) — API/diagnostics only."""
         return int(self.rowptr[self.n].item())
+
+    def step_edges(self) -> int:
+        """E of the last one-launch step (sum of its neighbour counts; host sync)."""
+        return int(self.step_deg.sum().item())
+
+    def step_timeout(self) -> bool:
+        """True if a workgroup of the one-launch step gave up waiting (its error word)."""
+        return self.step_flags is not None and int(self.step_flags[256].item()) != 0
+
+
+def step_path(epd_struct, sin, ws: StepWorkspace):
+    """(one_launch, nodes per workgroup, workgroups) of sgnn_predict_positions for these arguments."""
+    nt, grid = ctypes.c_int32(0), ctypes.c_int32(0)
+    one = lib().sgnn_step_path(ctypes.byref(epd_struct), ctypes.byref(sin), ctypes.byref(ws.c),
+                               ctypes.byref(nt), ctypes.byref(grid))
+    return bool(one), nt.value, grid.value
 
 
 def ex_ptr_tensor(counts: Sequence[int], device: torch.device) -> torch.Tensor:

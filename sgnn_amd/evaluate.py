@@ -52,7 +52,8 @@ def rollout(simulator, position: torch.Tensor, particle_types: torch.Tensor, n_p
     any_erosional = bool(erosional.any())
     start = time.time()
     fast = (inference_mode == "autoregressive" and not any_erosional and nsteps > 0
-            and hasattr(simulator, "rollout_runner") and position.is_cuda)
+            and hasattr(simulator, "rollout_runner") and position.is_cuda
+            and getattr(simulator, "_fast_path", lambda: True)())
     if fast:
         # device-resident loop: one sgnn_rollout call (window shift fused into the
         # decoder kernel; same kernels and arithmetic as predict_positions)

@@ -4,9 +4,10 @@ Mirrors sgnn/single_scale/graph_network.py (build_mlp :7-45, Encoder :48-111,
 InteractionNetwork :114-222, Processor :225-293, Decoder :296-333,
 EncodeProcessDecode :336-406) so that `state_dict()` keys, shapes and the
 default-initialisation RNG order are identical to the reference's — reference
-checkpoints load unchanged.  The arithmetic does NOT run through these
-modules: `sgnn_amd.engine` drives the HIP kernels in libsgnn_hip.so with
-their parameters.
+checkpoints load unchanged.  The arithmetic runs in libsgnn_hip.so: a
+whole EncodeProcessDecode (and LearnedSimulator's steps) through the fused
+MFMA kernels (`sgnn_amd.engine`), each module's own forward on explicit
+tensors through the width-generic kernels (`sgnn_amd.generic`).
 """
 from __future__ import annotations
 
@@ -40,6 +41,11 @@ class Encoder(nn.Module):
         self.node_fn = mlp_ln(nnode_in_features, mlp_hidden_dim, nnode_out_features, nmlp_layers)
         self.edge_fn = mlp_ln(nedge_in_features, mlp_hidden_dim, nedge_out_features, nmlp_layers)
 
+    def forward(self, x, edge_features):
+        """graph_network.py:98-111 -> (node latent, edge latent)."""
+        from . import generic
+        return generic.encoder_forward(self, x, edge_features)
+
 
 class InteractionNetwork(nn.Module):
     """graph_network.py:114-148 (node_fn built before edge_fn, as there)."""
@@ -48,6 +54,11 @@ class InteractionNetwork(nn.Module):
         super().__init__()
         self.node_fn = mlp_ln(nnode_in + nedge_out, mlp_hidden_dim, nnode_out, nmlp_layers)
         self.edge_fn = mlp_ln(nnode_in + nnode_in + nedge_in, mlp_hidden_dim, nedge_out, nmlp_layers)
+
+    def forward(self, x, edge_index, edge_features):
+        """graph_network.py:150-176 -> (x + node_fn([aggr, x]), e + e)."""
+        from . import generic
+        return generic.message_passing(self, x, edge_index, edge_features)
 
 
 class Processor(nn.Module):
@@ -60,6 +71,11 @@ class Processor(nn.Module):
             InteractionNetwork(nnode_in, nnode_out, nedge_in, nedge_out, nmlp_layers, mlp_hidden_dim)
             for _ in range(nmessage_passing_steps)])
 
+    def forward(self, x, edge_index, edge_features):
+        """graph_network.py:276-293"""
+        from . import generic
+        return generic.processor_forward(self, x, edge_index, edge_features)
+
 
 class Decoder(nn.Module):
     """graph_network.py:296-322 (no LayerNorm)."""
@@ -67,6 +83,11 @@ class Decoder(nn.Module):
     def __init__(self, nnode_in, nnode_out, nmlp_layers, mlp_hidden_dim):
         super().__init__()
         self.node_fn = build_mlp(nnode_in, [mlp_hidden_dim] * nmlp_layers, nnode_out)
+
+    def forward(self, x):
+        """graph_network.py:324-333"""
+        from . import generic
+        return generic.decoder_forward(self, x)
 
 
 class EncodeProcessDecode(nn.Module):
@@ -81,6 +102,7 @@ class EncodeProcessDecode(nn.Module):
                                     nmessage_passing_steps, nmlp_layers, mlp_hidden_dim)
         self._decoder = Decoder(latent_dim, nnode_out_features, nmlp_layers, mlp_hidden_dim)
         self.latent_dim = latent_dim
+        self.mlp_hidden_dim = mlp_hidden_dim
         self.nlayers = nmessage_passing_steps
         self.nmlp_layers = nmlp_layers
         self.nnode_in = nnode_in_features
@@ -88,6 +110,10 @@ class EncodeProcessDecode(nn.Module):
         self.nnode_out = nnode_out_features
 
     def forward(self, x, edge_index, edge_features):
-        """graph_network.py:388-406 on explicit features (HIP kernels)."""
-        from . import engine
-        return engine.epd_forward(self, x, edge_index, edge_features)
+        """graph_network.py:388-406 on explicit features: the fused MFMA chain
+        (engine.epd_forward) for the widths it is built for, else module by
+        module on the width-generic kernels."""
+        from . import engine, generic
+        if generic.fast_shapes(self):
+            return engine.epd_forward(self, x, edge_index, edge_features)
+        return generic.epd_forward(self, x, edge_index, edge_features)

@@ -11,7 +11,7 @@ from typing import Dict, Tuple
 import torch
 import torch.nn as nn
 
-from . import engine, graph_network, training
+from . import engine, generic, graph_network, training
 from ._hip import require_gpu_tensor
 
 
@@ -88,7 +88,8 @@ class LearnedSimulator(nn.Module):
                 self._ws_cache.clear()
             ws = engine.StepWorkspace(n, T, self._particle_dimensions,
                                       self._encode_process_decode.latent_dim,
-                                      self._max_num_neighbors, loop, device)
+                                      self._max_num_neighbors, loop, device,
+                                      nlayers=len(self._encode_process_decode._processor.gnn_stacks))
             self._ws_cache[key] = ws
         return ws
 
@@ -184,6 +185,9 @@ class LearnedSimulator(nn.Module):
         """learned_simulator.py:413-438 -> (next_positions [N,d], predicted_strain [N])."""
         inp, use_emb = self._step_inputs(current_positions, nparticles_per_example, particle_types)
         n, T, d = inp.pos_seq.shape
+        if not self._fast_path():   # widths the fused kernels are not built for
+            pred = generic.predict_step(self, inp, use_emb)
+            return self._decoder_postprocessor(pred[:, :d], inp.pos_seq), pred[:, -1]
         ws = self._workspace(n, T, inp.pos_seq.device)
         pred = torch.empty(n, d + 1, dtype=torch.float32, device=inp.pos_seq.device)
         next_pos = torch.empty(n, d, dtype=torch.float32, device=inp.pos_seq.device)
@@ -191,9 +195,16 @@ class LearnedSimulator(nn.Module):
                             self._connectivity_radius, inp, ws, pred, next_pos)
         return next_pos, pred[:, -1]
 
+    def _fast_path(self) -> bool:
+        """The fused MFMA kernels implement this model's widths (else generic.py)."""
+        return generic.fast_shapes(self._encode_process_decode)
+
     def rollout_runner(self, window: torch.Tensor, nparticles_per_example, particle_types, nsteps: int):
         """Device-resident autoregressive rollout of `nsteps` predict_positions
         steps from `window` (evaluate.py:117-145): one sgnn_rollout call."""
+        if not self._fast_path():
+            raise NotImplementedError("the device rollout needs the fused kernels' widths (hidden = latent "
+                                      "in {64, 128}); evaluate.rollout steps predict_positions instead")
         inp, use_emb = self._step_inputs(window, nparticles_per_example, particle_types)
         n, T, d = inp.pos_seq.shape
         ws = self._workspace(n, T, inp.pos_seq.device)
@@ -219,6 +230,8 @@ class LearnedSimulator(nn.Module):
             tw = self._train_workspace(n, T, inp.pos_seq.device)
             emb = self._particle_type_embedding.weight if use_emb else None
             pred = _TrainedEPD.apply(self, inp, tw, emb, *params)
+        elif not self._fast_path():
+            pred = generic.predict_step(self, inp, use_emb)
         else:
             ws = self._workspace(n, T, inp.pos_seq.device)
             pred = torch.empty(n, d + 1, dtype=torch.float32, device=inp.pos_seq.device)

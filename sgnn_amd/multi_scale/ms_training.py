@@ -34,8 +34,9 @@ KIND_SLOT = {"g2m": 0, "m2m": 1, "m2g": 2}
 
 def check_trainable(sim) -> None:
     gnn = sim._multi_scale_gnn
-    if gnn.latent_dim not in (64, 128):
-        raise NotImplementedError("HIP multi-scale training: latent_dim must be 64 or 128")
+    if gnn.latent_dim not in (64, 128) or gnn.nedge_out != gnn.latent_dim:
+        raise NotImplementedError("HIP multi-scale training: latent_dim = nedge_out in {64, 128} (other widths "
+                                  "run inference only, on the width-generic kernels)")
     if gnn.nmlp_layers not in (1, 2):
         raise NotImplementedError("HIP multi-scale training: nmlp_layers must be 1 or 2")
     if sim._nparticle_types > 32:
@@ -283,6 +284,7 @@ class MultiScaleTrainer:
             if len(self._tw) > 2:
                 self._tw.clear()
             tw = MSTrainWorkspace(self.gnn, n, T, self.sim._kinematic_dimensions, graphs, device, self.nslab)
+            tw.loss_out = self.flat.loss   # loss sums land in the gradient buffer's tail
             self._tw[key] = tw
         return tw
 
@@ -315,7 +317,7 @@ class MultiScaleTrainer:
                        noise=noise, next_strain=next_strain.to(torch.float32).contiguous(), w_pos=self.w_pos,
                        w_strain=self.w_strain, inv_count=1.0 / n_global, timers=timers, emb_weight=emb,
                        emb_grad=self.grads.get("_particle_type_embedding.weight"))
-        self.dp.allreduce_(self.flat.grad, tw.loss_out)
+        self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
         self.opt.step()
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6
         self.step += 1

@@ -6,7 +6,9 @@ unchanged; under one seed both draw identical weights).  The arithmetic of
 `MultiScaleGNN.forward` runs as the fused HIP chain in `ms_engine`
 (encoder -> G2M -> M2M x L -> M2G -> prediction head), driven by
 `MultiScaleSimulator`; `MultiScaleGNN.forward` on explicit features runs the
-same kernels (the individual block modules are not callable on their own).
+same kernels, and each block's own forward (and any width the fused kernels
+are not built for, e.g. nedge_out != latent_dim) runs on the width-generic
+kernels (`sgnn_amd.generic`).
 
 Semantics the kernels implement (what PyG executes for these blocks):
   message  m = LN(MLP_e([x_i, x_j, e]))   (multi_scale_gnn.py:96-101)
@@ -41,8 +43,9 @@ class _Block(nn.Module):
         self.edge_fn = _mlp_ln(nnode_in + nnode_in + nedge_in, latent_dim, nedge_out, nmlp_layers)
 
     def forward(self, x, edge_index, edge_features):
-        raise NotImplementedError("multi-scale blocks run fused inside MultiScaleSimulator "
-                                  "(predict_positions / predict_accelerations)")
+        """multi_scale_gnn.py:84-94 (and :132-142, :179-189) -> (x + node_fn([aggr, x]), e + e)."""
+        from .. import generic
+        return generic.message_passing(self, x, edge_index, edge_features)
 
 
 class G2MBlock(_Block):
@@ -88,8 +91,13 @@ class MultiScaleGNN(nn.Module):
 
     def forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index, m2m_edge_features,
                 m2g_edge_index, m2g_edge_features, graph_hierarchy=None):
-        """multi_scale_gnn.py:262-326 on explicit features (HIP kernels);
-        graph_hierarchy is unused, as in the reference."""
+        """multi_scale_gnn.py:262-326 on explicit features (HIP kernels: the fused
+        chain, or block by block on the width-generic kernels for widths it is
+        not built for); graph_hierarchy is unused, as in the reference."""
+        from .. import generic
         from . import ms_engine
-        return ms_engine.gnn_forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index,
-                                     m2m_edge_features, m2g_edge_index, m2g_edge_features)
+        if generic.ms_fast_shapes(self):
+            return ms_engine.gnn_forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index,
+                                         m2m_edge_features, m2g_edge_index, m2g_edge_features)
+        return generic.ms_gnn_forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index,
+                                      m2m_edge_features, m2g_edge_index, m2g_edge_features)

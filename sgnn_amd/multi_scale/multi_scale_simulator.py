@@ -14,7 +14,7 @@ from typing import Any, Dict, Optional, Tuple
 import torch
 import torch.nn as nn
 
-from .. import engine
+from .. import engine, generic
 from .._hip import require_gpu_tensor
 from . import ms_engine
 from .multi_scale_gnn import MultiScaleGNN
@@ -152,9 +152,6 @@ class MultiScaleSimulator(nn.Module):
         if d != self._kinematic_dimensions:
             raise ValueError(f"positions have dim {d}, simulator has {self._kinematic_dimensions}")
         gnn = self._multi_scale_gnn
-        if gnn.nedge_out != gnn.latent_dim:
-            raise NotImplementedError("libsgnn_hip needs nedge_out == latent_dim "
-                                      "(multi_scale_train.py:312-318 sets both to hidden_dim)")
         use_emb = self._nparticle_types > 1
         feat = (T - 1) * d + 1 + (self._particle_type_embedding.embedding_dim if use_emb else 0)
         if feat != gnn.nnode_in:
@@ -176,9 +173,20 @@ class MultiScaleSimulator(nn.Module):
             self._ws_cache[key] = ws
         return ws
 
+    def _fast_path(self) -> bool:
+        """The fused MFMA chain implements this model's widths (else generic.py)."""
+        return generic.ms_fast_shapes(self._multi_scale_gnn)
+
     def _run(self, position_sequence, particle_types, window_out=None):
         inp, use_emb = self._step_inputs(position_sequence, particle_types)
         n, T, d = inp.pos_seq.shape
+        if not self._fast_path():   # e.g. nedge_out != latent_dim: block by block, width-generic kernels
+            if window_out is not None:
+                raise NotImplementedError("window_out needs the fused chain")
+            nf, idx, ef = self._encoder_preprocessor(inp.pos_seq, None, particle_types)
+            pred = generic.ms_gnn_forward(self._multi_scale_gnn, nf, idx["g2m"], ef["g2m"], idx["m2m"], ef["m2m"],
+                                          idx["m2g"], ef["m2g"])
+            return inp, pred, self._decoder_postprocessor(pred[:, :d], inp.pos_seq)
         dev = inp.pos_seq.device
         graphs = self._csr(n, dev)
         ws = self._workspace(n, T, dev, graphs)
@@ -328,6 +336,15 @@ class _MSRollout:
         n, T, d = self.win[0].shape
         dev = self.win[0].device
         gnn = sim._multi_scale_gnn
+        if not sim._fast_path():   # widths the fused chain is not built for: step by step
+            cur = self.win[0]
+            for k in range(self.nsteps):
+                _, pred, nxt_pos = sim._run(cur, self.types)
+                self.out_pred[k].copy_(pred)
+                self.out_pos[k].copy_(nxt_pos)
+                src = nxt_pos if ground_truth is None else ground_truth[:, k]
+                cur = torch.cat([cur[:, 1:], src[:, None, :]], dim=1)
+            return self.out_pos[:self.nsteps], self.out_pred[:self.nsteps, :, -1]
         graphs = sim._csr(n, dev)
         ws = sim._workspace(n, T, dev, graphs)
         cur, nxt = self.win

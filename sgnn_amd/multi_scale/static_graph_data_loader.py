@@ -37,9 +37,23 @@ def build_static_multi_scale_graph(initial_positions: torch.Tensor, num_scales: 
     return _build_on_device(initial_positions.to(dev, torch.float32), num_scales, window_size, radius_multiplier)
 
 
+def _to_host(obj):
+    """Every tensor of a (nested) graph dict moved to host memory."""
+    if isinstance(obj, torch.Tensor):
+        return obj.cpu()
+    if isinstance(obj, dict):
+        return {k: _to_host(v) for k, v in obj.items()}
+    return obj
+
+
 def _graphs_for(trajectories, num_scales, window_size, radius_multiplier, device, graph_builder):
+    """One static graph per trajectory, built on the GPU and kept in HOST memory
+    as the reference's are (:100-118): the DataLoader may then pin the batch
+    (pin_memory=True, the reference's default) and fork workers; the simulator
+    moves the edges to its device once per graph (`set_static_graph` / `_csr`)."""
     build = graph_builder or functools.partial(build_static_multi_scale_graph, device=device)
-    return {i: build(torch.tensor(pos[0], dtype=torch.float32), num_scales, window_size, radius_multiplier)
+    return {i: _to_host(build(torch.tensor(pos[0], dtype=torch.float32), num_scales, window_size,
+                              radius_multiplier))
             for i, (pos, _, _) in enumerate(trajectories)}
 
 

@@ -64,6 +64,9 @@ class DataParallel:
         on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if on else 1
         self.rank = dist.get_rank(group) if on else 0
+        # gloo (CPU tests, or several ranks sharing one GPU) reduces host tensors: device buffers are
+        # staged through host memory; nccl (= RCCL on ROCm) reduces them in place over xGMI
+        self.host_staging = on and dist.get_backend(group) == "gloo"
 
     def layout(self, n_local: int, device) -> Tuple[int, int]:
         """(N_global, offset): the particle count over all ranks (the mean
@@ -73,7 +76,7 @@ class DataParallel:
         from step to step can never pair it with a different collective."""
         if self.world == 1:
             return int(n_local), 0
-        t = torch.tensor([int(n_local)], dtype=torch.int64, device=device)
+        t = torch.tensor([int(n_local)], dtype=torch.int64, device="cpu" if self.host_staging else device)
         out = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(out, t, group=self.group)
         counts = torch.cat(out).tolist()
@@ -87,7 +90,12 @@ class DataParallel:
         if self.world == 1:
             return
         for t in tensors:
-            dist.all_reduce(t, group=self.group)
+            if self.host_staging and t.is_cuda:
+                h = t.cpu()
+                dist.all_reduce(h, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, group=self.group)
 
 
 def split_batch(idx: Sequence[int], rank: int, world: int) -> Optional[List[int]]:
@@ -136,6 +144,7 @@ class Trainer:
                 self._tw.clear()
             tw = training.TrainWorkspace(self.epd, cap, T, self.sim._particle_dimensions,
                                          self.sim._max_num_neighbors, True, device, self.nslab)
+            tw.loss_out = self.flat.loss   # loss sums land in the gradient buffer's tail
             self._tw[key] = tw
         return tw.activate(n)
 
@@ -177,7 +186,7 @@ class Trainer:
                                 next_strain=next_strain.to(torch.float32).contiguous(),
                                 w_pos=self.w_pos, w_strain=self.w_strain, inv_count=1.0 / n_global,
                                 emb_weight=emb, emb_grad=self.grads.get("_particle_type_embedding.weight"))
-        self.dp.allreduce_(self.flat.grad, tw.loss_out)
+        self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
         self.opt.step()
         # train.py:276-278: LR for the NEXT step, computed from the pre-increment step
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6
@@ -281,8 +290,10 @@ def train(simulator, metadata: dict, device, config: dict, group=None, log_every
     Batches come from the split resident in device memory (data.DeviceSamples:
     the reference DataLoader's samples and order, sliced on the device).  With
     a process group of W ranks every global batch of `batch_size` windows is
-    split round-robin over the ranks (whole graphs per rank, one gradient
-    all-reduce per step) so the update equals the single-process one.
+    split into contiguous, balanced slices over the ranks (`split_batch`: whole
+    graphs per rank, rank order = the concatenated batch's order, one all-reduce
+    of gradient + loss sums per step) so the update equals the single-process
+    one.
     Validation every `nsave_steps` keeps only improving checkpoints
     (model-best-<step>.pt + train_state-best-<step>.pt); without any
     validation the final state is saved as model-final-<step>.pt.  Resumes from

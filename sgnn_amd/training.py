@@ -27,14 +27,19 @@ NODE_NSLAB = 256     # node-level backward kernels (128 measured slower: fewer C
 
 class FlatParams:
     """Point every parameter of `module` into one flat fp32 buffer, and its
-    `.grad` into one flat gradient buffer: one RCCL all-reduce, one Adam launch."""
+    `.grad` into one flat gradient buffer (+ the step's loss sums in its tail):
+    one RCCL all-reduce, one Adam launch."""
 
     def __init__(self, module: nn.Module):
         params = list(module.parameters())
         dev = params[0].device
         total = sum(p.numel() for p in params)
         self.param = torch.empty(total, dtype=torch.float32, device=dev)
-        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        # the flat gradient and an 8-float tail for the loss sums (the decoder's slab reduction writes
+        # them there): one buffer, so a data-parallel step is ONE all-reduce
+        self.comm = torch.zeros(total + 8, dtype=torch.float32, device=dev)
+        self.grad = self.comm[:total]
+        self.loss = self.comm[total:]
         self.offsets: Dict[int, Tuple[int, int]] = {}
         self.order = []   # (offset, numel, shape) in parameters() order
         off = 0
@@ -351,8 +356,9 @@ def _saves(h=None, yhat=None, rstd=None, agg=None, hd=None, h2=None, hd2=None) -
 
 
 def check_trainable(epd: nn.Module, nparticle_types: int) -> None:
-    if epd.latent_dim not in (64, 128):
-        raise NotImplementedError("HIP training path: latent_dim must be 64 or 128")
+    if epd.latent_dim not in (64, 128) or getattr(epd, "mlp_hidden_dim", epd.latent_dim) != epd.latent_dim:
+        raise NotImplementedError("HIP training path: latent_dim = mlp_hidden_dim in {64, 128} (other widths "
+                                  "run inference only, on the width-generic kernels)")
     if epd.nmlp_layers not in (1, 2):
         raise NotImplementedError("HIP training path: nmlp_layers must be 1 or 2")
     if nparticle_types > 32:

@@ -1,0 +1,95 @@
+"""Shared cases of the multi-rank GPU training test (tests/test_gpu_dp.py):
+whole-graph data parallelism of the HIP trainers with ragged, real-size
+graphs, run identically by the single-process reference run and by every
+rank (tests/gpu_dp_child.py).  Noise is drawn on the CPU from seeded
+generators, so every process sees the same windows."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+LR = 1e-3
+STEPS = 2
+# single scale: the real Taylor-bar sizes (120/160/200 x 40 lattices = 4,800 / 6,400 / 8,000 particles)
+SS_GRAPHS = [(120, 40), (160, 40), (200, 40)]
+SS_RANKS = [[0, 1], [2]]          # rank 0 holds two graphs (4,800 + 6,400), rank 1 one (8,000)
+# multi scale (nmlp_layers 2, two scales): one graph per rank, unequal sizes
+MS_GRAPHS = [(30, 14), (36, 12)]
+MS_RANKS = [[0], [1]]
+T_SS, T_MS = 11, 6
+
+
+def _stats(dim=2):
+    from sgnn_amd import synthetic
+    st = synthetic.normalization_stats(dim, noise_std=0.02)
+    return {k: {kk: torch.from_numpy(vv) for kk, vv in v.items()} for k, v in st.items()}
+
+
+def _window(nx, ny, T, seed, x0=0.25):
+    """(window [n,T,2], next position [n,2], next strain [n], noise [n,T,2]) on the CPU."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import synthetic
+    seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny, x0=x0), T + STEPS, seed=seed)
+    out = []
+    for s in range(STEPS):
+        pos = torch.from_numpy(np.ascontiguousarray(seq[:, s:s + T]))
+        nxt = torch.from_numpy(np.ascontiguousarray(seq[:, s + T]))
+        strain = torch.from_numpy(np.random.default_rng(seed + s).normal(0, 1, seq.shape[0]).astype(np.float32))
+        noise = O.random_walk_noise(pos, 0.02, generator=torch.Generator().manual_seed(seed * 7 + s))
+        out.append((pos, nxt, strain, noise))
+    return out
+
+
+def _cat(items):
+    return [torch.cat([it[k] for it in items], 0) for k in range(4)]
+
+
+def _result(tr, losses):
+    return {"loss": torch.tensor(losses, dtype=torch.float64), "grad": tr.flat.grad.detach().cpu().clone(),
+            "param": tr.flat.param.detach().cpu().clone()}
+
+
+def run_single_scale(graph_ids):
+    """STEPS Trainer steps on the concatenation of `graph_ids` (this process's
+    share of the global batch); DP bookkeeping from the default process group."""
+    from sgnn_amd.learned_simulator import LearnedSimulator
+    from sgnn_amd.train import Trainer
+    torch.manual_seed(7)
+    sim = LearnedSimulator(2, 21, 3, 64, 5, 1, 64, 0.6, _stats(), 1, 9).cuda()
+    tr = Trainer(sim, lr_init=LR)
+    wins = [_window(nx, ny, T_SS, 100 + g) for g, (nx, ny) in enumerate(SS_GRAPHS)]
+    losses = []
+    for s in range(STEPS):
+        parts = [wins[g][s] for g in graph_ids]
+        pos, nxt, strain, noise = _cat(parts)
+        counts = [p[0].shape[0] for p in parts]
+        out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), counts, noise=noise.cuda())
+        losses.append(float(out["loss"]))
+    torch.cuda.synchronize()
+    return _result(tr, losses)
+
+
+def run_multi_scale(graph_ids):
+    """STEPS MultiScaleTrainer steps on `graph_ids` (one static graph each,
+    merged block-diagonally when a process holds several)."""
+    from sgnn_amd.multi_scale import MultiScaleSimulator
+    from sgnn_amd.multi_scale.ms_training import MultiScaleTrainer
+    from sgnn_amd.multi_scale.multi_scale_graph import build_static_multi_scale_graph
+    from sgnn_amd.multi_scale.static_graph_data_loader import merge_static_graphs
+    torch.manual_seed(5)
+    sim = MultiScaleSimulator(2, (T_MS - 1) * 2 + 1, 3, 64, 64, 3, 2, _stats(), 1, 9, 2, 2, 2.0).cuda()
+    wins = [_window(nx, ny, T_MS, 300 + g, x0=-1.75) for g, (nx, ny) in enumerate(MS_GRAPHS)]
+    graphs = [build_static_multi_scale_graph(wins[g][0][0][:, 0].cuda(), 2, 2, 2.0) for g in graph_ids]
+    counts = [wins[g][0][0].shape[0] for g in graph_ids]
+    sim.set_static_graph(graphs[0] if len(graphs) == 1 else merge_static_graphs(graphs, counts))
+    tr = MultiScaleTrainer(sim, lr_init=LR)
+    losses = []
+    for s in range(STEPS):
+        pos, nxt, strain, noise = _cat([wins[g][s] for g in graph_ids])
+        out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), noise=noise.cuda())
+        losses.append(float(out["loss"]))
+    torch.cuda.synchronize()
+    return _result(tr, losses)
+
+
+CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, MS_GRAPHS, MS_RANKS)}

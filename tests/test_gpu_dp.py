@@ -1,0 +1,66 @@
+"""The multi-rank HIP training path on hardware:
+two fresh child processes on the one leased GPU, joined by a gloo group,
+each run Trainer.train_step (single scale) / MultiScaleTrainer.train_step on
+its own ragged share of a global batch -- 4,800 + 6,400 particles on rank 0,
+8,000 on rank 1 -- for two steps: the noise offset, the 1/N_global loss
+scaling, the one all-reduce of gradient + loss sums, and the fused Adam after
+it.  Every rank must end with the loss, gradient and Adam-updated weights of
+ONE process running the concatenated batch (train.py:268 averages over the
+whole batch).  Tolerances: loss 1e-5 relative; gradients 2e-5 of the largest
+(the ranks' partial sums are added in another order, fp32); weights 2e-6
+absolute where |g| > 1e-6 max|g| (Adam's first steps are lr sign(g)-like:
+only near-zero gradients can flip a step of 1e-3)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("case", ["ss", "ms"])
+def test_two_ranks_match_one_process(case, tmp_path):
+    from tests.dp_cases import CASES, LR
+    run, _, ranks = CASES[case]
+    world, port = len(ranks), str(_free_port())
+    outs = [str(tmp_path / f"rank{r}.pt") for r in range(world)]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_dp_child.py"), case, str(r),
+                               str(world), port, outs[r]], cwd=ROOT, env=env) for r in range(world)]
+    try:
+        codes = [p.wait(timeout=100) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert codes == [0] * world, codes
+    ref = run(sum(ranks, []))
+    gmax = float(ref["grad"].abs().max())
+    for r, path in enumerate(outs):
+        got = torch.load(path, weights_only=True)
+        rel = np.abs(got["loss"].numpy() - ref["loss"].numpy()) / np.abs(ref["loss"].numpy())
+        print(f"{case} rank {r}: loss {got['loss'].tolist()} vs {ref['loss'].tolist()} (rel {rel.max():.2e})")
+        assert rel.max() <= 1e-5
+        dg = (got["grad"] - ref["grad"]).abs()
+        print(f"{case} rank {r}: max|dgrad| {float(dg.max()):.3e} of max|g| {gmax:.3e}")
+        assert float(dg.max()) <= 2e-5 * gmax
+        dw = (got["param"] - ref["param"]).abs().numpy()
+        loose = (ref["grad"].abs() <= 1e-6 * gmax).numpy()
+        assert (dw[~loose] <= 2e-6).all(), float(dw[~loose].max())
+        assert (dw[loose] <= 2 * 2 * LR + 1e-6).all()
+    g0, g1 = (torch.load(p, weights_only=True) for p in outs)
+    assert torch.equal(g0["grad"], g1["grad"]) and torch.equal(g0["param"], g1["param"])

@@ -193,3 +193,39 @@ def test_batched_static_graphs_per_sample(tmp_path):
     np.testing.assert_allclose(nxt.cpu().numpy(), torch.cat([o[0] for o in outs]).cpu().numpy(), rtol=0, atol=1e-5)
     np.testing.assert_allclose(strain.cpu().numpy(), torch.cat([o[1] for o in outs]).cpu().numpy(), rtol=0,
                                atol=2e-4)
+
+
+def test_multi_scale_loaders_default_arguments(tmp_path):
+    """Both multi-scale loaders with their default arguments (GPU graph builder,
+    pin_memory=True as in the reference): the static graphs live in host memory,
+    so the DataLoader can pin every batch; a batch drives the simulator."""
+    import json
+    from sgnn_amd import data as D
+    from sgnn_amd import synthetic
+    from sgnn_amd.multi_scale import MultiScaleSimulator
+    from sgnn_amd.multi_scale import static_graph_data_loader as S
+    trajs = {}
+    for k, (nx, ny) in enumerate([(16, 10), (18, 8)]):
+        seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny, x0=-1.75), 9, seed=50 + k)
+        pos = np.transpose(seq, (1, 0, 2)).copy()
+        trajs[f"t{k}"] = (pos, np.zeros(pos.shape[1], np.int64), np.zeros(pos.shape[:2]))
+    path = str(tmp_path / "train.npz")
+    D.save_trajectories(path, trajs, reference_format=True)
+    (tmp_path / "metadata.json").write_text(json.dumps({"stress_mean": 0.0, "stress_std": 1.0}))
+    batches = list(S.get_multi_scale_data_loader_by_samples(path, input_length_sequence=6, batch_size=1,
+                                                            num_scales=2, window_size=2))
+    trajectories = list(S.get_multi_scale_data_loader_by_trajectories(path, num_scales=2, window_size=2))
+    assert len(batches) == sum(t[0].shape[0] - 6 for t in trajs.values())
+    assert len(trajectories) == 2
+    for b in batches[:2] + trajectories:
+        assert all(not v.is_cuda for v in (b["graph"]["grid2mesh_edges"], b["graph"]["mesh2mesh_edges"]))
+    st = synthetic.normalization_stats(2, noise_std=0.02)
+    stats = {k: {kk: torch.from_numpy(vv) for kk, vv in v.items()} for k, v in st.items()}
+    torch.manual_seed(6)
+    sim = MultiScaleSimulator(2, 11, 3, 64, 64, 3, 2, stats, 1, 9, 2, 2, 2.0).cuda()
+    b = batches[0]
+    sim.set_static_graph(b["graph"])
+    p = b["input"]["positions"].cuda()
+    nxt, strain = sim.predict_positions(p, b["input"]["n_particles_per_example"].tolist(), None)
+    torch.cuda.synchronize()
+    assert torch.isfinite(nxt).all() and torch.isfinite(strain).all()

@@ -1,0 +1,124 @@
+"""The one-launch step (step16.hip: radius graph, encoders, every layer,
+decoder and integrator in ONE kernel, tiles handing node halves to each other
+through per-tile phase counters) against the reference's golden outputs, the
+oracle, and the per-kernel sequence it replaces.  Tolerances as in
+test_gpu_parity.py (fp32; |got - ref| <= ATOL + RTOL |ref| on the normalised
+decoder output, x acc_std on positions)."""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import golden, hparams, oracle_sim, product_sim, state_of, stats_of
+from tests.test_gpu_parity import ATOL, FWD_H64, _close
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(sim, pos, counts, types_, one_launch):
+    """predict_positions with the one-launch step enabled or not (a workspace
+    without its buffers makes the driver take the per-kernel sequence)."""
+    from sgnn_amd import engine
+    inp, use_emb = sim._step_inputs(pos, counts, types_)
+    n, T, d = inp.pos_seq.shape
+    ws = sim._workspace(n, T, pos.device)
+    if not one_launch:
+        ws = engine.StepWorkspace(n, T, d, 64, sim._max_num_neighbors, True, pos.device, nlayers=0)
+    pk = engine.ParamPack.get(sim._encode_process_decode)
+    sin = engine.step_in(inp, ws, sim._connectivity_radius, sim._particle_type_embedding.weight, use_emb)
+    path = engine.step_path(pk.epd, sin, ws)
+    pred = torch.empty(n, d + 1, device=pos.device)
+    nxt = torch.empty(n, d, device=pos.device)
+    engine.forward_step(sim._encode_process_decode, sim._particle_type_embedding.weight, use_emb,
+                        sim._connectivity_radius, inp, ws, pred, nxt)
+    torch.cuda.synchronize()
+    return pred, nxt, ws, path
+
+
+@pytest.mark.parametrize("case", FWD_H64)
+def test_one_launch_matches_golden_and_kernel_sequence(case):
+    z = golden(case)
+    hp = hparams(z)
+    sim = product_sim(z)
+    pos = torch.from_numpy(z["positions"][:, :hp["T"]]).cuda()
+    types_ = torch.from_numpy(z["particle_types"]).cuda()
+    counts = z["nparticles_per_example"]
+    pred1, nxt1, ws1, path = _run(sim, pos, counts, types_, True)
+    assert path[0], f"{case}: expected the one-launch step, got {path}"
+    assert not ws1.step_timeout()
+    pred0, nxt0, ws0, path0 = _run(sim, pos, counts, types_, False)
+    assert not path0[0]
+    # the same graph (neighbour counts) and the same arithmetic in the same order
+    assert ws1.step_edges() == ws0.num_edges() == z["edge_index"].shape[1]
+    np.testing.assert_array_equal(pred1.cpu().numpy(), pred0.cpu().numpy())
+    np.testing.assert_array_equal(nxt1.cpu().numpy(), nxt0.cpu().numpy())
+    _close(pred1[:, -1].cpu().numpy(), z["strain"], what=f"{case} strain")
+    scale = float(np.max(z["acc_std"]))
+    _close(nxt1.cpu().numpy(), z["next_position"], atol=ATOL * scale, rtol=1e-6, what=f"{case} next_pos")
+
+
+@pytest.mark.parametrize("dim,dims,radius,n_ex,ntypes,K", [
+    (2, (30, 20), 15.0, 3, 3, 20),     # 1,800 particles in 3 examples, cap binds, type embeddings
+    (3, (12, 10, 8), 0.75, 1, 1, 20),  # 3D
+    (2, (64, 64), 0.6, 1, 1, 20),      # 4,096 particles: 16 receivers per workgroup, 256 workgroups
+    (2, (9, 7), 2.0, 2, 1, 33),        # tiny grid (16 workgroups); cap 33 = torch_cluster's default
+])
+def test_one_launch_against_oracle(dim, dims, radius, n_ex, ntypes, K):
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import synthetic
+    from sgnn_amd.learned_simulator import LearnedSimulator
+    lat = synthetic.lattice_2d if dim == 2 else synthetic.lattice_3d
+    seqs = [synthetic.trajectory(lat(*dims), 11, seed=60 + k) for k in range(n_ex)]
+    for k, sq in enumerate(seqs):
+        sq[..., 0] += 0.17 * k
+    seq = np.concatenate(seqs, 0)
+    counts = [s.shape[0] for s in seqs]
+    n = seq.shape[0]
+    st = synthetic.normalization_stats(dim, noise_std=0.02)
+    stats = {k: {kk: torch.from_numpy(vv) for kk, vv in v.items()} for k, v in st.items()}
+    torch.manual_seed(11)
+    emb = 16 if ntypes > 1 else 0
+    sim = LearnedSimulator(dim, 10 * dim + 1 + emb, dim + 1, 64, 5, 1, 64, radius, stats, ntypes, emb or 9)
+    sim._max_num_neighbors = K
+    state = {k: v.detach().clone() for k, v in sim.state_dict().items()}
+    types_ = torch.from_numpy(np.random.default_rng(2).integers(0, ntypes, n))
+    pos = torch.from_numpy(seq)
+    osim = O.OracleSimulator(state, dim, 5, radius, stats, ntypes)
+    osim.max_num_neighbors = K
+    ref_next, ref_strain = osim.predict_positions(pos, counts, types_)
+    sim = sim.cuda()
+    pred, nxt, ws, path = _run(sim, pos.cuda(), counts, types_.cuda(), True)
+    assert path[0], path
+    assert not ws.step_timeout()
+    ref_e = O.radius_graph(pos[:, -1], counts, radius, max_num_neighbors=K).shape[1]
+    assert ws.step_edges() == ref_e
+    _close(pred[:, -1].cpu().numpy(), ref_strain.numpy(), what=f"n={n} dim={dim} strain")
+    scale = float(np.max(st["acceleration"]["std"]))
+    _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * scale, rtol=1e-6, what=f"n={n} next_pos")
+
+
+def test_headline_rollout_20_steps_against_oracle():
+    """The headline's timed path itself: 20 autoregressive sgnn_rollout steps
+    at C1 r = 15 (2,000 particles, the cap of 20 binds) vs the oracle's
+    rollout (evaluate.py:117-145)."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import engine, synthetic
+    z = golden("c1_r15")
+    hp = hparams(z)
+    T, nsteps = hp["T"], 20
+    seq = synthetic.trajectory(synthetic.lattice_2d(50, 40), T + nsteps, seed=1000)
+    n = seq.shape[0]
+    sim = product_sim(z)
+    types_ = torch.zeros(n, dtype=torch.long, device="cuda")
+    win = torch.from_numpy(seq[:, :T]).cuda()
+    runner = sim.rollout_runner(win, [n], types_, nsteps)
+    pk = engine.ParamPack.get(sim._encode_process_decode)
+    assert engine.step_path(pk.epd, runner.sin, runner.ws)[0]
+    pos, strain = runner.run()
+    torch.cuda.synchronize()
+    assert not runner.ws.step_timeout()
+    ref_pos, ref_str = O.rollout(oracle_sim(z), torch.from_numpy(seq), torch.zeros(n, dtype=torch.long), n,
+                                 nsteps, T)
+    scale = float(np.max(z["acc_std"]))
+    _close(pos.cpu().numpy(), ref_pos.numpy(), atol=2 * nsteps * ATOL * scale, rtol=1e-6,
+           what="C1 r=15 20-step rollout positions")
+    _close(strain.cpu().numpy(), ref_str.numpy(), atol=2 * nsteps * ATOL, what="C1 r=15 20-step rollout strain")
