@@ -183,45 +183,78 @@ def cpu_model():
     return platform.processor() or platform.machine()
 
 
-def cpu_threads() -> dict:
-    """Threads for the CPU baseline: every core this process may run on
-    (sched_getaffinity), capped by OMP_NUM_THREADS when the environment sets
-    it (on the GPU box it is the box's CPU share, while os.cpu_count() shows
-    the whole host).  Reported with the raw counts."""
+def cpu_threads(n=None) -> dict:
+    """Threads for a CPU baseline leg: `n`, or every core this process may run
+    on (sched_getaffinity -- BASELINE.md §3's os.cpu_count() restricted to what
+    the process may use) capped by OMP_NUM_THREADS when the environment sets it
+    (on the GPU box that is the box's CPU share, while os.cpu_count() shows the
+    whole host).  Reported with the raw counts."""
     aff = len(os.sched_getaffinity(0))
     omp = os.environ.get("OMP_NUM_THREADS")
-    n = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    if n is None:
+        n = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
     torch.set_num_threads(n)
     return {"cores": torch.get_num_threads(), "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
             "omp_num_threads": omp, "cpu_model": cpu_model(), "kind": "port"}
 
 
+def thread_counts():
+    """The CPU-leg thread counts to try: the box's share (OMP_NUM_THREADS) and
+    every CPU of the affinity mask, when they differ."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return sorted({share, aff})
+
+
 def profiled(workload, mode, kernel):
-    """Per-launch HBM bytes and duration of `kernel` (all its template
-    variants, weighted by launches) from the newest committed rocprofv3
-    summary (profiles/r*_summary.json: FETCH_SIZE x2 + WRITE_SIZE)."""
+    """Per-launch HBM bytes and duration of `kernel` from the newest committed
+    rocprofv3 summary (profiles/r*_summary.json: FETCH_SIZE x2 + WRITE_SIZE).
+    `kernel` is a name (all its template variants, weighted by launches) or a
+    composite "a + 3 b<..>" (one launch of a plus three of b<..>, exact names:
+    a timed region that issues several kernels)."""
+    parts = []
+    for term in kernel.split(" + "):
+        mult, _, name = term.partition(" ") if term.split(" ")[0].isdigit() else ("1", "", term)
+        parts.append((int(mult), name.strip()))
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
         d = json.load(open(path))
         if d.get("workload") != workload or d.get("mode", "rollout") != mode:
             continue
-        ks = [v for k, v in d["kernels"].items() if k.split("<")[0] == kernel and "hbm_bytes" in v]
-        if ks:
+        tot_b = tot_us = 0.0
+        ok = True
+        for mult, name in parts:
+            exact = "<" in name or len(parts) > 1
+            ks = [v for k, v in d["kernels"].items()
+                  if (k == name if exact else k.split("<")[0] == name) and "hbm_bytes" in v]
+            if not ks:
+                ok = False
+                break
             calls = sum(v["calls"] for v in ks)
-            best = {"bytes": sum(v["hbm_bytes"] * v["calls"] for v in ks) / calls,
-                    "avg_us": sum(v["avg_us"] * v["calls"] for v in ks) / calls,
-                    "source": os.path.relpath(path, ROOT)}
+            tot_b += mult * sum(v["hbm_bytes"] * v["calls"] for v in ks) / calls
+            tot_us += mult * sum(v["avg_us"] * v["calls"] for v in ks) / calls
+        if ok:
+            best = {"bytes": tot_b, "avg_us": tot_us, "source": os.path.relpath(path, ROOT)}
     return best
 
 
-def roofline(kernel, flops, avg_s, workload, mode, alg_bytes=None):
+def roofline(kernel, flops, avg_s, workload, mode, alg_bytes=None, executed_flops=None):
+    """`achieved` / `frac`: ALGORITHMIC FLOPs per launch (SURVEY.md §8(d)'s
+    count, as BASELINE.md §3 asks) / the live average launch time, against the
+    dense fp32 MFMA peak; `executed_frac` the same for the FLOPs the kernel
+    actually multiplies (the u/v factorisation removes 2H^2 of every edge's
+    first Linear); `traffic` per launch from this round's rocprofv3 passes."""
     prof = profiled(workload, mode, kernel)
     r = {"bound": "mfma", "kernel": kernel, "achieved": flops / avg_s / 1e12, "peak": MFMA_F32_PEAK / 1e12,
          "unit": "TFLOP/s", "frac": flops / avg_s / MFMA_F32_PEAK,
          "traffic": prof["bytes"] if prof else None,
          "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
          "traffic_source": prof["source"] if prof else None,
-         "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops}
+         "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops, "flops_count": "SURVEY.md §8(d) algorithmic"}
+    if executed_flops is not None:
+        r["executed_flops_per_launch"] = executed_flops
+        r["executed_frac"] = executed_flops / avg_s / MFMA_F32_PEAK
     if prof:
         r["hbm_frac"] = prof["bytes"] / avg_s / HBM_PEAK          # achieved HBM fraction (live duration)
         r["profiled_avg_us"] = prof["avg_us"]
@@ -261,9 +294,10 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload, min_seconds=0.
     """Oracle (test infrastructure: CPU restatement of the reference) rollout:
     one warm-up step, then at least `steps` timed autoregressive steps, more
     until `min_seconds` of CPU work (at most 20x steps) -- graph build +
-    features + EPD + integration all inside the timed region."""
+    features + EPD + integration all inside the timed region.  Run at every
+    thread count of thread_counts(); `value` is the fastest leg (the baseline
+    most favourable to the CPU), every leg is listed."""
     from oracle import sgnn_oracle as O
-    info = cpu_threads()
     state = {k: v.detach().cpu() for k, v in sim.state_dict().items()}
     sample = ""
     if workload in CPU_SAMPLE_DIMS:
@@ -271,35 +305,56 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload, min_seconds=0.
         sample = (f" (a {'x'.join(map(str, CPU_SAMPLE_DIMS[workload]))} sample of the same lattice, "
                   f"spacing, radius and model: per-particle rate, not the full config size)")
     osim = O.OracleSimulator(state, window.shape[2], L, radius, sim._normalization_stats)
-    cur, n = window.cpu(), window.shape[0]
+    n = window.shape[0]
     types_ = torch.zeros(n, dtype=torch.long)
-    edges = 0
-    with torch.no_grad():
-        nxt, _ = osim.predict_positions(cur, [n], types_)
-        cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
-        t0 = time.perf_counter()
-        done = 0
-        while done < steps or (time.perf_counter() - t0 < min_seconds and done < 20 * steps):
+    legs = []
+    for nthreads in thread_counts():
+        info = cpu_threads(nthreads)
+        cur = window.cpu()
+        with torch.no_grad():
             nxt, _ = osim.predict_positions(cur, [n], types_)
             cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
-            done += 1
-        dt = time.perf_counter() - t0
-        steps = done
-        edges = int(O.radius_graph(cur[:, -1], [n], radius)[0].shape[0])
-    return {"value": n * steps / dt, "unit": "particle-steps/s", **info, "seconds": dt,
-            "M_edge_messages_per_s": edges * L * steps / dt / 1e6,
-            "sample": f"{steps} autoregressive oracle rollout steps after 1 warm-up (torch CPU fp32 "
-                      f"restatement of the reference ops + C cell-list radius search), {n} particles{sample}"}
+            t0 = time.perf_counter()
+            done = 0
+            while done < steps or (time.perf_counter() - t0 < min_seconds and done < 20 * steps):
+                nxt, _ = osim.predict_positions(cur, [n], types_)
+                cur = torch.cat([cur[:, 1:], nxt[:, None]], 1)
+                done += 1
+            dt = time.perf_counter() - t0
+            edges = int(O.radius_graph(cur[:, -1], [n], radius)[0].shape[0])
+        legs.append({"value": n * done / dt, "unit": "particle-steps/s", **info, "seconds": dt, "steps": done,
+                     "M_edge_messages_per_s": edges * L * done / dt / 1e6})
+    cpu_threads()
+    best = max(legs, key=lambda r: r["value"])
+    return {**best, "legs": [{k: r[k] for k in ("cores", "value", "steps", "seconds")} for r in legs],
+            "sample": f"{best['steps']} autoregressive oracle rollout steps after 1 warm-up (torch CPU fp32 "
+                      f"restatement of the reference ops + C cell-list radius search), {n} particles{sample}; "
+                      f"fastest of the thread counts tried (legs)"}
+
+
+def step_flops(n, E, H, L, dim, feat):
+    """(algorithmic, executed) FLOPs of one predict_positions step.
+    Algorithmic = SURVEY.md §8(d) (2 in out per Linear row, first edge Linear
+    3H x H): n (2 F_n H + 2H^2 + L 6H^2 + 2H^2 + 2H(d+1)) + E (2 F_e H + 2H^2 + L 8H^2).
+    Executed = what the kernels multiply after the u/v factorisation (first
+    edge Linear H x H per edge, u = W1_i x and v = W1_j x once per node)."""
+    fe = dim + 1
+    alg = n * (2 * feat * H + 2 * H * H + L * 6 * H * H + 2 * H * H + 2 * H * (dim + 1)) + \
+        E * (2 * fe * H + 2 * H * H + L * 8 * H * H)
+    exe = n * (2 * feat * H + 2 * H * H + 4 * H * H + (L - 1) * 10 * H * H + 6 * H * H + 2 * H * H + 2 * H * (dim + 1)) + \
+        E * (2 * fe * H + 2 * H * H + L * 4 * H * H)
+    return alg, exe
 
 
 def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps, cpu_seconds=0.0):
     """Timed region: `steps` autoregressive steps issued as ONE sgnn_rollout
     call (evaluate.rollout's device path: the C driver launches every kernel of
     every step; no host round trip).  Warm-up: full untimed rollouts.  The
-    edge-layer launch time comes from a second, event-timed pass."""
+    dominant kernel's launch time comes from a second, event-timed pass."""
     from sgnn_amd import engine
     dims, radius, H, L = WORKLOADS[workload]
     dim = len(dims)
+    feat = (T_SEQ - 1) * dim + 1
     sim = quiet_decoder(make_sim(H, L, radius, dim, device, seed))
     seq = synthetic.trajectory(lattice(dims), T_SEQ, seed=1000 + rank)
     n = seq.shape[0]
@@ -308,6 +363,7 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps,
     with torch.no_grad():
         w0 = window0.to(device)
         runner = sim.rollout_runner(w0, [n], types_, steps)
+        one_launch, nt, grid = engine.step_path(runner.epd, runner.sin, runner.ws)
         for _ in range(max(1, -(-warmup // max(steps, 1)))):
             runner.run(w0)
         sync_barrier(world)
@@ -315,41 +371,62 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps,
         runner.run(w0)
         sync_barrier(world)
         dt = time.perf_counter() - t0
-        # event-timed pass (same kernels, launched from Python per step)
-        inp, use_emb = sim._step_inputs(w0, [n], types_)
-        ws = sim._workspace(n, T_SEQ, device)
-        win = [inp.pos_seq.clone(), torch.empty_like(inp.pos_seq)]
-        pred = torch.empty(n, dim + 1, device=device)
-        nxt = torch.empty(n, dim, device=device)
-        timers = []
-        edges = []
-        for k in range(steps):
-            inp.pos_seq = win[k % 2]
-            # a spin kernel ahead of the step lets the host queue all of the step's launches and events
-            # before the GPU reaches them, so no host gap lands inside an event pair
+        if one_launch:
+            # the whole step is ONE k_step16 launch: one event pair on the launch stream around the
+            # `steps` back-to-back launches of a rollout call (a spin kernel first, so the host has
+            # queued them all before the GPU reaches them); per launch = elapsed / steps
             torch.cuda._sleep(2_000_000)
-            engine.forward_step(sim._encode_process_decode, sim._particle_type_embedding.weight, use_emb,
-                                radius, inp, ws, pred, nxt, window_out=win[(k + 1) % 2], timers=timers)
-            edges.append(ws.num_edges())
-        torch.cuda.synchronize()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            runner.run(w0)
+            ev1.record()
+            torch.cuda.synchronize()
+            kernel_s = ev0.elapsed_time(ev1) * 1e-3 / steps
+            edges = [runner.ws.step_edges()]
+            if runner.ws.step_timeout():
+                raise RuntimeError("k_step16: a workgroup timed out waiting for its sender tiles")
+        else:
+            # event-timed pass (same kernels, launched from Python per step)
+            inp, use_emb = sim._step_inputs(w0, [n], types_)
+            ws = sim._workspace(n, T_SEQ, device)
+            win = [inp.pos_seq.clone(), torch.empty_like(inp.pos_seq)]
+            pred = torch.empty(n, dim + 1, device=device)
+            nxt = torch.empty(n, dim, device=device)
+            timers = []
+            edges = []
+            for k in range(steps):
+                inp.pos_seq = win[k % 2]
+                # a spin kernel ahead of the step lets the host queue all of the step's launches and events
+                # before the GPU reaches them, so no host gap lands inside an event pair
+                torch.cuda._sleep(2_000_000)
+                engine.forward_step(sim._encode_process_decode, sim._particle_type_embedding.weight, use_emb,
+                                    radius, inp, ws, pred, nxt, window_out=win[(k + 1) % 2], timers=timers)
+                edges.append(ws.num_edges())
+            torch.cuda.synchronize()
+            kernel_s = float(np.mean([a.elapsed_time(b) for a, b in timers])) * 1e-3
     dt = max_over_ranks(dt, world, device)
     E = float(np.mean(edges))
     E_all = sum_over_ranks(E, world, device)
-    edge_avg_s = float(np.mean([a.elapsed_time(b) for a, b in timers])) * 1e-3
-    if H == 64 and n <= engine.FUSED_MAX_N:
-        edge_avg_s /= L      # one event pair per step around the L fused launches
-        # fused layer (sgnn_interaction_layer): edge MLP (two H x H Linears per edge, u/v factorised
-        # out of the first) + node MLP (2H x H, H x H) + the next layer's u/v (2 x H x H) per node
+    alg_step, exe_step = step_flops(n, E, H, L, dim, feat)
+    if one_launch:
+        kernel = "k_step16"
+        flops, exe = alg_step, exe_step
+        # window read + written (n T d 4 each), each layer's u/v written and read once (16 H n), outputs
+        alg_bytes = n * (2 * T_SEQ * dim * 4 + L * 16 * H + 4 * (2 * dim + 1))
+    elif H == 64 and n <= engine.FUSED_MAX_N:
+        kernel_s /= L      # one event pair per step around the L fused launches
         kernel = "k_layer16"
-        # per launch, averaged over the L launches: layer 0 also runs Encoder.edge_fn on its edges
-        # (dim+1 -> H -> H) and the last layer the decoder (H -> H -> dim+1) instead of the next u/v
-        flops = (L * E * 4 * H * H + E * 2 * (H * H + (dim + 1) * H)
-                 + (L - 1) * n * 10 * H * H + n * (8 * H * H + 2 * H * (dim + 1))) / L
-        # e0 row (4H) + ids (8) per edge; u/v rows read (8H), x read (4H), x/u/v written (12H) per node
+        # per launch, averaged over the L launches: edge MLP (two H x H Linears per edge after the u/v
+        # factorisation) + node MLP + the next u/v, layer 0's Encoder.edge_fn and the last layer's decoder
+        exe = (L * E * 4 * H * H + E * 2 * (H * H + (dim + 1) * H)
+               + (L - 1) * n * 10 * H * H + n * (8 * H * H + 2 * H * (dim + 1))) / L
+        # the same launches by §8(d)'s count: the processor's and the edge encoder's share of the step
+        flops = (alg_step - n * (2 * feat * H + 2 * H * H)) / L
         alg_bytes = E * (4 * H + 8) + n * 24 * H
     else:
         kernel = "k_edge_layer"
-        flops = E * 4 * H * H        # two H x H Linears per edge (u/v factorised out of the first)
+        exe = E * 4 * H * H          # two H x H Linears per edge (u/v factorised out of the first)
+        flops = E * 8 * H * H        # §8(d): 3H x H + H x H per edge
         # e0 row (4H) + sender/receiver ids (8) per edge, u/v rows per node (8H), agg row written (4H)
         alg_bytes = E * (4 * H + 8) + n * 12 * H
     out = {"workload": f"{workload}: {'x'.join(map(str, dims))} lattice = {n} particles/GPU, "
@@ -357,8 +434,10 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps,
            "value": n * steps * world / dt, "unit": "particle-steps/s",
            "ms_per_step": dt / steps * 1e3,
            "M_edge_messages_per_s": E_all * L * steps / dt / 1e6,
-           "roofline": roofline(kernel, flops, edge_avg_s, workload, "rollout", alg_bytes)}
-    out["roofline"]["share_of_step"] = edge_avg_s * L / (dt / steps)
+           "path": (f"one launch per step (k_step16, {grid} workgroups of {nt} receivers)" if one_launch
+                    else "kernel sequence"),
+           "roofline": roofline(kernel, flops, kernel_s, workload, "rollout", alg_bytes, exe)}
+    out["roofline"]["share_of_step"] = kernel_s * (1 if one_launch else L) / (dt / steps)
     if cpu_steps > 0 and rank == 0 and world == 1:
         out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps, workload, cpu_seconds)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
@@ -460,10 +539,11 @@ def bench_train(mode, steps, warmup, world, rank, device, seed, cpu_steps):
     E = tw.f.num_edges()
     E_all = sum_over_ranks(E, world, device)
     kstats = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in timers.items()}
-    # dominant kernel: the edge-layer backward (W2^T dy, dW2 += dy h^T; H = 64
-    # forms dE0 / dW1e of all layers afterwards in k_edge_latent_grad)
+    # dominant kernel: the edge-layer backward (H = 64, nmlp_layers 1: k_edge_bwd64, Wl^T dy and
+    # dWl += dy h^T; dE0 / dW1e of all layers are formed afterwards by k_edge_latent_grad)
     dom = "k_edge_bwd"
     flops_bwd = E * (4 if tw.latent_pass else 8) * H * H
+    kname = "k_edge_bwd64" if (H == 64 and tw.nlin == 2) else "k_edge_bwd"
     res = {
         "metric": "particle-steps/sec (2D Taylor-impact, training fwd+bwd+Adam)",
         "value": n_global * steps / dt, "unit": "particle-steps/s", "n_gpus": world, "steps": steps,
@@ -473,7 +553,8 @@ def bench_train(mode, steps, warmup, world, rank, device, seed, cpu_steps):
                    "parallelism": f"dp{world} (whole-graph, RCCL all-reduce)" if world > 1 else "single GPU"},
         "M_edge_messages_per_s": E_all * L * steps / dt / 1e6,
         "final_loss": float(out["loss"]),
-        "roofline": roofline(dom, flops_bwd, kstats[dom], "c2" if mode == "train" else "c3", "train"),
+        "roofline": roofline(kname, flops_bwd, kstats[dom], "c2" if mode == "train" else "c3", "train",
+                             executed_flops=flops_bwd),
         "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
     }
     res["roofline"]["share_of_step"] = float(np.sum([a.elapsed_time(b) for a, b in timers[dom]])) / (dt_ev * 1e3)
@@ -578,6 +659,10 @@ def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps
     # edge backward per edge: last (+ middle) Linear W^T dy and dW, W1e^T dh and dW1e
     flops_bwd = eb / (L + 2) * (8 + (4 if nmlp == 2 else 0)) * H * H
     dom = "k_edge_bwd"
+    # H = 128: one sgnn_edge_layer_bwd call = the per-edge items kernel + one split-K weight-gradient
+    # GEMM per Linear (3 at nmlp_layers 2)
+    kname = "k_edge_bwd64" if (H == 64 and nmlp == 1) else \
+        f"k_edge_items<{nmlp + 1}> + {nmlp + 1} k_wgrad<{H // 32}, {H // 32}>"
     res = {
         "metric": "particle-steps/sec (multi-scale training fwd+bwd+Adam)",
         "value": n * steps * world / dt, "unit": "particle-steps/s", "n_gpus": world,
@@ -589,7 +674,8 @@ def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps
         "M_edge_messages_per_s": eb * steps * world / dt / 1e6,
         "final_loss": float(out["loss"]),
         "hbm_peak_gib": torch.cuda.max_memory_allocated(device) / 2 ** 30,
-        "roofline": roofline(dom, flops_bwd, kstats.get(dom, float("nan")), workload, "train"),
+        "roofline": roofline(kname, flops_bwd, kstats.get(dom, float("nan")), workload, "train",
+                             executed_flops=flops_bwd),
         "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and cpu_steps > 0:

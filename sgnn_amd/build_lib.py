@@ -32,15 +32,18 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB) -> str:
+    """Compile every csrc/*.hip for gfx950 and link `lib`.  `defines` (e.g.
+    SGNN_PROBE) are for experiment builds linked to another path."""
+    if not force and not defines and lib == LIB and not needs_build():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     objs = []
     procs = []
+    tag = "".join("_" + d.lower() for d in defines)
     for src in sources():
-        obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
-        cmd = [HIPCC, *[f for f in FLAGS if f != "-shared"], "-c", src, "-o", obj,
+        obj = os.path.join(LIBDIR, os.path.basename(src) + tag + ".o")
+        cmd = [HIPCC, *[f for f in FLAGS if f != "-shared"], *[f"-D{d}" for d in defines], "-c", src, "-o", obj,
                "-I", os.path.join(ROOT, "include")]
         if verbose:
             print(" ".join(cmd))
@@ -49,12 +52,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs])
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

@@ -97,8 +97,10 @@ extern "C" int sgnn_step_path(const sgnn_epd* m, const sgnn_step_in* in, const s
 
 // One predict_positions; `step` = index of this step within the call (the
 // one-launch step's phase counters are zeroed at step 0 and count on).
+// pos_last: optional contiguous copy of pos_seq's last frame (a rollout's previous next_pos).
 static int predict_impl(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq, const sgnn_step_ws* ws,
-                        float* pred, float* next_pos, float* window_out, void* stream, int32_t step) {
+                        float* pred, float* next_pos, float* window_out, void* stream, int32_t step,
+                        const float* pos_last = nullptr) {
   using namespace sgnn;
   if (!m || !in || !pos_seq || !ws || !pred || !next_pos || m->nlayers < 1 || !m->edge || !m->node)
     return set_error(SGNN_ERR_INVALID, "predict_positions: bad arguments");
@@ -109,6 +111,7 @@ static int predict_impl(const sgnn_epd* m, const sgnn_step_in* in, const float* 
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (step == 0) (void)hipMemsetAsync(ws->step_flags, 0, kStepFlagBytes, s);
     sa.epoch0 = (uint32_t)step * (uint32_t)(m->nlayers + 1);
+    sa.pos_last = pos_last;
     return step16_launch(sa, s);
   }
   const int64_t n = in->n;
@@ -212,8 +215,9 @@ extern "C" int sgnn_rollout(const sgnn_epd* m, const sgnn_step_in* in, float* wi
   for (int32_t k = 0; k < nsteps; ++k) {
     float* cur = (k & 1) ? win_b : win_a;
     float* nxt = (k & 1) ? win_a : win_b;
+    // step k's window ends with step k-1's prediction, already contiguous in out_pos
     const int st = predict_impl(m, in, cur, ws, out_pred + (int64_t)k * n * (d + 1), out_pos + (int64_t)k * n * d,
-                                nxt, stream, k);
+                                nxt, stream, k, k > 0 ? out_pos + (int64_t)(k - 1) * n * d : nullptr);
     if (st) return st;
   }
   return SGNN_OK;

@@ -23,6 +23,7 @@ struct Lay16 {
 struct Step16Args {
   // inputs (learned_simulator.py:413-438): window [n][T][dim], examples
   const float* pos_seq;
+  const float* pos_last;  // optional: the window's last frame as a contiguous [n][dim] copy (rollout steps > 0)
   int n, T, dim;
   const int64_t* ex_ptr;
   int n_ex;

@@ -62,7 +62,7 @@ SGNN_DEV void st4_sc1(__amdgpu_buffer_rsrc_t rs, int voff, f32x4 v) {
 
 // LDS carve (floats), shared with the host's size query.
 struct Carve {
-  int sw0, sw1, svec, sxw, sxv, scratch, xs, region, ints, total;  // float offsets / count
+  int sw0, sw1, svec, sxw, sxv, scratch, xs, tb, region, ints, total;  // float offsets / count
   int region_floats;
 };
 SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
@@ -75,29 +75,47 @@ SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
   c.sxv = o; o += 4 * H;          // Encoder.edge_fn b1, b2, gamma, beta
   c.scratch = o; o += 4 * 16 * LDX;  // per-wave receiver sums; node-phase exchange buffers
   c.xs = o; o += 16 * LDX;        // x rows of the tile's nodes (resident for the step)
+  c.tb = o; o += 4 * H * 20;      // per-wave [unit][edge] tiles of the MFMA receiver sums (kTB = 20)
   const int e0f = e0g ? 0 : nt * cap * LDX, posf = n * dim;
   c.region_floats = e0f > posf ? e0f : posf;  // positions (radius phase), then e0 rows (unless in HBM)
   c.region = o; o += (c.region_floats + 3) & ~3;
-  c.ints = o;                     // lsend, lrecv, nbr [nt*cap] each; deg [16]; pre [20]; mask [8]; kw [4][64]
-  o += 3 * nt * cap + 16 + 20 + 8 + 4 * 64;
+  // lsend, lrecv [round16(nt*cap)] each, nbr [nt*cap]; deg [16]; pre [20]; mask [8]; kw [4][64]; deps [256] + count
+  c.ints = o;
+  o += 2 * ((nt * cap + 15) & ~15) + nt * cap + 16 + 20 + 8 + 4 * 64 + sgnn::kStep16MaxGrid + 4;
   c.total = (o + 3) & ~3;
   return c;
 }
 
-// Per-tile counters: wave 0 polls those of the tiles in `mask`, the others wait at the barrier.
-SGNN_DEV void wait_tiles(const uint32_t* mask, uint32_t* flags, int G, uint32_t epoch, int b, int lane) {
+// Experiment builds (-DSGNN_PROBE, tools/exp_probe_step16.py): per-wave s_memtime marks at the phase
+// boundaries, [workgroup][wave][32] into the buffer set by sgnn_set_probe16.
+#ifdef SGNN_PROBE
+__device__ uint64_t* g_probe16;
+SGNN_DEV void mark(int slot) {
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  if (g_probe16 && lane_id() == 0) g_probe16[((int64_t)blockIdx.x * kWaves16 + wave_id()) * 32 + slot] = t;
+}
+#else
+SGNN_DEV void mark(int) {}
+#endif
+
+// Per-tile counters: wave 0 polls those of the sender tiles `deps` (up to 256, all requested at
+// once), the other waves wait at the barrier.
+SGNN_DEV void wait_tiles(const int32_t* deps, int ndeps, uint32_t* flags, uint32_t epoch, int b, int lane) {
   if (b == 0) {
     for (int it = 0;; ++it) {
+      uint32_t v[kMaxGrid / 64];
+#pragma unroll
+      for (int q = 0; q < kMaxGrid / 64; ++q)
+        v[q] = lane + 64 * q < ndeps ? __hip_atomic_load((gu32*)(flags + deps[lane + 64 * q]), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : epoch;
       bool ok = true;
-      for (int t = lane; t < G; t += 64)
-        if ((mask[t >> 5] >> (t & 31)) & 1u)
-          ok = ok && __hip_atomic_load((gu32*)(flags + t), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+#pragma unroll
+      for (int q = 0; q < kMaxGrid / 64; ++q) ok = ok && v[q] >= epoch;
       if (__all(ok)) break;
       if (it >= kPollLimit) {
         if (lane == 0)
-          __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -168,128 +186,213 @@ SGNN_DEV void step_tail(const Step16Args& a, const NodeW<2, MODE>& W, float* scr
   }
 }
 
-// The edge MLP over the tile's edges (wave b takes the 16-edge halves b, b + 4,
-// ... of the compacted tile CSR), LayerNorm, and the receiver sums (DPP
-// row-segmented scan, per-wave LDS rows, fixed order).  FIRST: the edge
-// features and Encoder.edge_fn run inline and e0 rows are kept in LDS.
-template <bool FIRST>
-SGNN_DEV void step_edges(const Step16Args& a, const float* sw0, const float* sw1, const float* svec,
-                         const float* sxw, const float* sxv, const float (&xw1)[KQ], float* sums, float* e0l,
-                         const int32_t* lsend, const int32_t* lrecv, int Et, int i0,
-                         __amdgpu_buffer_rsrc_t ru, __amdgpu_buffer_rsrc_t rv, int b, int j, int g) {
-  int r_n = 0, s_n = 0;
-  f32x4 x_n[KQ], uv_n[KQ];
-  float ps_n[3] = {0.0f, 0.0f, 0.0f}, pr_n[3] = {0.0f, 0.0f, 0.0f};
-  const float* pos = a.pos_seq + (int64_t)(a.T - 1) * a.dim;
-  const int pstride = a.T * a.dim;
-  auto load_half = [&](int hs) {
-    const int e = hs + j;
-    const int ec = e < Et ? e : Et - 1;
-    r_n = lrecv[ec];
-    s_n = lsend[ec];
-    if constexpr (FIRST) {
+// The receiver sums of one 16-edge half on the matrix cores.  The last
+// Linear's output y (D layout: lane (edge j, g) holds units 16 t + 4 g + c) is
+// LayerNorm'd (graph_network.py:197-198), written to this wave's LDS tile
+// tb [unit][edge] (row stride kTB: conflict-free both ways), and
+//   agg[unit][recv] += m[unit][edge] S[edge][recv],   S = the half's 0/1 receiver incidence
+// runs as 16 v_mfma_f32_16x16x4_f32 (A = m read back [unit][4 edges], B = S
+// built from the half's receiver ids): the segmented sum becomes 16 MFMAs
+// instead of ~200 DPP / select / add instructions plus an LDS read-modify-write
+// per half, and the wave's aggregates stay in registers across its halves.
+// Receiver r of the tile is column r - i0 (< 16); padding edges have S = 0.
+constexpr int kTB = 20;   // tb row stride (floats): lanes of a b128 read hit disjoint banks
+SGNN_DEV void half_agg(const f32x4 (&y)[KQ], f32x4 (&agg)[KQ], const float* svec, float* tb, const int32_t* lrecv,
+                       int hs, int Et, int i0, int j, int g, int l) {
+  float mu, rs;
+  ln_stats(y, mu, rs);
+  const bool ev = hs + j < Et;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        if (c < a.dim) {
-          ps_n[c] = pos[(int64_t)s_n * pstride + c];
-          pr_n[c] = pos[(int64_t)r_n * pstride + c];
-        }
-    } else {
+  for (int t = 0; t < KQ; ++t) {
+    const f32x4 ga = ld4(svec + H + 16 * t + 4 * g), be = ld4(svec + 2 * H + 16 * t + 4 * g);
 #pragma unroll
-      for (int q = 0; q < KQ; ++q) x_n[q] = ld4(e0l + ec * LDX + 16 * q + 4 * g);
-    }
+    for (int c = 0; c < 4; ++c)
+      tb[(16 * t + 4 * g + c) * kTB + j] = ev ? (y[t][c] - mu) * rs * ga[c] + be[c] : 0.0f;
+  }
+  // B: lane (k = l >> 4, col = l & 15) supplies S[edge 4k + s][col] for step s = 0..3 (the K order of A)
+  const int kk = l >> 4, col = l & 15;
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 rv = *reinterpret_cast<const i32x4*>(lrecv + hs + 4 * kk);
+  float sb[4];
 #pragma unroll
-    for (int t = 0; t < KQ; ++t)
-      uv_n[t] = ld4_sc1(ru, r_n * (H * 4) + (16 * t + 4 * g) * 4) + ld4_sc1(rv, s_n * (H * 4) + (16 * t + 4 * g) * 4);
-  };
-  if (16 * b < Et) load_half(16 * b);
-  for (int hs = 16 * b; hs < Et; hs += 16 * kWaves16) {
-    const bool ev = hs + j < Et;
-    const int r = r_n;
-    f32x4 x[KQ], acc[KQ];
-    float ps[3], pr[3];
+  for (int s2 = 0; s2 < 4; ++s2) sb[s2] = (hs + 4 * kk + s2 < Et && rv[s2] - i0 == col) ? 1.0f : 0.0f;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-      x[q] = x_n[q];
-      acc[q] = uv_n[q];
-    }
+  for (int t = 0; t < KQ; ++t) {
+    const f32x4 av = ld4(tb + (16 * t + col) * kTB + 4 * kk);  // A: lane (unit col, k) = m[unit][4k .. 4k+3]
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      ps[c] = ps_n[c];
-      pr[c] = pr_n[c];
-    }
-    if (hs + 16 * kWaves16 < Et) load_half(hs + 16 * kWaves16);
-    if constexpr (FIRST) {
-      // edge features (p_s - p_r) / R and their norm (learned_simulator.py:299-312)
-      float f[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ss = 0.0f;
+    for (int s2 = 0; s2 < 4; ++s2) agg[t] = mfma16(av[s2], sb[s2], agg[t]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();   // tb is rewritten by the next half
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kPre = 3;   // halves per wave whose W1e e0 product runs before the wait
+
+// The edge MLP of a layer, split around the wait for the sender tiles.  Wave b
+// takes the 16-edge halves b, b + 4, ... of the compacted tile CSR.  The first
+// Linear on cat[x_i, x_j, e] is u[recv] + v[send] + 2^k W1_e e0 (graph_network.py:
+// 197): its e0 part needs no other tile's data, so `prewait` forms it for the
+// wave's first kPre halves BEFORE the wait (and, FIRST, runs the edge features +
+// Encoder.edge_fn for every half and keeps the e0 rows), and `postwait` adds the
+// gathered u / v rows, runs the last Linear + LayerNorm and the receiver sums
+// (half_agg, on the matrix cores).
+struct EdgePhase {
+  const Step16Args& a;
+  const float *sw0, *sw1, *svec, *sxw, *sxv;
+  float *sums, *tb, *e0l;
+  const int32_t *lsend, *lrecv;
+  int Et, i0, b, j, g, l;
+  f32x4 pre[kPre][KQ];
+
+  // Encoder.edge_fn of one half from its endpoints' positions -> x (e0), rows kept in e0l
+  SGNN_DEV void encode(f32x4 (&x)[KQ], const float (&xw1)[KQ], const float (&ps)[3], const float (&pr)[3], int hs,
+                       bool ev) const {
+    // edge features (p_s - p_r) / R and their norm (learned_simulator.py:299-312)
+    float f[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ss = 0.0f;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        if (c < a.dim) {
-          const float dd = __fdiv_rn(__fsub_rn(ps[c], pr[c]), a.radius);
-          f[c] = dd;
-          ss = __fadd_rn(ss, __fmul_rn(dd, dd));
-        }
-      const float nrm = sqrtf(ss);
-      if (a.dim == 1) f[1] = nrm; else if (a.dim == 2) f[2] = nrm; else f[3] = nrm;
-      const float fg = g == 0 ? f[0] : g == 1 ? f[1] : g == 2 ? f[2] : f[3];
-      // Encoder.edge_fn: Linear(dim + 1, H) -> ReLU -> Linear(H, H) -> LayerNorm (graph_network.py:92-96)
-      f32x4 hx[KQ], y[KQ];
-#pragma unroll
-      for (int t = 0; t < KQ; ++t) {
-        hx[t] = relu4(mfma16(xw1[t], fg, ld4(sxv + 16 * t + 4 * g)));
-        y[t] = ld4(sxv + H + 16 * t + 4 * g);
+    for (int c = 0; c < 3; ++c)
+      if (c < a.dim) {
+        const float dd = __fdiv_rn(__fsub_rn(ps[c], pr[c]), a.radius);
+        f[c] = dd;
+        ss = __fadd_rn(ss, __fmul_rn(dd, dd));
       }
-      mm_full(y, sxw, hx, j, g);
-      float mu, rs;
-      ln_stats(y, mu, rs);
-      const int e = hs + j;
-#pragma unroll
-      for (int t = 0; t < KQ; ++t) {
-        const f32x4 ga = ld4(sxv + 2 * H + 16 * t + 4 * g), be = ld4(sxv + 3 * H + 16 * t + 4 * g);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) x[t][c] = (y[t][c] - mu) * rs * ga[c] + be[c];
-        if (ev) st4(e0l + e * LDX + 16 * t + 4 * g, x[t]);  // e0 rows for the later layers
-      }
-    }
-    // first Linear: u[recv] + v[send] + 2^k W1_e e0 (graph_network.py:197 on cat[x_i, x_j, e])
-    mm_full(acc, sw0, x, j, g);
-#pragma unroll
-    for (int t = 0; t < KQ; ++t) x[t] = relu4(acc[t]);
-#pragma unroll
-    for (int t = 0; t < KQ; ++t) acc[t] = ld4(svec + 16 * t + 4 * g);
-    mm_full(acc, sw1, x, j, g);
-    float mu, rs;
-    ln_stats(acc, mu, rs);
-    f32x4 m[KQ];
+    const float nrm = sqrtf(ss);
+    if (a.dim == 1) f[1] = nrm; else if (a.dim == 2) f[2] = nrm; else f[3] = nrm;
+    const float fg = g == 0 ? f[0] : g == 1 ? f[1] : g == 2 ? f[2] : f[3];
+    // Linear(dim + 1, H) -> ReLU -> Linear(H, H) -> LayerNorm (graph_network.py:92-96)
+    f32x4 hx[KQ], y[KQ];
 #pragma unroll
     for (int t = 0; t < KQ; ++t) {
-      const f32x4 ga = ld4(svec + H + 16 * t + 4 * g), be = ld4(svec + 2 * H + 16 * t + 4 * g);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) m[t][c] = (acc[t][c] - mu) * rs * ga[c] + be[c];
+      hx[t] = relu4(mfma16(xw1[t], fg, ld4(sxv + 16 * t + 4 * g)));
+      y[t] = ld4(sxv + H + 16 * t + 4 * g);
     }
-    // receiver runs of the half (recv sorted along the 16-lane rows): segmented
-    // inclusive scan with DPP row shifts; the last lane of each run adds its
-    // total to the receiver's row of this wave's sums
-    const int rk = ev ? r : -1 - j;
+    mm_full(y, sxw, hx, j, g);
+    float mu, rs;
+    ln_stats(y, mu, rs);
+    const int e = hs + j;
 #pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-      const int prv = dpp_row_shr(rk, d, INT32_MIN);
+    for (int t = 0; t < KQ; ++t) {
+      const f32x4 ga = ld4(sxv + 2 * H + 16 * t + 4 * g), be = ld4(sxv + 3 * H + 16 * t + 4 * g);
 #pragma unroll
-      for (int t = 0; t < KQ; ++t)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float pv = __int_as_float(dpp_row_shr(__float_as_int(m[t][c]), d, 0));
-          m[t][c] = prv == rk ? m[t][c] + pv : m[t][c];
-        }
-    }
-    const int rn = dpp_row_shl1(rk, INT32_MIN);
-    if (ev && rn != rk) {
-      float* dst = sums + (r - i0) * LDX + 4 * g;
-#pragma unroll
-      for (int t = 0; t < KQ; ++t) st4(dst + 16 * t, ld4(dst + 16 * t) + m[t]);
+      for (int c = 0; c < 4; ++c) x[t][c] = (y[t][c] - mu) * rs * ga[c] + be[c];
+      if (ev) st4(e0l + e * LDX + 16 * t + 4 * g, x[t]);
     }
   }
-}
+
+  SGNN_DEV void ld_e0(f32x4 (&x)[KQ], int hs) const {
+    const int e = hs + j, ec = e < Et ? e : Et - 1;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) x[q] = ld4(e0l + ec * LDX + 16 * q + 4 * g);
+  }
+
+  // before the wait: (FIRST) e0 of every half; W1e e0 of the first kPre halves
+  template <bool FIRST>
+  SGNN_DEV void prewait(const float (&xw1)[KQ]) {
+    const float* pos = a.pos_last ? a.pos_last : a.pos_seq + (int64_t)(a.T - 1) * a.dim;
+    const int pstride = a.pos_last ? a.dim : a.T * a.dim;
+    float ps_n[3] = {0.0f, 0.0f, 0.0f}, pr_n[3] = {0.0f, 0.0f, 0.0f};
+    auto load_pos = [&](int hs) {
+      const int e = hs + j, ec = e < Et ? e : Et - 1;
+      const int r = lrecv[ec], s = lsend[ec];
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (c < a.dim) {
+          ps_n[c] = pos[(int64_t)s * pstride + c];
+          pr_n[c] = pos[(int64_t)r * pstride + c];
+        }
+    };
+    if (FIRST && 16 * b < Et) load_pos(16 * b);
+#pragma unroll
+    for (int m = 0; m < kPre; ++m) {
+      const int hs = 16 * b + 16 * kWaves16 * m;
+      if (hs >= Et) break;
+      f32x4 x[KQ];
+      if constexpr (FIRST) {
+        float ps[3], pr[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          ps[c] = ps_n[c];
+          pr[c] = pr_n[c];
+        }
+        load_pos(hs + 16 * kWaves16);
+        encode(x, xw1, ps, pr, hs, hs + j < Et);
+      } else {
+        ld_e0(x, hs);
+      }
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) pre[m][t] = zero4();
+      mm_full(pre[m], sw0, x, j, g);
+    }
+    if constexpr (FIRST) {  // the rest of the halves: e0 rows only
+      for (int hs = 16 * b + 16 * kWaves16 * kPre; hs < Et; hs += 16 * kWaves16) {
+        float ps[3], pr[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          ps[c] = ps_n[c];
+          pr[c] = pr_n[c];
+        }
+        load_pos(hs + 16 * kWaves16);
+        f32x4 x[KQ];
+        encode(x, xw1, ps, pr, hs, hs + j < Et);
+      }
+    }
+  }
+
+  // after the wait: + u[recv] + v[send], ReLU, last Linear, LayerNorm, receiver sums (half_agg);
+  // the wave's receiver aggregates are stored to its rows of `sums` at the end
+  SGNN_DEV void postwait(__amdgpu_buffer_rsrc_t ru, __amdgpu_buffer_rsrc_t rv, bool probe = false) {
+    f32x4 agg[KQ];
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) agg[t] = zero4();
+    f32x4 uv_n[KQ];
+    auto gather = [&](int hs) {  // clamped: harmless past the end
+      const int e = hs + j, ec = e < Et ? e : Et - 1;
+      const int r = lrecv[ec], s = lsend[ec];
+#pragma unroll
+      for (int t = 0; t < KQ; ++t)
+        uv_n[t] = ld4_sc1(ru, r * (H * 4) + (16 * t + 4 * g) * 4) + ld4_sc1(rv, s * (H * 4) + (16 * t + 4 * g) * 4);
+    };
+    auto finish = [&](f32x4 (&acc)[KQ], int hs) {  // ReLU -> last Linear -> LayerNorm -> sums
+      f32x4 x[KQ], y[KQ];
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) {
+        x[t] = relu4(acc[t]);
+        y[t] = ld4(svec + 16 * t + 4 * g);
+      }
+      mm_full(y, sw1, x, j, g);
+      half_agg(y, agg, svec, tb, lrecv, hs, Et, i0, j, g, l);
+    };
+    int hs = 16 * b;
+    if (hs < Et) gather(hs);
+    if (probe) mark(28);
+#pragma unroll
+    for (int m = 0; m < kPre; ++m) {
+      if (hs >= Et) break;
+      f32x4 acc[KQ];
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) acc[t] = pre[m][t] + uv_n[t];
+      gather(hs + 16 * kWaves16);
+      finish(acc, hs);
+      if (probe) mark(29 + m);
+      hs += 16 * kWaves16;
+    }
+    for (; hs < Et; hs += 16 * kWaves16) {   // halves past kPre: the e0 product here
+      f32x4 x[KQ], acc[KQ];
+      ld_e0(x, hs);
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) acc[t] = uv_n[t];
+      gather(hs + 16 * kWaves16);
+      mm_full(acc, sw0, x, j, g);
+      finish(acc, hs);
+    }
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) st4(sums + j * LDX + 16 * t + 4 * g, agg[t]);
+  }
+};
 
 // Stage an edge MLP's LDS images: W1e (columns 2H..3H of W1, x scale) and W2 + vectors.
 struct EdgeStage {
@@ -342,31 +445,37 @@ SGNN_DEV Node16Args node_args(const Step16Args& a, const Lay16& L, const Lay16* 
 // next layer's edge weights.
 template <bool FIRST, int MODE, bool E0G>
 SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv, const float (&xw1)[KQ],
-                         const uint32_t* mask, const int32_t* lsend, const int32_t* lrecv, int Et, int i0, int cnt,
-                         int b, int j, int g, int l) {
-  const int tile = blockIdx.x, G = gridDim.x;
+                         const int32_t* deps, int ndeps, const int32_t* lsend, const int32_t* lrecv, int Et, int i0,
+                         int cnt, int b, int j, int g, int l) {
+  const int tile = blockIdx.x;
   float* sw0 = lds + cv.sw0;
   float* sw1 = lds + cv.sw1;
   float* svec = lds + cv.svec;
   float* scratch = lds + cv.scratch;
   float* xs = lds + cv.xs;
+  float* tb = lds + cv.tb + b * H * kTB;
   const int64_t nH = (int64_t)a.n * H;
   // e0 rows of the tile's edges: LDS, or (graphs whose tile does not fit) a per-tile HBM block behind
   // the layers' node halves -- written and read by this workgroup only
   float* e0l = E0G ? a.uvl + 2 * a.L * nH + (int64_t)tile * a.ecap_t * LDX : lds + cv.region;
   const __amdgpu_buffer_rsrc_t ru = buf_rsrc(a.uvl + (2 * k) * nH), rv = buf_rsrc(a.uvl + (2 * k + 1) * nH);
-  // this layer's node weights (VGPR-resident) are requested before the wait
   const Lay16 Lk = lay_at(a, k), Ln = lay_at(a, MODE == 0 ? k + 1 : k);
+  // this layer's node weights (VGPR-resident) are requested first: the W1e e0 products and the wait
+  // for the sender tiles hide their latency (this layer's edge weights were staged in LDS before the
+  // previous layer published)
   NodeW<2, MODE> W;
   W.load(node_args(a, Lk, MODE == 0 ? &Ln : nullptr), b, j, g);
-  wait_tiles(mask, a.flags, G, a.epoch0 + (uint32_t)k + 1, b, l);
   float* sums = scratch + b * 16 * LDX;
-#pragma unroll
-  for (int q = 0; q < KQ; ++q) st4(sums + j * LDX + 16 * q + 4 * g, zero4());
-  step_edges<FIRST>(a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, xw1, sums, e0l, lsend, lrecv, Et, i0, ru, rv, b, j,
-                    g);
+  EdgePhase ep{a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, sums, tb, e0l, lsend, lrecv, Et, i0, b, j, g, l};
+  mark(3 + 5 * k);
+  ep.template prewait<FIRST>(xw1);
+  mark(4 + 5 * k);
+  wait_tiles(deps, ndeps, a.flags, a.epoch0 + (uint32_t)k + 1, b, l);
+  mark(5 + 5 * k);
+  ep.postwait(ru, rv, k == 1);
+  mark(6 + 5 * k);
   __syncthreads();
-  // the next layer's edge weights: requested now, stored once the node phase is done
+  // the next layer's edge weights: requested now, staged in LDS before this layer publishes
   EdgeStage nxt;
   if (MODE == 0) nxt.load(Ln);
   f32x4 ag[KQ];
@@ -387,10 +496,12 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   if constexpr (MODE == 0) {
     const __amdgpu_buffer_rsrc_t ru1 = buf_rsrc(a.uvl + (2 * k + 2) * nH), rv1 = buf_rsrc(a.uvl + (2 * k + 3) * nH);
     step_tail<0>(a, W, scratch, xs, i, valid, h, xo, b, j, g, ru1, rv1);
-    publish(a.flags, tile, a.epoch0 + (uint32_t)k + 2);
     nxt.store(sw0, sw1, svec, Ln, (float)(2 << k));  // W1e x 2^(k+1): exact
+    mark(7 + 5 * k);
+    publish(a.flags, tile, a.epoch0 + (uint32_t)k + 2);
   } else {
     step_tail<1>(a, W, scratch, xs, i, valid, h, xo, b, j, g, ru, rv);
+    mark(7 + 5 * k);
   }
 }
 
@@ -409,26 +520,56 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   const Carve cv = carve(n, DIM, nt, cap, E0G);
   int32_t* ints = reinterpret_cast<int32_t*>(lds + cv.ints);
   int32_t* lsend = ints;
-  int32_t* lrecv = lsend + nt * cap;
-  int32_t* nbr_l = lrecv + nt * cap;
+  int32_t* lrecv = lsend + ((nt * cap + 15) & ~15);   // 16-B aligned rows: half_agg reads int4s
+  int32_t* nbr_l = lrecv + ((nt * cap + 15) & ~15);
   int32_t* ldeg = nbr_l + nt * cap;
   int32_t* lpre = ldeg + 16;
   uint32_t* mask = reinterpret_cast<uint32_t*>(lpre + 20);
   int32_t* kw_all = reinterpret_cast<int32_t*>(mask + 8);
+  int32_t* deps = kw_all + 4 * 64;       // the sender tiles of this tile's edges, compacted
+  int32_t* ndeps_l = deps + kMaxGrid;
 
-  // weights of layer 0's edge MLP and of Encoder.edge_fn, in flight during the radius search
-  EdgeStage st0;
-  st0.load(a.lay[0]);
-  f32x4 sx[kStagePer];
-  stage_w64_load(sx, a.xe_w2, H);
+  mark(0);
   if (threadIdx.x < 8) mask[threadIdx.x] = 0u;
 
   // ---- radius graph of the tile's receivers (torch_cluster's rule: first `cap` in-range senders of
   // the receiver's example in ascending index, strict <; learned_simulator.py:116-117) --------------
   float* sp = lds + cv.region;  // [DIM][n] SoA
-  for (int t = threadIdx.x; t < n * DIM; t += kBlock16) {
-    const int i = t / DIM, d = t - i * DIM;
-    sp[d * n + i] = a.pos_seq[((int64_t)i * a.T + a.T - 1) * DIM + d];
+  if (a.pos_last) {  // the previous step's next_pos: contiguous, coalesced
+    for (int t = threadIdx.x; t < n * DIM; t += kBlock16) {
+      const int i = t / DIM, d = t - i * DIM;
+      sp[d * n + i] = a.pos_last[t];
+    }
+  } else {
+    for (int t = threadIdx.x; t < n * DIM; t += kBlock16) {
+      const int i = t / DIM, d = t - i * DIM;
+      sp[d * n + i] = a.pos_seq[((int64_t)i * a.T + a.T - 1) * DIM + d];
+    }
+  }
+
+  // weights of layer 0's edge MLP, of Encoder.edge_fn and of Encoder.node_fn (VGPR-resident), issued after the
+  // positions (loads complete in order) and in flight during the radius queries
+  EdgeStage st0;
+  st0.load(a.lay[0]);
+  f32x4 sx[kStagePer];
+  stage_w64_load(sx, a.xe_w2, H);
+  NodeW<2, 0> E;
+  f32x4 w1f[KQF];
+  f32x4 vb1;
+  {
+    Node16Args nd{};
+    nd.w2 = a.xn_w2; nd.b2 = a.xn_b2; nd.g = a.xn_g; nd.bb = a.xn_bb;
+    nd.we = a.lay[0].ew1; nd.be = a.lay[0].eb1; nd.dim = DIM;
+    E.load_tail(nd, b, j, g);
+    const int urow = 16 * b + j;
+#pragma unroll
+    for (int q = 0; q < KQF; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * q + 4 * g + c;
+        w1f[q][c] = f < a.feat ? a.xn_w1[(int64_t)urow * a.feat + f] : 0.0f;
+      }
+    vb1 = ld4(a.xn_b1 + 16 * b + 4 * g);
   }
   __syncthreads();
   {
@@ -479,6 +620,7 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
       wave_lds_sync();
     }
   }
+  mark(1);
   // LDS images of the staged weights (the radius phase never touches them)
   st0.store(lds + cv.sw0, lds + cv.sw1, lds + cv.svec, a.lay[0], 1.0f);
   stage_w64_store(lds + cv.sxw, sx, 1.0f);
@@ -514,6 +656,18 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
       if (a.nbr_out) a.nbr_out[(int64_t)(i0 + k) * cap + q] = sv;
     }
   }
+  __syncthreads();
+  if (b == 0) {  // the mask as a list (wave_lds_sync-free: one wave, in order)
+    int base = 0;
+    for (int t0 = 0; t0 < (int)gridDim.x; t0 += 64) {
+      const int t = t0 + l;
+      const bool on = t < (int)gridDim.x && ((mask[t >> 5] >> (t & 31)) & 1u);
+      const uint64_t bal = __ballot(on);
+      if (on) deps[base + (int)__popcll(bal & ((1ull << l) - 1ull))] = t;
+      base += (int)__popcll(bal);
+    }
+    if (l == 0) *ndeps_l = base;
+  }
 
   // ---- Encoder.node_fn of the tile's nodes (features: learned_simulator.py:256-290) -> x0 (LDS),
   // u_0 / v_0 (published as phase 1) ------------------------------------------------------------
@@ -521,21 +675,6 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
 #pragma unroll
   for (int t = 0; t < KQ; ++t) xw1[t] = g <= DIM ? a.xe_w1[(16 * t + j) * (DIM + 1) + g] : 0.0f;
   {
-    Node16Args nd{};
-    nd.w2 = a.xn_w2; nd.b2 = a.xn_b2; nd.g = a.xn_g; nd.bb = a.xn_bb;
-    nd.we = a.lay[0].ew1; nd.be = a.lay[0].eb1; nd.dim = DIM;
-    NodeW<2, 0> E;
-    E.load_tail(nd, b, j, g);
-    f32x4 w1f[KQF];
-    const int urow = 16 * b + j;
-#pragma unroll
-    for (int q = 0; q < KQF; ++q)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int f = 16 * q + 4 * g + c;
-        w1f[q][c] = f < a.feat ? a.xn_w1[(int64_t)urow * a.feat + f] : 0.0f;
-      }
-    const f32x4 vb1 = ld4(a.xn_b1 + 16 * b + 4 * g);
     const int64_t i = i0 + j;
     const bool valid = j < cnt;
     const int64_t ic = valid ? i : (int64_t)i0;
@@ -564,13 +703,15 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     step_tail<0>(a, E, lds + cv.scratch, lds + cv.xs, i, valid, h, zero4(), b, j, g, buf_rsrc(a.uvl),
                  buf_rsrc(a.uvl + nH));
     publish(a.flags, tile, a.epoch0 + 1);
+    mark(2);
   }
 
   // ---- the interaction layers ------------------------------------------------------------------
-  step_layer<true, 0, E0G>(a, 0, lds, cv, xw1, mask, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+  const int ndeps = *ndeps_l;
+  step_layer<true, 0, E0G>(a, 0, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
   for (int k = 1; k < a.L - 1; ++k)
-    step_layer<false, 0, E0G>(a, k, lds, cv, xw1, mask, lsend, lrecv, Et, i0, cnt, b, j, g, l);
-  step_layer<false, 1, E0G>(a, a.L - 1, lds, cv, xw1, mask, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+    step_layer<false, 0, E0G>(a, k, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+  step_layer<false, 1, E0G>(a, a.L - 1, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
 }
 
 }  // namespace
@@ -617,3 +758,9 @@ int step16_launch(const Step16Args& a, hipStream_t s) {
 }
 
 }  // namespace sgnn
+
+#ifdef SGNN_PROBE
+extern "C" int sgnn_set_probe16(uint64_t* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_probe16), &buf, sizeof(buf)) == hipSuccess ? 0 : 3;
+}
+#endif

@@ -176,7 +176,8 @@ class LearnedSimulator(nn.Module):
     def _decoder_postprocessor(self, normalized_acceleration, position_sequence):
         """learned_simulator.py:381-411 (used only on materialised tensors)."""
         st = self._normalization_stats["acceleration"]
-        acc = normalized_acceleration * st["std"] + st["mean"]
+        dev = normalized_acceleration.device
+        acc = normalized_acceleration * torch.as_tensor(st["std"]).to(dev) + torch.as_tensor(st["mean"]).to(dev)
         most_recent = position_sequence[:, -1]
         return most_recent + ((most_recent - position_sequence[:, -2]) + acc)
 

@@ -249,7 +249,8 @@ class MultiScaleSimulator(nn.Module):
     def _decoder_postprocessor(self, normalized_acceleration, position_sequence):
         """:253-279"""
         st = self._normalization_stats["acceleration"]
-        acc = normalized_acceleration * st["std"] + st["mean"]
+        dev = normalized_acceleration.device
+        acc = normalized_acceleration * torch.as_tensor(st["std"]).to(dev) + torch.as_tensor(st["mean"]).to(dev)
         recent = position_sequence[:, -1]
         return recent + ((recent - position_sequence[:, -2]) + acc)
 

@@ -7,9 +7,9 @@ scaling, the one all-reduce of gradient + loss sums, and the fused Adam after
 it.  Every rank must end with the loss, gradient and Adam-updated weights of
 ONE process running the concatenated batch (train.py:268 averages over the
 whole batch).  Tolerances: loss 1e-5 relative; gradients 2e-5 of the largest
-(the ranks' partial sums are added in another order, fp32); weights 2e-6
-absolute where |g| > 1e-6 max|g| (Adam's first steps are lr sign(g)-like:
-only near-zero gradients can flip a step of 1e-3)."""
+(the ranks' partial sums are added in another order, fp32); weights within
+what that gradient error can move an Adam step (~lr x the relative gradient
+error, at most 2 lr per step)."""
 import os
 import socket
 import subprocess
@@ -34,7 +34,7 @@ def _free_port():
 
 @pytest.mark.parametrize("case", ["ss", "ms"])
 def test_two_ranks_match_one_process(case, tmp_path):
-    from tests.dp_cases import CASES, LR
+    from tests.dp_cases import CASES, LR, STEPS
     run, _, ranks = CASES[case]
     world, port = len(ranks), str(_free_port())
     outs = [str(tmp_path / f"rank{r}.pt") for r in range(world)]
@@ -58,9 +58,12 @@ def test_two_ranks_match_one_process(case, tmp_path):
         dg = (got["grad"] - ref["grad"]).abs()
         print(f"{case} rank {r}: max|dgrad| {float(dg.max()):.3e} of max|g| {gmax:.3e}")
         assert float(dg.max()) <= 2e-5 * gmax
+        # Adam moves a weight by ~lr (g1, g2 ratios) per step: a relative gradient error d moves it
+        # by ~lr d, at most 2 lr per step -> |dw| <= 1e-6 + 2 STEPS lr min(1, 2e-5 gmax / |g|)
         dw = (got["param"] - ref["param"]).abs().numpy()
-        loose = (ref["grad"].abs() <= 1e-6 * gmax).numpy()
-        assert (dw[~loose] <= 2e-6).all(), float(dw[~loose].max())
-        assert (dw[loose] <= 2 * 2 * LR + 1e-6).all()
+        g = ref["grad"].abs().numpy()
+        bound = 1e-6 + 2 * STEPS * LR * np.minimum(1.0, 2e-5 * gmax / np.maximum(g, 1e-30))
+        print(f"{case} rank {r}: max|dw| {dw.max():.3e}, worst |dw|/bound {(dw / bound).max():.3f}")
+        assert (dw <= bound).all()
     g0, g1 = (torch.load(p, weights_only=True) for p in outs)
     assert torch.equal(g0["grad"], g1["grad"]) and torch.equal(g0["param"], g1["param"])

