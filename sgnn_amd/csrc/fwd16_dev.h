@@ -134,6 +134,18 @@ struct NodeW {
   }
   // everything after the first Linear (the encoder supplies its own first Linear)
   SGNN_DEV void load_tail(const Node16Args& a, int b, int j, int g) {
+    load_mid(a, b, j, g);
+    load_out(a, b, j, g);
+  }
+  // the first Linear only / the node MLP's tail / the next edge MLP's node halves or the decoder: three
+  // parts the one-launch step requests at different points
+  SGNN_DEV void load_first(const Node16Args& a, int b, int j, int g) {
+    const int urow = 16 * b + j, ucol = 16 * b + 4 * g;
+    load_wrow(w1a, a.w1, 2 * H, urow, 0, g);
+    load_wrow(w1x, a.w1, 2 * H, urow, H, g);
+    vb1 = ld4(a.b1 + ucol);
+  }
+  SGNN_DEV void load_mid(const Node16Args& a, int b, int j, int g) {
     const int urow = 16 * b + j, ucol = 16 * b + 4 * g;
     if (NL == 3) load_wrow(wm, a.wm, H, urow, 0, g);
     load_wrow(w2, a.w2, H, urow, 0, g);
@@ -141,6 +153,9 @@ struct NodeW {
     vg = ld4(a.g + ucol);
     vbb = ld4(a.bb + ucol);
     vbm = NL == 3 ? ld4(a.bm + ucol) : zero4();
+  }
+  SGNN_DEV void load_out(const Node16Args& a, int b, int j, int g) {
+    const int urow = 16 * b + j, ucol = 16 * b + 4 * g;
     vbmd = zero4();
     vbo = zero4();
     if (MODE == 0) {  // next edge MLP: u = W1_i x + b1 (cols 0..H), v = W1_j x (cols H..2H)
@@ -196,6 +211,9 @@ SGNN_DEV int dpp_row_shl1(int v, int fill) { return __builtin_amdgcn_update_dpp(
 // units 16 t + 4 g + c of item j in acc[t][c]); A rows from an LDS image
 // [H][LDX]; B = x (the same tile layout: tile q supplies k = 16 q + 4 g + c).
 // Four independent accumulator chains, so the MFMAs issue back to back.
+// TR: the same products with the operands swapped, y^T = x^T W^T: lane (j, g) then holds
+// y[unit 16 t + j][item 4 g + c] (units on the lane's row position, items on its column group).
+template <bool TR = false>
 SGNN_DEV void mm_full(f32x4 (&acc)[KQ], const float* Wl, const f32x4 (&x)[KQ], int j, int g) {
   f32x4 w[2][KQ];  // the A rows of k-group q + 1 are read while group q multiplies
 #pragma unroll
@@ -210,7 +228,8 @@ SGNN_DEV void mm_full(f32x4 (&acc)[KQ], const float* Wl, const f32x4 (&x)[KQ], i
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int t = 0; t < KQ; ++t) acc[t] = mfma16(w[q & 1][t][c], x[q][c], acc[t]);
+      for (int t = 0; t < KQ; ++t)
+        acc[t] = TR ? mfma16(x[q][c], w[q & 1][t][c], acc[t]) : mfma16(w[q & 1][t][c], x[q][c], acc[t]);
     __builtin_amdgcn_sched_barrier(0);
   }
 }

@@ -62,7 +62,7 @@ SGNN_DEV void st4_sc1(__amdgpu_buffer_rsrc_t rs, int voff, f32x4 v) {
 
 // LDS carve (floats), shared with the host's size query.
 struct Carve {
-  int sw0, sw1, svec, sxw, sxv, scratch, xs, tb, region, ints, total;  // float offsets / count
+  int sw0, sw1, svec, sxw, sxv, scratch, xs, region, ints, total;  // float offsets / count
   int region_floats;
 };
 SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
@@ -75,7 +75,6 @@ SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
   c.sxv = o; o += 4 * H;          // Encoder.edge_fn b1, b2, gamma, beta
   c.scratch = o; o += 4 * 16 * LDX;  // per-wave receiver sums; node-phase exchange buffers
   c.xs = o; o += 16 * LDX;        // x rows of the tile's nodes (resident for the step)
-  c.tb = o; o += 4 * H * 20;      // per-wave [unit][edge] tiles of the MFMA receiver sums (kTB = 20)
   const int e0f = e0g ? 0 : nt * cap * LDX, posf = n * dim;
   c.region_floats = e0f > posf ? e0f : posf;  // positions (radius phase), then e0 rows (unless in HBM)
   c.region = o; o += (c.region_floats + 3) & ~3;
@@ -87,12 +86,16 @@ SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
 }
 
 // Experiment builds (-DSGNN_PROBE, tools/exp_probe_step16.py): per-wave s_memtime marks at the phase
-// boundaries, [workgroup][wave][32] into the buffer set by sgnn_set_probe16.
+// boundaries, [workgroup][wave][64] into the buffer set by sgnn_set_probe16.  Slots: 0 start, 1 radius done,
+// 2 encoder done; layer k < 5 at 3 + 8 k + (0 start, 1 node weights requested, 2 published, 3 pre-wait done,
+// 4 wait done, 5 edge phase done, 6 node tail done, 7 end); layer 1's halves at 48 + (0 gathers issued,
+// 1.. after each), its node phase at 52 (sums read), 53 (first Linear).
 #ifdef SGNN_PROBE
 __device__ uint64_t* g_probe16;
 SGNN_DEV void mark(int slot) {
   const uint64_t t = __builtin_amdgcn_s_memtime();
-  if (g_probe16 && lane_id() == 0) g_probe16[((int64_t)blockIdx.x * kWaves16 + wave_id()) * 32 + slot] = t;
+  if (g_probe16 && lane_id() == 0 && slot >= 0 && slot < 64)
+    g_probe16[((int64_t)blockIdx.x * kWaves16 + wave_id()) * 64 + slot] = t;
 }
 #else
 SGNN_DEV void mark(int) {}
@@ -186,51 +189,79 @@ SGNN_DEV void step_tail(const Step16Args& a, const NodeW<2, MODE>& W, float* scr
   }
 }
 
-// The receiver sums of one 16-edge half on the matrix cores.  The last
-// Linear's output y (D layout: lane (edge j, g) holds units 16 t + 4 g + c) is
-// LayerNorm'd (graph_network.py:197-198), written to this wave's LDS tile
-// tb [unit][edge] (row stride kTB: conflict-free both ways), and
+// Sum of v over the 16 lanes of each row (DPP: xor 1, xor 2, half mirror, mirror); every lane of the
+// row ends with the same value.
+template <int C>
+SGNN_DEV float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), C, 0xf, 0xf, false));
+}
+SGNN_DEV float row_sum16(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  return v;
+}
+
+// The last Linear of the edge MLP, its LayerNorm and the receiver sums of one
+// 16-edge half, with no transposition through LDS.  The Linear runs with its
+// operands swapped (mm_full<true>): lane (j, g) receives y[unit 16 t + j][edge
+// 4 g + c], so each edge's LayerNorm statistics (graph_network.py:197-198) are
+// an in-lane sum over t plus a 16-lane row sum, and the LayerNorm'd messages m
+// are already the A operand of
 //   agg[unit][recv] += m[unit][edge] S[edge][recv],   S = the half's 0/1 receiver incidence
-// runs as 16 v_mfma_f32_16x16x4_f32 (A = m read back [unit][4 edges], B = S
-// built from the half's receiver ids): the segmented sum becomes 16 MFMAs
-// instead of ~200 DPP / select / add instructions plus an LDS read-modify-write
-// per half, and the wave's aggregates stay in registers across its halves.
-// Receiver r of the tile is column r - i0 (< 16); padding edges have S = 0.
-constexpr int kTB = 20;   // tb row stride (floats): lanes of a b128 read hit disjoint banks
-SGNN_DEV void half_agg(const f32x4 (&y)[KQ], f32x4 (&agg)[KQ], const float* svec, float* tb, const int32_t* lrecv,
-                       int hs, int Et, int i0, int j, int g, int l) {
-  float mu, rs;
-  ln_stats(y, mu, rs);
-  const bool ev = hs + j < Et;
+// (16 v_mfma_f32_16x16x4_f32, B = S built from the half's receiver ids): the
+// segmented sum runs on the matrix cores and the wave's aggregates stay in
+// registers across its halves.  Receiver r of the tile is column r - i0 (< 16);
+// padding edges have S = 0 (their rows are clamped copies, finite).
+// ep: edge bias b2 / gamma / beta of the lane's units 16 t + j.
+struct EdgeVec {
+  float b2[KQ], ga[KQ], be[KQ];
+};
+SGNN_DEV void edge_out(const f32x4 (&acc)[KQ], f32x4 (&agg)[KQ], const float* sw1, const EdgeVec& ev,
+                       const int32_t* lrecv, int hs, int Et, int i0, int j, int g) {
+  f32x4 x[KQ], y[KQ];
 #pragma unroll
   for (int t = 0; t < KQ; ++t) {
-    const f32x4 ga = ld4(svec + H + 16 * t + 4 * g), be = ld4(svec + 2 * H + 16 * t + 4 * g);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      tb[(16 * t + 4 * g + c) * kTB + j] = ev ? (y[t][c] - mu) * rs * ga[c] + be[c] : 0.0f;
+    x[t] = relu4(acc[t]);
+    y[t] = f32x4{ev.b2[t], ev.b2[t], ev.b2[t], ev.b2[t]};
   }
-  // B: lane (k = l >> 4, col = l & 15) supplies S[edge 4k + s][col] for step s = 0..3 (the K order of A)
-  const int kk = l >> 4, col = l & 15;
+  mm_full<true>(y, sw1, x, j, g);
+  // two-pass statistics per edge 4 g + c (torch: biased variance, eps 1e-5)
+  f32x4 mu = (y[0] + y[1]) + (y[2] + y[3]);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) mu[c] = row_sum16(mu[c]) * (1.0f / H);
+  f32x4 d[KQ], var = zero4();
+#pragma unroll
+  for (int t = 0; t < KQ; ++t) {
+    d[t] = y[t] - mu;
+    var += d[t] * d[t];
+  }
+  f32x4 rs;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) rs[c] = __builtin_amdgcn_rsqf(row_sum16(var[c]) * (1.0f / H) + 1e-5f);
+  // B: lane (col j, k = g) supplies S[edge 4 g + s][recv i0 + j] for step s = 0..3
   typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const i32x4 rv = *reinterpret_cast<const i32x4*>(lrecv + hs + 4 * kk);
+  const i32x4 rv = *reinterpret_cast<const i32x4*>(lrecv + hs + 4 * g);
   float sb[4];
 #pragma unroll
-  for (int s2 = 0; s2 < 4; ++s2) sb[s2] = (hs + 4 * kk + s2 < Et && rv[s2] - i0 == col) ? 1.0f : 0.0f;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int s2 = 0; s2 < 4; ++s2) sb[s2] = (hs + 4 * g + s2 < Et && rv[s2] - i0 == j) ? 1.0f : 0.0f;
 #pragma unroll
   for (int t = 0; t < KQ; ++t) {
-    const f32x4 av = ld4(tb + (16 * t + col) * kTB + 4 * kk);  // A: lane (unit col, k) = m[unit][4k .. 4k+3]
+    const f32x4 m = d[t] * rs * ev.ga[t] + ev.be[t];  // A: lane (unit j, k = g) = m[unit 16 t + j][edge 4 g + s]
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) agg[t] = mfma16(av[s2], sb[s2], agg[t]);
+    for (int s2 = 0; s2 < 4; ++s2) agg[t] = mfma16(m[s2], sb[s2], agg[t]);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();   // tb is rewritten by the next half
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 constexpr int kPre = 3;   // halves per wave whose W1e e0 product runs before the wait
+// The tile publishes the node halves its previous stage stored after this many of those products: the
+// drain of the write-through stores overlaps them (SGNN_PUB_AT: experiment builds)
+#ifndef SGNN_PUB_AT
+#define SGNN_PUB_AT 1
+#endif
+constexpr int kPubAt = SGNN_PUB_AT;
+static_assert(kPubAt >= 0 && kPubAt <= kPre, "publish point within the pre-wait");
 
 // The edge MLP of a layer, split around the wait for the sender tiles.  Wave b
 // takes the 16-edge halves b, b + 4, ... of the compacted tile CSR.  The first
@@ -243,7 +274,7 @@ constexpr int kPre = 3;   // halves per wave whose W1e e0 product runs before th
 struct EdgePhase {
   const Step16Args& a;
   const float *sw0, *sw1, *svec, *sxw, *sxv;
-  float *sums, *tb, *e0l;
+  float *sums, *e0l;
   const int32_t *lsend, *lrecv;
   int Et, i0, b, j, g, l;
   f32x4 pre[kPre][KQ];
@@ -290,8 +321,10 @@ struct EdgePhase {
   }
 
   // before the wait: (FIRST) e0 of every half; W1e e0 of the first kPre halves
-  template <bool FIRST>
-  SGNN_DEV void prewait(const float (&xw1)[KQ]) {
+  // hook(m) runs before the wave's half m (m = 0 .. kPre - 1) and hook(kPre) after the last: the
+  // caller publishes and requests the node weights there, between the products
+  template <bool FIRST, class Hook>
+  SGNN_DEV void prewait(const float (&xw1)[KQ], Hook&& hook) {
     const float* pos = a.pos_last ? a.pos_last : a.pos_seq + (int64_t)(a.T - 1) * a.dim;
     const int pstride = a.pos_last ? a.dim : a.T * a.dim;
     float ps_n[3] = {0.0f, 0.0f, 0.0f}, pr_n[3] = {0.0f, 0.0f, 0.0f};
@@ -309,7 +342,8 @@ struct EdgePhase {
 #pragma unroll
     for (int m = 0; m < kPre; ++m) {
       const int hs = 16 * b + 16 * kWaves16 * m;
-      if (hs >= Et) break;
+      hook(m);
+      if (hs >= Et) continue;
       f32x4 x[KQ];
       if constexpr (FIRST) {
         float ps[3], pr[3];
@@ -327,6 +361,7 @@ struct EdgePhase {
       for (int t = 0; t < KQ; ++t) pre[m][t] = zero4();
       mm_full(pre[m], sw0, x, j, g);
     }
+    hook(kPre);
     if constexpr (FIRST) {  // the rest of the halves: e0 rows only
       for (int hs = 16 * b + 16 * kWaves16 * kPre; hs < Et; hs += 16 * kWaves16) {
         float ps[3], pr[3];
@@ -348,43 +383,47 @@ struct EdgePhase {
     f32x4 agg[KQ];
 #pragma unroll
     for (int t = 0; t < KQ; ++t) agg[t] = zero4();
-    f32x4 uv_n[KQ];
+    // the raw u / v rows of the next half stay in flight across the current half's MFMAs: summing them
+    // here would put a wait for the loads just issued in front of those MFMAs
+    f32x4 gu[KQ], gv[KQ];
     auto gather = [&](int hs) {  // clamped: harmless past the end
       const int e = hs + j, ec = e < Et ? e : Et - 1;
       const int r = lrecv[ec], s = lsend[ec];
 #pragma unroll
-      for (int t = 0; t < KQ; ++t)
-        uv_n[t] = ld4_sc1(ru, r * (H * 4) + (16 * t + 4 * g) * 4) + ld4_sc1(rv, s * (H * 4) + (16 * t + 4 * g) * 4);
-    };
-    auto finish = [&](f32x4 (&acc)[KQ], int hs) {  // ReLU -> last Linear -> LayerNorm -> sums
-      f32x4 x[KQ], y[KQ];
-#pragma unroll
       for (int t = 0; t < KQ; ++t) {
-        x[t] = relu4(acc[t]);
-        y[t] = ld4(svec + 16 * t + 4 * g);
+        gu[t] = ld4_sc1(ru, r * (H * 4) + (16 * t + 4 * g) * 4);
+        gv[t] = ld4_sc1(rv, s * (H * 4) + (16 * t + 4 * g) * 4);
       }
-      mm_full(y, sw1, x, j, g);
-      half_agg(y, agg, svec, tb, lrecv, hs, Et, i0, j, g, l);
+    };
+    EdgeVec ev;
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) {
+      ev.b2[t] = svec[16 * t + j];
+      ev.ga[t] = svec[H + 16 * t + j];
+      ev.be[t] = svec[2 * H + 16 * t + j];
+    }
+    auto finish = [&](f32x4 (&acc)[KQ], int hs) {  // ReLU -> last Linear -> LayerNorm -> sums
+      edge_out(acc, agg, sw1, ev, lrecv, hs, Et, i0, j, g);
     };
     int hs = 16 * b;
     if (hs < Et) gather(hs);
-    if (probe) mark(28);
+    if (probe) mark(48);
 #pragma unroll
     for (int m = 0; m < kPre; ++m) {
       if (hs >= Et) break;
       f32x4 acc[KQ];
 #pragma unroll
-      for (int t = 0; t < KQ; ++t) acc[t] = pre[m][t] + uv_n[t];
+      for (int t = 0; t < KQ; ++t) acc[t] = pre[m][t] + (gu[t] + gv[t]);
       gather(hs + 16 * kWaves16);
       finish(acc, hs);
-      if (probe) mark(29 + m);
+      if (probe) mark(49 + m);
       hs += 16 * kWaves16;
     }
     for (; hs < Et; hs += 16 * kWaves16) {   // halves past kPre: the e0 product here
       f32x4 x[KQ], acc[KQ];
       ld_e0(x, hs);
 #pragma unroll
-      for (int t = 0; t < KQ; ++t) acc[t] = uv_n[t];
+      for (int t = 0; t < KQ; ++t) acc[t] = gu[t] + gv[t];
       gather(hs + 16 * kWaves16);
       mm_full(acc, sw0, x, j, g);
       finish(acc, hs);
@@ -395,18 +434,33 @@ struct EdgePhase {
 };
 
 // Stage an edge MLP's LDS images: W1e (columns 2H..3H of W1, x scale) and W2 + vectors.
+// Up to four H-vectors, one element per thread (wave b holds vector b): requested with the matrices, so
+// the LDS images are written without a load round trip of their own.
+struct VecStage {
+  float v;
+  SGNN_DEV void load(const float* p0, const float* p1, const float* p2, const float* p3) {
+    const int b = threadIdx.x / 64;
+    const float* p = b == 0 ? p0 : b == 1 ? p1 : b == 2 ? p2 : p3;
+    v = p ? p[threadIdx.x & 63] : 0.0f;
+  }
+  SGNN_DEV void store(float* dst, int nvec) const {
+    if ((int)threadIdx.x < nvec * H) dst[threadIdx.x] = v;
+  }
+};
+static_assert(kBlock16 == 4 * H, "VecStage: one element per thread");
+
 struct EdgeStage {
   f32x4 w1e[kStagePer], w2[kStagePer];
+  VecStage vec;
   SGNN_DEV void load(const Lay16& L) {
     stage_w64_load(w1e, L.ew1 + 2 * H, 3 * H);
     stage_w64_load(w2, L.ew2, H);
+    vec.load(L.eb2, L.eg, L.ebb, nullptr);
   }
-  SGNN_DEV void store(float* sw0, float* sw1, float* svec, const Lay16& L, float scale) const {
+  SGNN_DEV void store(float* sw0, float* sw1, float* svec, float scale) const {
     stage_w64_store(sw0, w1e, scale);
     stage_w64_store(sw1, w2, 1.0f);
-    stage_vec(svec, L.eb2, H, H);
-    stage_vec(svec + H, L.eg, H, H);
-    stage_vec(svec + 2 * H, L.ebb, H, H);
+    vec.store(svec, 3);
   }
 };
 
@@ -453,7 +507,6 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   float* svec = lds + cv.svec;
   float* scratch = lds + cv.scratch;
   float* xs = lds + cv.xs;
-  float* tb = lds + cv.tb + b * H * kTB;
   const int64_t nH = (int64_t)a.n * H;
   // e0 rows of the tile's edges: LDS, or (graphs whose tile does not fit) a per-tile HBM block behind
   // the layers' node halves -- written and read by this workgroup only
@@ -463,17 +516,30 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   // this layer's node weights (VGPR-resident) are requested first: the W1e e0 products and the wait
   // for the sender tiles hide their latency (this layer's edge weights were staged in LDS before the
   // previous layer published)
+  const int ps = k < 5 ? 3 + 8 * k : -1;  // probe slots of this layer
+  mark(ps);
   NodeW<2, MODE> W;
-  W.load(node_args(a, Lk, MODE == 0 ? &Ln : nullptr), b, j, g);
+  const Node16Args nd = node_args(a, Lk, MODE == 0 ? &Ln : nullptr);
   float* sums = scratch + b * 16 * LDX;
-  EdgePhase ep{a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, sums, tb, e0l, lsend, lrecv, Et, i0, b, j, g, l};
-  mark(3 + 5 * k);
-  ep.template prewait<FIRST>(xw1);
-  mark(4 + 5 * k);
+  EdgePhase ep{a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, sums, e0l, lsend, lrecv, Et, i0, b, j, g, l};
+  mark(ps < 0 ? -1 : ps + 1);
+  // Between the pre-wait products: publish phase k + 1 (u_k / v_k, stored by the previous stage; the
+  // drain of those write-through stores overlaps the first product), then request this layer's node
+  // weights (VGPR-resident) in three parts, so neither the drain nor the load issue stalls the MFMAs.
+  ep.template prewait<FIRST>(xw1, [&](int m) {
+    if (m == kPubAt) {
+      publish(a.flags, tile, a.epoch0 + (uint32_t)k + 1);
+      mark(ps < 0 ? -1 : ps + 2);
+      W.load_first(nd, b, j, g);
+    }
+    if (m == (kPubAt + 1 < kPre ? kPubAt + 1 : kPre)) W.load_mid(nd, b, j, g);
+    if (m == (kPubAt + 2 < kPre ? kPubAt + 2 : kPre)) W.load_out(nd, b, j, g);
+  });
+  mark(ps < 0 ? -1 : ps + 3);
   wait_tiles(deps, ndeps, a.flags, a.epoch0 + (uint32_t)k + 1, b, l);
-  mark(5 + 5 * k);
+  mark(ps < 0 ? -1 : ps + 4);
   ep.postwait(ru, rv, k == 1);
-  mark(6 + 5 * k);
+  mark(ps < 0 ? -1 : ps + 5);
   __syncthreads();
   // the next layer's edge weights: requested now, staged in LDS before this layer publishes
   EdgeStage nxt;
@@ -490,18 +556,22 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   for (int q = 0; q < KQ; ++q) xr[q] = ld4(xs + j * LDX + 16 * q + 4 * g);
   const f32x4 xo = ld4(xs + j * LDX + 16 * b + 4 * g);
   __syncthreads();  // the exchange buffers alias the sums
+  if (k == 1) mark(52);
   const bool valid = j < cnt;
   const int64_t i = i0 + j;
   const f32x4 h = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));  // graph_network.py:220
+  if (k == 1) mark(53);
   if constexpr (MODE == 0) {
     const __amdgpu_buffer_rsrc_t ru1 = buf_rsrc(a.uvl + (2 * k + 2) * nH), rv1 = buf_rsrc(a.uvl + (2 * k + 3) * nH);
     step_tail<0>(a, W, scratch, xs, i, valid, h, xo, b, j, g, ru1, rv1);
-    nxt.store(sw0, sw1, svec, Ln, (float)(2 << k));  // W1e x 2^(k+1): exact
-    mark(7 + 5 * k);
-    publish(a.flags, tile, a.epoch0 + (uint32_t)k + 2);
+    mark(ps < 0 ? -1 : ps + 6);
+    nxt.store(sw0, sw1, svec, (float)(2 << k));  // W1e x 2^(k+1): exact
+    __syncthreads();  // the next layer's pre-wait reads the staged weights; it publishes u_{k+1} / v_{k+1}
+    mark(ps < 0 ? -1 : ps + 7);
   } else {
     step_tail<1>(a, W, scratch, xs, i, valid, h, xo, b, j, g, ru, rv);
-    mark(7 + 5 * k);
+    mark(ps < 0 ? -1 : ps + 6);
+    mark(ps < 0 ? -1 : ps + 7);
   }
 }
 
@@ -553,6 +623,8 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   st0.load(a.lay[0]);
   f32x4 sx[kStagePer];
   stage_w64_load(sx, a.xe_w2, H);
+  VecStage sxv;
+  sxv.load(a.xe_b1, a.xe_b2, a.xe_g, a.xe_bb);
   NodeW<2, 0> E;
   f32x4 w1f[KQF];
   f32x4 vb1;
@@ -622,12 +694,9 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   }
   mark(1);
   // LDS images of the staged weights (the radius phase never touches them)
-  st0.store(lds + cv.sw0, lds + cv.sw1, lds + cv.svec, a.lay[0], 1.0f);
+  st0.store(lds + cv.sw0, lds + cv.sw1, lds + cv.svec, 1.0f);
   stage_w64_store(lds + cv.sxw, sx, 1.0f);
-  stage_vec(lds + cv.sxv, a.xe_b1, H, H);
-  stage_vec(lds + cv.sxv + H, a.xe_b2, H, H);
-  stage_vec(lds + cv.sxv + 2 * H, a.xe_g, H, H);
-  stage_vec(lds + cv.sxv + 3 * H, a.xe_bb, H, H);
+  sxv.store(lds + cv.sxv, 4);
   __syncthreads();
   // tile CSR (receiver-sorted, senders ascending) from the kept lists; sender-tile mask
   if (b == 0) {
@@ -702,8 +771,7 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     const int64_t nH = (int64_t)n * H;
     step_tail<0>(a, E, lds + cv.scratch, lds + cv.xs, i, valid, h, zero4(), b, j, g, buf_rsrc(a.uvl),
                  buf_rsrc(a.uvl + nH));
-    publish(a.flags, tile, a.epoch0 + 1);
-    mark(2);
+    mark(2);  // u_0 / v_0 are published by layer 0's pre-wait
   }
 
   // ---- the interaction layers ------------------------------------------------------------------

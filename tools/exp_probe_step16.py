@@ -35,29 +35,45 @@ assert one, "workload does not take the one-launch step"
 for _ in range(20):
     runner.run(w0)
 torch.cuda.synchronize()
-buf = torch.zeros(grid * 4 * 32, dtype=torch.int64, device=dev)
+buf = torch.zeros(grid * 4 * 64, dtype=torch.int64, device=dev)
 lib = _hip.lib()
 lib.sgnn_set_probe16.argtypes = [ctypes.c_void_p]
 lib.sgnn_set_probe16(ctypes.c_void_p(buf.data_ptr()))
 runner.run(w0)
 torch.cuda.synchronize()
 lib.sgnn_set_probe16(ctypes.c_void_p(0))
-t = buf.view(grid * 4, 32).cpu().numpy().astype(np.float64)
-last = 7 + 5 * (L - 1)
-print(f"{wl}: n={n} grid={grid} nt={nt}; wave life p50/p90/max "
+t = buf.view(grid * 4, 64).cpu().numpy().astype(np.float64)
+nl = min(L, 5)
+last = 3 + 8 * (nl - 1) + 7
+print(f"{wl}: n={n} grid={grid} nt={nt} L={L}; wave life (to layer {nl - 1}'s end) p50/p90/max "
       f"{np.percentile(t[:, last] - t[:, 0], [50, 90, 100]).round()} cycles (s_memtime)")
-names = [(0, 1, "radius search"), (1, 2, "stage + CSR + encoder")]
-for k in range(L):
-    names += [(2 if k == 0 else 7 + 5 * (k - 1), 3 + 5 * k, f"L{k} publish + loads"),
-              (3 + 5 * k, 4 + 5 * k, f"L{k} pre-wait W1e e0"), (4 + 5 * k, 5 + 5 * k, f"L{k} wait"),
-              (5 + 5 * k, 6 + 5 * k, f"L{k} edge phase"), (6 + 5 * k, 7 + 5 * k, f"L{k} node phase")]
-for a, b, nm in names:
-    d = t[:, b] - t[:, a]
-    print(f"  {nm:24s} p10 {np.percentile(d, 10):8.0f}  p50 {np.percentile(d, 50):8.0f}  p90 {np.percentile(d, 90):8.0f}"
-          f"  max {d.max():8.0f}")
-print("layer 1 edge phase per half (waves with 3 halves):")
-three = t[:, 31] > 0
-for a, b, nm in [(5 + 5, 28, "gather issue"), (28, 29, "half 0"), (29, 30, "half 1"), (30, 31, "half 2")]:
-    sel = three if b == 31 else np.ones(t.shape[0], bool)
+
+
+def show(a, b, nm, sel=None):
+    sel = np.ones(t.shape[0], bool) if sel is None else sel
     d = t[sel, b] - t[sel, a]
-    print(f"  {nm:24s} p10 {np.percentile(d, 10):8.0f}  p50 {np.percentile(d, 50):8.0f}  p90 {np.percentile(d, 90):8.0f}")
+    print(f"  {nm:28s} p10 {np.percentile(d, 10):8.0f}  p50 {np.percentile(d, 50):8.0f}  p90 {np.percentile(d, 90):8.0f}"
+          f"  max {d.max():8.0f}")
+
+
+show(0, 1, "radius search")
+show(1, 2, "stage + CSR + encoder")
+for k in range(nl):
+    s0 = 3 + 8 * k
+    show(2 if k == 0 else s0 - 1, s0, f"L{k} layer boundary")
+    show(s0, s0 + 1, f"L{k} node weights requested")
+    show(s0 + 1, s0 + 2, f"L{k} pre-wait to publish")
+    show(s0 + 2, s0 + 3, f"L{k} pre-wait rest")
+    show(s0 + 3, s0 + 4, f"L{k} wait")
+    show(s0 + 4, s0 + 5, f"L{k} edge phase")
+    show(s0 + 5, s0 + 6, f"L{k} node phase")
+    show(s0 + 6, s0 + 7, f"L{k} stage + barrier")
+print("layer 1 detail:")
+three = t[:, 51] > 0
+show(3 + 8 + 4, 48, "gather issue")
+show(48, 49, "half 0")
+show(49, 50, "half 1")
+show(50, 51, "half 2", three)
+show(3 + 8 + 5, 52, "node: sums + barriers")
+show(52, 53, "node: first Linear")
+show(53, 3 + 8 + 6, "node: tail")
