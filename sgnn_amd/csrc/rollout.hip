@@ -38,7 +38,8 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   const int d = in->dim, T = in->T;
   const int cap = in->K;  // predict_positions keeps self loops (learned_simulator.py:75,117)
   if (L < 2 || L > kStep16MaxL || n < 1 || n > kStep16MaxGrid * kStep16MaxNT || d < 1 || d > 3 || T < 2 ||
-      cap < 1 || cap > kStep16MaxCap || in->n_ex < 1 || !in->ex_ptr || !(in->radius > 0.0f))
+      cap < 1 || cap > kStep16MaxCap || in->n_ex < 1 || in->n_ex > kStep16MaxEx || !in->ex_ptr ||
+      !(in->radius > 0.0f))
     return false;
   const int feat = (T - 1) * d + 1 + (in->use_emb ? in->emb_dim : 0);
   if (feat > 48 || !mlp16(m->enc_node, feat, 64, true) || !mlp16(m->enc_edge, d + 1, 64, true) ||

@@ -10,6 +10,7 @@ constexpr int kStep16MaxL = 10;     // interaction layers carried in the kernel 
 constexpr int kStep16MaxNT = 16;    // receivers per workgroup (one 16-item node tile)
 constexpr int kStep16MaxCap = 64;   // neighbour cap (K, +1 without self loops)
 constexpr int kStep16MaxGrid = 256; // one workgroup per CU, every workgroup resident
+constexpr int kStep16MaxEx = 64;    // examples in the batch (their offsets are staged in LDS)
 constexpr size_t kStep16MaxLds = 160 * 1024;
 
 // Weights of one InteractionNetwork (nmlp_layers 1): edge_fn = Linear(3H, H) ->

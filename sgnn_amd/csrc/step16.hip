@@ -62,7 +62,7 @@ SGNN_DEV void st4_sc1(__amdgpu_buffer_rsrc_t rs, int voff, f32x4 v) {
 
 // LDS carve (floats), shared with the host's size query.
 struct Carve {
-  int sw0, sw1, svec, sxw, sxv, scratch, xs, region, ints, total;  // float offsets / count
+  int sw0, sw1, svec, sxw, sxv, scratch, xs, dbuf, region, ints, total;  // float offsets / count
   int region_floats;
 };
 SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
@@ -75,12 +75,14 @@ SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
   c.sxv = o; o += 4 * H;          // Encoder.edge_fn b1, b2, gamma, beta
   c.scratch = o; o += 4 * 16 * LDX;  // per-wave receiver sums; node-phase exchange buffers
   c.xs = o; o += 16 * LDX;        // x rows of the tile's nodes (resident for the step)
+  c.dbuf = o; o += 2 * KQ * 64 * 4;  // donated pre-wait products (EdgePhase::plan)
   const int e0f = e0g ? 0 : nt * cap * LDX, posf = n * dim;
   c.region_floats = e0f > posf ? e0f : posf;  // positions (radius phase), then e0 rows (unless in HBM)
   c.region = o; o += (c.region_floats + 3) & ~3;
-  // lsend, lrecv [round16(nt*cap)] each, nbr [nt*cap]; deg [16]; pre [20]; mask [8]; kw [4][64]; deps [256] + count
+  // lsend, lrecv [round16(nt*cap)] each, nbr [nt*cap]; deg [16]; pre [20]; mask [8]; kw [4][64]; deps [256] + count;
+  // example offsets [kStep16MaxEx + 1]
   c.ints = o;
-  o += 2 * ((nt * cap + 15) & ~15) + nt * cap + 16 + 20 + 8 + 4 * 64 + sgnn::kStep16MaxGrid + 4;
+  o += 2 * ((nt * cap + 15) & ~15) + nt * cap + 16 + 20 + 8 + 4 * 64 + sgnn::kStep16MaxGrid + 4 + sgnn::kStep16MaxEx + 4;
   c.total = (o + 3) & ~3;
   return c;
 }
@@ -101,17 +103,22 @@ SGNN_DEV void mark(int slot) {
 SGNN_DEV void mark(int) {}
 #endif
 
-// Per-tile counters: wave 0 polls those of the sender tiles `deps` (up to 256, all requested at
-// once), the other waves wait at the barrier.
-SGNN_DEV void wait_tiles(const int32_t* deps, int ndeps, uint32_t* flags, uint32_t epoch, int b, int lane) {
-  if (b == 0) {
-    for (int it = 0;; ++it) {
-      uint32_t v[kMaxGrid / 64];
+// Per-tile counters of the sender tiles `deps` (up to 256, all requested at once).  Every wave polls for
+// itself (no workgroup barrier after the match): `issue` requests the counters early -- before the
+// wave's last pre-wait product, so their round trip overlaps it -- and `wait` checks them and polls
+// on until they match.
+struct TilePoll {
+  uint32_t v[kMaxGrid / 64];
+  SGNN_DEV void issue(const int32_t* deps, int ndeps, const uint32_t* flags, uint32_t epoch, int lane) {
 #pragma unroll
-      for (int q = 0; q < kMaxGrid / 64; ++q)
-        v[q] = lane + 64 * q < ndeps ? __hip_atomic_load((gu32*)(flags + deps[lane + 64 * q]), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                                     : epoch;
+    for (int q = 0; q < kMaxGrid / 64; ++q)
+      v[q] = lane + 64 * q < ndeps
+                 ? __hip_atomic_load((const gu32*)(flags + deps[lane + 64 * q]), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT)
+                 : epoch;
+  }
+  SGNN_DEV void wait(const int32_t* deps, int ndeps, uint32_t* flags, uint32_t epoch, int lane) {
+    for (int it = 0;; ++it) {
       bool ok = true;
 #pragma unroll
       for (int q = 0; q < kMaxGrid / 64; ++q) ok = ok && v[q] >= epoch;
@@ -122,10 +129,10 @@ SGNN_DEV void wait_tiles(const int32_t* deps, int ndeps, uint32_t* flags, uint32
         break;
       }
       __builtin_amdgcn_s_sleep(1);
+      issue(deps, ndeps, flags, epoch, lane);
     }
   }
-  __syncthreads();
-}
+};
 
 // Every storing wave drains its sc1 stores, then one lane publishes the phase.
 SGNN_DEV void publish(uint32_t* flags, int tile, uint32_t epoch) {
@@ -133,6 +140,33 @@ SGNN_DEV void publish(uint32_t* flags, int tile, uint32_t epoch) {
   __syncthreads();
   if (threadIdx.x == 0)
     __hip_atomic_store((gu32*)(flags + tile), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sum over the lanes j, j + 16, j + 32, j + 48 (the column groups holding one item's units): two
+// cross-row swaps on the VALU instead of two LDS permute round trips.
+SGNN_DEV float xg_sum(float v) {
+  // v_permlane32_swap / v_permlane16_swap exchange lanes between two registers (both written): with
+  // both holding v, their sum is the sum over lanes l and l ^ 32, then l and l ^ 16.  Inline: this
+  // compiler's builtins for them return the first register twice.  s_nop: VALU -> permlane hazards.
+  float p = v, q = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(p), "+v"(q));
+  v = p + q;
+  p = v;
+  q = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(p), "+v"(q));
+  return p + q;
+}
+// LayerNorm statistics of full rows held as in ln_stats (two-pass, biased variance, eps 1e-5)
+SGNN_DEV void ln_stats_x(const f32x4 (&r)[KQ], float& mean, float& rstd) {
+  f32x4 p = (r[0] + r[1]) + (r[2] + r[3]);
+  mean = xg_sum((p[0] + p[1]) + (p[2] + p[3])) * (1.0f / H);
+  f32x4 v = zero4();
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const f32x4 d = r[q] - mean;
+    v += d * d;
+  }
+  rstd = __builtin_amdgcn_rsqf(xg_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / H) + 1e-5f);
 }
 
 // Node update of the tile (16 item rows, `valid` rows written) from the first
@@ -149,7 +183,7 @@ SGNN_DEV void step_tail(const Step16Args& a, const NodeW<2, MODE>& W, float* scr
   const f32x4 y = mm(W.vb2, W.w2, hr);
   xchg(scratch + 16 * LDX, j, ucol, g, y, yr);
   float mean, rstd;
-  ln_stats(yr, mean, rstd);
+  ln_stats_x(yr, mean, rstd);
   f32x4 xn;
 #pragma unroll
   for (int c = 0; c < 4; ++c) xn[c] = (y[c] - mean) * rstd * W.vg[c] + W.vbb[c] + xo[c];  // LN (+ :176 residual)
@@ -203,6 +237,52 @@ SGNN_DEV float row_sum16(float v) {
   return v;
 }
 
+// Edge bias b2 / gamma / beta of the lane's units 16 t + j (the swapped-operand layout below).
+struct EdgeVec {
+  float b2[KQ], ga[KQ], be[KQ];
+};
+
+// The LayerNorm + receiver sums of one half's y in four parts: 0 means, 1 deviations + variances,
+// 2 scales + incidence + messages, 3 the 16 aggregation MFMAs.  (Interleaving them with the next
+// half's MFMAs gains nothing: f32 MFMA occupies most of the SIMD's VALU, tools/exp/mfma_valu_overlap.hip.)
+struct LnAgg {
+  f32x4 d[KQ], mu, var;
+  float sb[4];
+  SGNN_DEV void part(int p, const f32x4 (&y)[KQ], f32x4 (&agg)[KQ], const EdgeVec& ev, const int32_t* lrecv,
+                     int hs, int Et, int i0, int j, int g) {
+    if (p == 0) {  // two-pass statistics per edge 4 g + c (torch: biased variance, eps 1e-5)
+      mu = (y[0] + y[1]) + (y[2] + y[3]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) mu[c] = row_sum16(mu[c]) * (1.0f / H);
+    } else if (p == 1) {
+      var = zero4();
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) {
+        d[t] = y[t] - mu;
+        var += d[t] * d[t];
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) var[c] = row_sum16(var[c]);
+    } else if (p == 2) {
+      f32x4 rs;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) rs[c] = __builtin_amdgcn_rsqf(var[c] * (1.0f / H) + 1e-5f);
+      // B: lane (col j, k = g) supplies S[edge 4 g + s][recv i0 + j] for step s = 0..3
+      typedef int i32x4 __attribute__((ext_vector_type(4)));
+      const i32x4 rv = *reinterpret_cast<const i32x4*>(lrecv + hs + 4 * g);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) sb[s2] = (hs + 4 * g + s2 < Et && rv[s2] - i0 == j) ? 1.0f : 0.0f;
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) d[t] = d[t] * rs * ev.ga[t] + ev.be[t];  // m (A: lane (unit j, k = g))
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)  // the four accumulators in turn: no dependent back-to-back MFMAs
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) agg[t] = mfma16(d[t][s2], sb[s2], agg[t]);
+    }
+  }
+};
+
 // The last Linear of the edge MLP, its LayerNorm and the receiver sums of one
 // 16-edge half, with no transposition through LDS.  The Linear runs with its
 // operands swapped (mm_full<true>): lane (j, g) receives y[unit 16 t + j][edge
@@ -214,43 +294,12 @@ SGNN_DEV float row_sum16(float v) {
 // segmented sum runs on the matrix cores and the wave's aggregates stay in
 // registers across its halves.  Receiver r of the tile is column r - i0 (< 16);
 // padding edges have S = 0 (their rows are clamped copies, finite).
-// ep: edge bias b2 / gamma / beta of the lane's units 16 t + j.
-struct EdgeVec {
-  float b2[KQ], ga[KQ], be[KQ];
-};
-SGNN_DEV void edge_out(const f32x4 (&acc)[KQ], f32x4 (&agg)[KQ], const float* sw1, const EdgeVec& ev,
-                       const int32_t* lrecv, int hs, int Et, int i0, int j, int g) {
-  f32x4 x[KQ], y[KQ];
+// lin2: ReLU + the Linear (y, before the LayerNorm); the LnAgg parts finish a half.
+SGNN_DEV void lin2_init(const f32x4 (&acc)[KQ], f32x4 (&x)[KQ], f32x4 (&y)[KQ], const EdgeVec& ev) {
 #pragma unroll
   for (int t = 0; t < KQ; ++t) {
     x[t] = relu4(acc[t]);
     y[t] = f32x4{ev.b2[t], ev.b2[t], ev.b2[t], ev.b2[t]};
-  }
-  mm_full<true>(y, sw1, x, j, g);
-  // two-pass statistics per edge 4 g + c (torch: biased variance, eps 1e-5)
-  f32x4 mu = (y[0] + y[1]) + (y[2] + y[3]);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) mu[c] = row_sum16(mu[c]) * (1.0f / H);
-  f32x4 d[KQ], var = zero4();
-#pragma unroll
-  for (int t = 0; t < KQ; ++t) {
-    d[t] = y[t] - mu;
-    var += d[t] * d[t];
-  }
-  f32x4 rs;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) rs[c] = __builtin_amdgcn_rsqf(row_sum16(var[c]) * (1.0f / H) + 1e-5f);
-  // B: lane (col j, k = g) supplies S[edge 4 g + s][recv i0 + j] for step s = 0..3
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const i32x4 rv = *reinterpret_cast<const i32x4*>(lrecv + hs + 4 * g);
-  float sb[4];
-#pragma unroll
-  for (int s2 = 0; s2 < 4; ++s2) sb[s2] = (hs + 4 * g + s2 < Et && rv[s2] - i0 == j) ? 1.0f : 0.0f;
-#pragma unroll
-  for (int t = 0; t < KQ; ++t) {
-    const f32x4 m = d[t] * rs * ev.ga[t] + ev.be[t];  // A: lane (unit j, k = g) = m[unit 16 t + j][edge 4 g + s]
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) agg[t] = mfma16(m[s2], sb[s2], agg[t]);
   }
 }
 
@@ -261,7 +310,7 @@ constexpr int kPre = 3;   // halves per wave whose W1e e0 product runs before th
 #define SGNN_PUB_AT 1
 #endif
 constexpr int kPubAt = SGNN_PUB_AT;
-static_assert(kPubAt >= 0 && kPubAt <= kPre, "publish point within the pre-wait");
+static_assert(kPubAt >= 1 && kPubAt <= kPre, "publish point within the pre-wait, after the donated product");
 
 // The edge MLP of a layer, split around the wait for the sender tiles.  Wave b
 // takes the 16-edge halves b, b + 4, ... of the compacted tile CSR.  The first
@@ -303,7 +352,7 @@ struct EdgePhase {
     }
     mm_full(y, sxw, hx, j, g);
     float mu, rs;
-    ln_stats(y, mu, rs);
+    ln_stats_x(y, mu, rs);
     const int e = hs + j;
 #pragma unroll
     for (int t = 0; t < KQ; ++t) {
@@ -321,58 +370,104 @@ struct EdgePhase {
   }
 
   // before the wait: (FIRST) e0 of every half; W1e e0 of the first kPre halves
-  // hook(m) runs before the wave's half m (m = 0 .. kPre - 1) and hook(kPre) after the last: the
-  // caller publishes and requests the node weights there, between the products
-  template <bool FIRST, class Hook>
+  // Balance of the pre-wait products: with NH halves in the tile, F = NH / 4 full rounds and r = NH % 4
+  // in {1, 2} (and F < kPre), waves b < r own F + 1 halves and the others F.  Then wave r + i (i < r)
+  // forms the W1e e0 product of wave i's last half (its first product, into dbuf before the publish
+  // barrier; FIRST: it also encodes that half's e0 rows), so every wave runs at most F + 1 products
+  // before the wait and the owner reads the donated one after it.
+  int F = 0, r = 0;
+  bool donor = false, owner_d = false;
+  int hd = -1;
+  float* dbuf = nullptr;   // [2][KQ][64] f32x4 donated products
+  SGNN_DEV void plan(float* dbuf_) {
+    const int NH = (Et + 15) / 16;
+    F = NH / 4;
+    r = NH % 4;
+    const bool don = (r == 1 || r == 2) && F + 1 <= kPre;
+    owner_d = don && b < r;
+    donor = don && b >= r && b - r < r;
+    hd = donor ? 16 * (kWaves16 * F + (b - r)) : -1;
+    dbuf = dbuf_;
+  }
+  // the wave's k-th product / encode item: the donated half first (donor), then its own halves;
+  // -1 skips an own half whose product runs on the donor, -2 ends the list
+  SGNN_DEV int item_half(int k) const {
+    int m = k;
+    if (donor) {
+      if (k == 0) return hd;
+      m = k - 1;
+    }
+    const int hs = 16 * b + 16 * kWaves16 * m;
+    if (hs >= Et) return -2;
+    if (owner_d && m == F) return -1;
+    return hs;
+  }
+
+  // hook(s) runs before the wave's product slot s (s = 0 .. kPre - 1) and hook(kPre) after the last: the
+  // caller publishes and requests the node weights there, between the products.  Slot s holds item s;
+  // its product goes to pre[s] (own half m = s), or (DONOR) slot 0's to dbuf and slot s's (own half
+  // m = s - 1) to pre[s - 1].
+  template <bool FIRST, bool DONOR, class Hook>
   SGNN_DEV void prewait(const float (&xw1)[KQ], Hook&& hook) {
     const float* pos = a.pos_last ? a.pos_last : a.pos_seq + (int64_t)(a.T - 1) * a.dim;
     const int pstride = a.pos_last ? a.dim : a.T * a.dim;
     float ps_n[3] = {0.0f, 0.0f, 0.0f}, pr_n[3] = {0.0f, 0.0f, 0.0f};
     auto load_pos = [&](int hs) {
       const int e = hs + j, ec = e < Et ? e : Et - 1;
-      const int r = lrecv[ec], s = lsend[ec];
+      const int rr = lrecv[ec], ss = lsend[ec];
 #pragma unroll
       for (int c = 0; c < 3; ++c)
         if (c < a.dim) {
-          ps_n[c] = pos[(int64_t)s * pstride + c];
-          pr_n[c] = pos[(int64_t)r * pstride + c];
+          ps_n[c] = pos[(int64_t)ss * pstride + c];
+          pr_n[c] = pos[(int64_t)rr * pstride + c];
         }
     };
-    if (FIRST && 16 * b < Et) load_pos(16 * b);
+    auto next_item = [&](int k) {  // the next item to encode from k on (-2: none)
+      int h = item_half(k);
+      while (h == -1) h = item_half(++k);
+      return h;
+    };
+    auto encode_item = [&](f32x4 (&x)[KQ], int hs, int k) {
+      float ps[3], pr[3];
 #pragma unroll
-    for (int m = 0; m < kPre; ++m) {
-      const int hs = 16 * b + 16 * kWaves16 * m;
-      hook(m);
-      if (hs >= Et) continue;
-      f32x4 x[KQ];
-      if constexpr (FIRST) {
-        float ps[3], pr[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          ps[c] = ps_n[c];
-          pr[c] = pr_n[c];
-        }
-        load_pos(hs + 16 * kWaves16);
-        encode(x, xw1, ps, pr, hs, hs + j < Et);
-      } else {
-        ld_e0(x, hs);
+      for (int c = 0; c < 3; ++c) {
+        ps[c] = ps_n[c];
+        pr[c] = pr_n[c];
       }
+      const int hn = next_item(k + 1);
+      if (hn >= 0) load_pos(hn);
+      encode(x, xw1, ps, pr, hs, hs + j < Et);
+    };
+    if (FIRST) {
+      const int h0 = next_item(0);
+      if (h0 >= 0) load_pos(h0);
+    }
 #pragma unroll
-      for (int t = 0; t < KQ; ++t) pre[m][t] = zero4();
-      mm_full(pre[m], sw0, x, j, g);
+    for (int sl = 0; sl < kPre; ++sl) {
+      hook(sl);
+      const int hs = item_half(sl);
+      if (hs < 0) continue;
+      f32x4 x[KQ];
+      if constexpr (FIRST) encode_item(x, hs, sl);
+      else ld_e0(x, hs);
+      constexpr int kLast = kPre - 1;
+      f32x4(&dst)[KQ] = pre[DONOR ? (sl == 0 ? kLast : sl - 1) : sl];
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) dst[t] = zero4();
+      mm_full(dst, sw0, x, j, g);
+      if (DONOR && sl == 0) {
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) st4(dbuf + (((b - r) * KQ + t) * 64 + l) * 4, dst[t]);
+      }
     }
     hook(kPre);
-    if constexpr (FIRST) {  // the rest of the halves: e0 rows only
-      for (int hs = 16 * b + 16 * kWaves16 * kPre; hs < Et; hs += 16 * kWaves16) {
-        float ps[3], pr[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          ps[c] = ps_n[c];
-          pr[c] = pr_n[c];
-        }
-        load_pos(hs + 16 * kWaves16);
+    if constexpr (FIRST) {  // the rest of the items: e0 rows only
+      for (int k = kPre;; ++k) {
+        const int hs = item_half(k);
+        if (hs == -2) break;
+        if (hs < 0) continue;
         f32x4 x[KQ];
-        encode(x, xw1, ps, pr, hs, hs + j < Et);
+        encode_item(x, hs, k);
       }
     }
   }
@@ -402,9 +497,15 @@ struct EdgePhase {
       ev.ga[t] = svec[H + 16 * t + j];
       ev.be[t] = svec[2 * H + 16 * t + j];
     }
-    auto finish = [&](f32x4 (&acc)[KQ], int hs) {  // ReLU -> last Linear -> LayerNorm -> sums
-      edge_out(acc, agg, sw1, ev, lrecv, hs, Et, i0, j, g);
+    LnAgg la;
+    auto finish = [&](const f32x4 (&acc)[KQ], int hs) {  // ReLU -> last Linear -> LayerNorm -> sums
+      f32x4 x[KQ], y[KQ];
+      lin2_init(acc, x, y, ev);
+      mm_full<true>(y, sw1, x, j, g);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) la.part(p, y, agg, ev, lrecv, hs, Et, i0, j, g);
     };
+    const int npre = donor ? kPre - 1 : kPre;  // own halves whose product ran before the wait
     int hs = 16 * b;
     if (hs < Et) gather(hs);
     if (probe) mark(48);
@@ -412,8 +513,19 @@ struct EdgePhase {
     for (int m = 0; m < kPre; ++m) {
       if (hs >= Et) break;
       f32x4 acc[KQ];
+      if (owner_d && m == F) {   // formed by the donor wave (published with the barrier before the wait)
 #pragma unroll
-      for (int t = 0; t < KQ; ++t) acc[t] = pre[m][t] + (gu[t] + gv[t]);
+        for (int t = 0; t < KQ; ++t) acc[t] = ld4(dbuf + ((b * KQ + t) * 64 + l) * 4) + (gu[t] + gv[t]);
+      } else if (m < npre) {
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) acc[t] = pre[m][t] + (gu[t] + gv[t]);
+      } else {
+        f32x4 x[KQ];
+        ld_e0(x, hs);
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) acc[t] = gu[t] + gv[t];
+        mm_full(acc, sw0, x, j, g);
+      }
       gather(hs + 16 * kWaves16);
       finish(acc, hs);
       if (probe) mark(49 + m);
@@ -526,17 +638,23 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   // Between the pre-wait products: publish phase k + 1 (u_k / v_k, stored by the previous stage; the
   // drain of those write-through stores overlaps the first product), then request this layer's node
   // weights (VGPR-resident) in three parts, so neither the drain nor the load issue stalls the MFMAs.
-  ep.template prewait<FIRST>(xw1, [&](int m) {
+  const uint32_t ep_k = a.epoch0 + (uint32_t)k + 1;
+  TilePoll poll;
+  auto hook = [&](int m) {
     if (m == kPubAt) {
-      publish(a.flags, tile, a.epoch0 + (uint32_t)k + 1);
+      publish(a.flags, tile, ep_k);
       mark(ps < 0 ? -1 : ps + 2);
       W.load_first(nd, b, j, g);
     }
     if (m == (kPubAt + 1 < kPre ? kPubAt + 1 : kPre)) W.load_mid(nd, b, j, g);
+    if (m == kPre - 1) poll.issue(deps, ndeps, a.flags, ep_k, l);
     if (m == (kPubAt + 2 < kPre ? kPubAt + 2 : kPre)) W.load_out(nd, b, j, g);
-  });
+  };
+  ep.plan(lds + cv.dbuf);
+  if (ep.donor) ep.template prewait<FIRST, true>(xw1, hook);
+  else ep.template prewait<FIRST, false>(xw1, hook);
   mark(ps < 0 ? -1 : ps + 3);
-  wait_tiles(deps, ndeps, a.flags, a.epoch0 + (uint32_t)k + 1, b, l);
+  poll.wait(deps, ndeps, a.flags, ep_k, l);
   mark(ps < 0 ? -1 : ps + 4);
   ep.postwait(ru, rv, k == 1);
   mark(ps < 0 ? -1 : ps + 5);
@@ -598,25 +716,63 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   int32_t* kw_all = reinterpret_cast<int32_t*>(mask + 8);
   int32_t* deps = kw_all + 4 * 64;       // the sender tiles of this tile's edges, compacted
   int32_t* ndeps_l = deps + kMaxGrid;
+  int32_t* exs = ndeps_l + 4;            // example offsets (ex_ptr)
 
   mark(0);
   if (threadIdx.x < 8) mask[threadIdx.x] = 0u;
+  if ((int)threadIdx.x <= a.n_ex) exs[threadIdx.x] = (int32_t)a.ex_ptr[threadIdx.x];
 
   // ---- radius graph of the tile's receivers (torch_cluster's rule: first `cap` in-range senders of
   // the receiver's example in ascending index, strict <; learned_simulator.py:116-117) --------------
   float* sp = lds + cv.region;  // [DIM][n] SoA
-  if (a.pos_last) {  // the previous step's next_pos: contiguous, coalesced
-    for (int t = threadIdx.x; t < n * DIM; t += kBlock16) {
-      const int i = t / DIM, d = t - i * DIM;
-      sp[d * n + i] = a.pos_last[t];
+  // the tile's node features (learned_simulator.py:256-290): their raw inputs are requested first and
+  // combined after the radius search, so the loads complete under it
+  const int64_t ic = j < cnt ? (int64_t)(i0 + j) : (int64_t)i0;
+  const int nvel = (a.T - 1) * DIM;
+  float fr0[KQF][4], fr1[KQF][4], vmean[DIM], vstd[DIM];
+  {
+    const float* p = a.pos_seq + ic * a.T * DIM;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
+      vmean[d] = a.vel_mean[d];
+      vstd[d] = a.vel_std[d];
     }
-  } else {
-    for (int t = threadIdx.x; t < n * DIM; t += kBlock16) {
-      const int i = t / DIM, d = t - i * DIM;
-      sp[d * n + i] = a.pos_seq[((int64_t)i * a.T + a.T - 1) * DIM + d];
+#pragma unroll
+    for (int q = 0; q < KQF; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * q + 4 * g + c, t = f / DIM, cc = f - t * DIM;
+        fr0[q][c] = f < nvel ? p[(t + 1) * DIM + cc] : f == nvel ? p[(a.T - 1) * DIM] : 0.0f;
+        fr1[q][c] = f < nvel ? p[t * DIM + cc] : 0.0f;
+      }
+  }
+  const int64_t ptype = a.use_emb ? a.types[ic] : 0;
+  {  // the window's last frame (or the previous step's contiguous next_pos), 16 loads in flight per thread
+    constexpr int kPosBatch = 16;
+    for (int t0 = threadIdx.x; t0 < n * DIM; t0 += kBlock16 * kPosBatch) {
+      float v[kPosBatch];
+#pragma unroll
+      for (int u = 0; u < kPosBatch; ++u) {
+        const int t = t0 + u * kBlock16, i = t / DIM, d = t - i * DIM;
+        v[u] = t >= n * DIM ? 0.0f : a.pos_last ? a.pos_last[t] : a.pos_seq[((int64_t)i * a.T + a.T - 1) * DIM + d];
+      }
+#pragma unroll
+      for (int u = 0; u < kPosBatch; ++u) {
+        const int t = t0 + u * kBlock16, i = t / DIM, d = t - i * DIM;
+        if (t < n * DIM) sp[d * n + i] = v[u];
+      }
     }
   }
 
+  if (a.use_emb) {  // :287-290 type embedding
+#pragma unroll
+    for (int q = 0; q < KQF; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * q + 4 * g + c;
+        if (f > nvel && f < nvel + 1 + a.emb_dim) fr0[q][c] = a.emb_w[ptype * a.emb_dim + (f - nvel - 1)];
+      }
+  }
   // weights of layer 0's edge MLP, of Encoder.edge_fn and of Encoder.node_fn (VGPR-resident), issued after the
   // positions (loads complete in order) and in flight during the radius queries
   EdgeStage st0;
@@ -651,9 +807,9 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
       int lo = 0, hi = a.n_ex - 1;  // example of i: largest e with ex_ptr[e] <= i
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (a.ex_ptr[mid] <= i) lo = mid; else hi = mid - 1;
+        if (exs[mid] <= i) lo = mid; else hi = mid - 1;
       }
-      const int jb = (int)a.ex_ptr[lo], je = (int)a.ex_ptr[lo + 1];
+      const int jb = exs[lo], je = exs[lo + 1];
       float pi[DIM];
 #pragma unroll
       for (int d = 0; d < DIM; ++d) pi[d] = sp[d * n + i];
@@ -746,24 +902,24 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   {
     const int64_t i = i0 + j;
     const bool valid = j < cnt;
-    const int64_t ic = valid ? i : (int64_t)i0;
-    const int nvel = (a.T - 1) * DIM;
-    const float* p = a.pos_seq + ic * a.T * DIM;
     f32x4 xf[KQF];
 #pragma unroll
     for (int q = 0; q < KQF; ++q)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int f = 16 * q + 4 * g + c;
-        float val = 0.0f;
+        const int f = 16 * q + 4 * g + c, t = f / DIM, cc = f - t * DIM;
+        float val = fr0[q][c];  // embedding, or 0 past the features
         if (f < nvel) {  // learned_simulator.py:258,272-278 normalised velocity history
-          const int t = f / DIM, cc = f - t * DIM;
-          const float vel = __fsub_rn(p[(t + 1) * DIM + cc], p[t * DIM + cc]);
-          val = __fdiv_rn(__fsub_rn(vel, a.vel_mean[cc]), a.vel_std[cc]);
+          float mn = vmean[0], sd = vstd[0];
+#pragma unroll
+          for (int d = 1; d < DIM; ++d)
+            if (cc == d) {
+              mn = vmean[d];
+              sd = vstd[d];
+            }
+          val = __fdiv_rn(__fsub_rn(__fsub_rn(fr0[q][c], fr1[q][c]), mn), sd);
         } else if (f == nvel) {  // :282-284 wall distance
-          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(p[(a.T - 1) * DIM], 2.0f), 0.0f), a.wall_max), a.wall_div);
-        } else if (a.use_emb && f < nvel + 1 + a.emb_dim) {  // :287-290 type embedding
-          val = a.emb_w[a.types[ic] * a.emb_dim + (f - nvel - 1)];
+          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(fr0[q][c], 2.0f), 0.0f), a.wall_max), a.wall_div);
         }
         xf[q][c] = val;
       }

@@ -29,7 +29,7 @@ seq = synthetic.trajectory(bench.lattice(dims), bench.T_SEQ, seed=1000)
 n = seq.shape[0]
 w0 = torch.from_numpy(seq).to(dev)
 types_ = torch.zeros(n, dtype=torch.long, device=dev)
-runner = sim.rollout_runner(w0, [n], types_, 1)
+runner = sim.rollout_runner(w0, [n], types_, 3)   # marks of the last step (contiguous pos_last)
 one, nt, grid = engine.step_path(runner.epd, runner.sin, runner.ws)
 assert one, "workload does not take the one-launch step"
 for _ in range(20):
