@@ -913,7 +913,9 @@ static int layer_common(sgnn::Layer16Args& L, const sgnn_mlp* edge_fn, const sgn
   // rounds (measured, tools/exp_layer16.py: C1 r = 15 21.4 -> 18.6-19.9 us at 8 nodes vs 4,
   // r = 0.6 17.9 -> 11.8 us; 4,800 particles best at 12, 8,000 at 16)
   L.nt = (int)std::min<int64_t>(16, std::max<int64_t>(8, (a.n + 399) / 400));
-  if (const char* e = getenv("SGNN_NT")) L.nt = atoi(e);  // experiment override (tools/exp_layer16.py)
+#ifdef SGNN_EXPERIMENT
+  if (const char* e = getenv("SGNN_NT")) L.nt = std::min(16, std::max(8, atoi(e)));  // tools/exp_layer16.py builds
+#endif
   return layer16_launch(L, mode, node_fn->nlin, static_cast<hipStream_t>(stream), first);
 }
 

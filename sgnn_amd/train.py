@@ -120,7 +120,7 @@ class Trainer:
     def __init__(self, simulator, lr_init: float = 1e-3, lr_decay: float = 0.1,
                  lr_decay_steps: int = 30000, noise_std: float = 0.02,
                  loss_weight_position: float = 1.0, loss_weight_strain: float = 1.0,
-                 group=None, nslab: int = training.DEFAULT_NSLAB):
+                 group=None, nslab: Optional[int] = None):
         self.sim = simulator
         self.epd = simulator._encode_process_decode
         training.check_trainable(self.epd, simulator._nparticle_types)

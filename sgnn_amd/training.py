@@ -21,6 +21,8 @@ from . import _hip, engine
 from ._hip import SgnnReduceDesc, SgnnSaves, check, lib, stream_ptr
 
 DEFAULT_NSLAB = 512  # persistent edge-backward workgroups: two per CU (k_edge_bwd64 sizes its LDS for that)
+WIDE_NSLAB = 256     # the other single-scale variants (H = 64 with nmlp_layers 2, H = 128): larger LDS,
+                     # one workgroup per CU, so 512 would run in two rounds
 MS_NSLAB = 256      # multi-scale (H = 128 items / weight-gradient kernels, one workgroup per CU)
 NODE_NSLAB = 256     # node-level backward kernels (128 measured slower: fewer CUs busy)
 
@@ -221,6 +223,12 @@ class SlabArena:
         return GradLayout(H, nl, feat, dim, self.arena, self.slab_off, self.slab_floats, self.nslab_of)
 
 
+def default_nslab(H: int, nlin: int) -> int:
+    """Persistent backward workgroups for this variant: two per CU only where the
+    k_*_bwd64 kernels (H = 64, nmlp_layers 1) are dispatched."""
+    return DEFAULT_NSLAB if (H == 64 and nlin == 2) else WIDE_NSLAB
+
+
 def nslab_table(nslab: int) -> Dict[int, int]:
     node_ns = max(1, min(nslab, NODE_NSLAB))
     # the edge, uv and node backward (H = 64: 80 KB kernels, two workgroups per CU) take the full
@@ -245,10 +253,11 @@ class TrainWorkspace:
     particles (`activate(n)` selects the batch size within the capacity)."""
 
     def __init__(self, epd: nn.Module, n: int, T: int, dim: int, K: int, loop: bool,
-                 device: torch.device, nslab: int = DEFAULT_NSLAB):
+                 device: torch.device, nslab: Optional[int] = None):
         L = lib()
         H, nl = epd.latent_dim, epd.nlayers
         self.nlin = epd.nmlp_layers + 1
+        nslab = default_nslab(H, self.nlin) if nslab is None else nslab
         self.H, self.L, self.n, self.T, self.dim, self.nslab = H, nl, n, T, dim, nslab
         self.n_cap = n
         self.nslab_of = nslab_table(nslab)

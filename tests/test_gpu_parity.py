@@ -94,6 +94,9 @@ def test_large_against_oracle(nx, ny, radius, n_ex):
     np.testing.assert_array_equal(torch.stack([r, s]).cpu().numpy(), ei_ref.numpy())
     nxt, strain = sim.predict_positions(pos.cuda(), counts, types_.cuda())
     _close(strain.cpu().numpy(), ref_strain.numpy(), what=f"{nx}x{ny} r={radius} strain")
+    # the acceleration channels through the Euler integrator (positions: the normalised-output bound x acc_std)
+    scale = float(np.max(z["acc_std"]))
+    _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * scale, rtol=1e-6, what=f"{nx}x{ny} r={radius} next_pos")
 
 
 def test_radius_graph_random_vs_bruteforce():

@@ -1,9 +1,21 @@
 """Fused-layer experiment: time one sgnn_interaction_layer launch (HIP events,
-100 launches) at a bench workload."""
+100 launches) at a bench workload, optionally at forced receivers-per-tile counts.
+
+  python tools/exp_layer16.py build              # here (CPU): _lib/libsgnn_hip_exp.so (-DSGNN_EXPERIMENT)
+  python tools/exp_layer16.py <workload> [nt...] # on the GPU box (SGNN_NT, clamped to 8..16, is read only
+                                                 # by that experiment build)"""
 import ctypes, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+EXP_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "sgnn_amd", "_lib",
+                       "libsgnn_hip_exp.so")
+if len(sys.argv) > 1 and sys.argv[1] == "build":
+    from sgnn_amd import build_lib
+    print(build_lib.build(defines=("SGNN_EXPERIMENT",), lib=EXP_LIB))
+    sys.exit(0)
 import numpy as np
 import torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from sgnn_amd import _hip
+_hip.load_library(EXP_LIB)
 import bench
 from sgnn_amd import engine, synthetic
 from sgnn_amd._hip import lib, check, stream_ptr
