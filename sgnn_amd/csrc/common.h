@@ -19,6 +19,24 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define SGNN_DEV __device__ __forceinline__
+
+// Debug builds (-DSGNN_DEBUG_BOUNDS, tools/exp_debug_bounds.py): index checks on the graph paths that
+// print the violation (device printf, no trap) and clamp the index so the run continues; no code in
+// product builds.
+#ifdef SGNN_DEBUG_BOUNDS
+#define SGNN_BOUNDS(idx, lo, hi, what)                                                               \
+  do {                                                                                              \
+    if ((int64_t)(idx) < (int64_t)(lo) || (int64_t)(idx) >= (int64_t)(hi)) {                         \
+      printf("SGNN-BOUNDS %s: %lld outside [%lld, %lld) at %s:%d block %d\n", what, (long long)(idx),  \
+             (long long)(lo), (long long)(hi), __FILE__, __LINE__, (int)blockIdx.x);                   \
+      idx = (int64_t)(idx) < (int64_t)(lo) ? (lo) : (hi) - 1;                                         \
+    }                                                                                               \
+  } while (0)
+#else
+#define SGNN_BOUNDS(idx, lo, hi, what) \
+  do {                                 \
+  } while (0)
+#endif
 #define SGNN_HOST_DEV __host__ __device__
 
 SGNN_DEV int lane_id() { return threadIdx.x & 63; }

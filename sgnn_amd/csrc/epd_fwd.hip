@@ -208,7 +208,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_edges(EncEdgeArgs a) {
       const int64_t src = a.perm[ec];
       for (int c = 0; c < a.fe; ++c) f[c] = a.efeat_in[src * a.fe + c];
     } else {
-      const int64_t s = a.send[ec], r = a.recv[ec];
+      int64_t s = a.send[ec], r = a.recv[ec];
+      SGNN_BOUNDS(s, 0, a.n, "encode_edges sender");
+      SGNN_BOUNDS(r, 0, a.n, "encode_edges receiver");
       float ss = 0.0f;
       for (int c = 0; c < a.dim; ++c) {  // learned_simulator.py:299-312
         const float d = __fdiv_rn(__fsub_rn(a.pos[s * a.stride + c], a.pos[r * a.stride + c]), a.radius);
@@ -312,6 +314,8 @@ void k_edge_layer(EdgeLayerArgs a) {
     const int64_t ecc = ee < E ? ee : E - 1;
     rv_n = a.recv[ecc];
     s_n = a.send[ecc];
+    SGNN_BOUNDS(rv_n, 0, a.n, "edge_layer receiver");
+    SGNN_BOUNDS(s_n, 0, a.n, "edge_layer sender");
     // receivers around the tile: lane 0 reads the one before, lane 1 the one
     // after, as one divergent load (a uniform-address load goes to an SGPR at
     // once -- a wait on every gather in flight); read back with readlane

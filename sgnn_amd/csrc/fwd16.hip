@@ -174,6 +174,8 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(WPE)))
       r_n = a.recv[ec];
       s_n = a.send[ec];
     }
+    SGNN_BOUNDS(r_n, 0, nd.n, "layer16 receiver");
+    SGNN_BOUNDS(s_n, 0, nd.n, "layer16 sender");
     if constexpr (FIRST) {
 #pragma unroll
       for (int c = 0; c < 3; ++c)
@@ -220,9 +222,12 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(WPE)))
       const int k = t / a.l_cap, q = t - k * a.l_cap;
       const int r0 = lpre[k];
       if (q < lpre[k + 1] - r0) {
-        const int32_t sv = a.l_nbr[(i0 + k) * a.l_cap + q];
-        lsend[r0 - base + q] = sv;
-        lrecv[r0 - base + q] = (int32_t)(i0 + k);
+        int32_t sv = a.l_nbr[(i0 + k) * a.l_cap + q];
+        SGNN_BOUNDS(sv, 0, nd.n, "layer16 padded-list sender");
+        int slot = r0 - base + q;
+        SGNN_BOUNDS(slot, 0, 16 * 32, "layer16 tile CSR slot");
+        lsend[slot] = sv;
+        lrecv[slot] = (int32_t)(i0 + k);
         a.send_out[r0 + q] = sv;
         a.recv_out[r0 + q] = (int32_t)(i0 + k);
       }

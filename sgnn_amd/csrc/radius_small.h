@@ -100,7 +100,10 @@ SGNN_DEV void radius_small_body(const RadiusSmallArgs& a, float* lds, int blk, i
         cnt -= 1;
       }
     }
-    if (lane < cnt) a.nbr[(int64_t)i * cap + lane] = top;
+    if (lane < cnt) {
+      SGNN_BOUNDS(top, 0, a.n, "radius(small) neighbour");
+      a.nbr[(int64_t)i * cap + lane] = top;
+    }
     if (lane == 0) a.deg[i] = cnt;
     wave_lds_sync();
   }

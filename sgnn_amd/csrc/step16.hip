@@ -91,7 +91,8 @@ SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
 // boundaries, [workgroup][wave][64] into the buffer set by sgnn_set_probe16.  Slots: 0 start, 1 radius done,
 // 2 encoder done; layer k < 5 at 3 + 8 k + (0 start, 1 node weights requested, 2 published, 3 pre-wait done,
 // 4 wait done, 5 edge phase done, 6 node tail done, 7 end); layer 1's halves at 48 + (0 gathers issued,
-// 1.. after each), its node phase at 52 (sums read), 53 (first Linear).
+// 1.. after each), its node phase at 52 (sums read), 53 (first Linear); 56 positions staged, 58 weights in
+// LDS, 59 tile CSR built.
 #ifdef SGNN_PROBE
 __device__ uint64_t* g_probe16;
 SGNN_DEV void mark(int slot) {
@@ -108,28 +109,40 @@ SGNN_DEV void mark(int) {}
 // wave's last pre-wait product, so their round trip overlaps it -- and `wait` checks them and polls
 // on until they match.
 struct TilePoll {
-  uint32_t v[kMaxGrid / 64];
-  SGNN_DEV void issue(const int32_t* deps, int ndeps, const uint32_t* flags, uint32_t epoch, int lane) {
+  uint32_t v[kMaxGrid / 64], w[kMaxGrid / 64];
+  SGNN_DEV static void read(uint32_t (&x)[kMaxGrid / 64], const int32_t* deps, int ndeps, const uint32_t* flags,
+                            uint32_t epoch, int lane) {
 #pragma unroll
     for (int q = 0; q < kMaxGrid / 64; ++q)
-      v[q] = lane + 64 * q < ndeps
+      x[q] = lane + 64 * q < ndeps
                  ? __hip_atomic_load((const gu32*)(flags + deps[lane + 64 * q]), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT)
                  : epoch;
   }
-  SGNN_DEV void wait(const int32_t* deps, int ndeps, uint32_t* flags, uint32_t epoch, int lane) {
-    for (int it = 0;; ++it) {
-      bool ok = true;
+  SGNN_DEV static bool ok(const uint32_t (&x)[kMaxGrid / 64], uint32_t epoch) {
+    bool r = true;
 #pragma unroll
-      for (int q = 0; q < kMaxGrid / 64; ++q) ok = ok && v[q] >= epoch;
-      if (__all(ok)) break;
+    for (int q = 0; q < kMaxGrid / 64; ++q) r = r && x[q] >= epoch;
+    return __all(r);
+  }
+  // two early reads, one product apart: the later one usually sees counters the earlier missed
+  SGNN_DEV void issue(const int32_t* deps, int ndeps, const uint32_t* flags, uint32_t epoch, int lane) {
+    read(v, deps, ndeps, flags, epoch, lane);
+  }
+  SGNN_DEV void issue2(const int32_t* deps, int ndeps, const uint32_t* flags, uint32_t epoch, int lane) {
+    read(w, deps, ndeps, flags, epoch, lane);
+  }
+  SGNN_DEV void wait(const int32_t* deps, int ndeps, uint32_t* flags, uint32_t epoch, int lane) {
+    if (ok(v, epoch) || ok(w, epoch)) return;
+    for (int it = 0;; ++it) {
+      if (ok(v, epoch)) break;
       if (it >= kPollLimit) {
         if (lane == 0)
           __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
-      issue(deps, ndeps, flags, epoch, lane);
+      read(v, deps, ndeps, flags, epoch, lane);
     }
   }
 };
@@ -483,7 +496,9 @@ struct EdgePhase {
     f32x4 gu[KQ], gv[KQ];
     auto gather = [&](int hs) {  // clamped: harmless past the end
       const int e = hs + j, ec = e < Et ? e : Et - 1;
-      const int r = lrecv[ec], s = lsend[ec];
+      int r = lrecv[ec], s = lsend[ec];
+      SGNN_BOUNDS(r, 0, a.n, "step16 gathered receiver");
+      SGNN_BOUNDS(s, 0, a.n, "step16 gathered sender");
 #pragma unroll
       for (int t = 0; t < KQ; ++t) {
         gu[t] = ld4_sc1(ru, r * (H * 4) + (16 * t + 4 * g) * 4);
@@ -648,6 +663,7 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
     }
     if (m == (kPubAt + 1 < kPre ? kPubAt + 1 : kPre)) W.load_mid(nd, b, j, g);
     if (m == kPre - 1) poll.issue(deps, ndeps, a.flags, ep_k, l);
+    if (m == kPre) poll.issue2(deps, ndeps, a.flags, ep_k, l);
     if (m == (kPubAt + 2 < kPre ? kPubAt + 2 : kPre)) W.load_out(nd, b, j, g);
   };
   ep.plan(lds + cv.dbuf);
@@ -720,7 +736,6 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
 
   mark(0);
   if (threadIdx.x < 8) mask[threadIdx.x] = 0u;
-  if ((int)threadIdx.x <= a.n_ex) exs[threadIdx.x] = (int32_t)a.ex_ptr[threadIdx.x];
 
   // ---- radius graph of the tile's receivers (torch_cluster's rule: first `cap` in-range senders of
   // the receiver's example in ascending index, strict <; learned_simulator.py:116-117) --------------
@@ -748,13 +763,18 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   }
   const int64_t ptype = a.use_emb ? a.types[ic] : 0;
   {  // the window's last frame (or the previous step's contiguous next_pos), 16 loads in flight per thread
+    // (one load path: a branch per load would put a wait in each), then the example offsets
+    const float* src = a.pos_last ? a.pos_last : a.pos_seq + (int64_t)(a.T - 1) * DIM;
+    const int stride = a.pos_last ? DIM : a.T * DIM;
+    const int n_ex = a.n_ex;
+    const int64_t exv = (int)threadIdx.x <= n_ex ? a.ex_ptr[threadIdx.x] : 0;
     constexpr int kPosBatch = 16;
     for (int t0 = threadIdx.x; t0 < n * DIM; t0 += kBlock16 * kPosBatch) {
       float v[kPosBatch];
 #pragma unroll
       for (int u = 0; u < kPosBatch; ++u) {
-        const int t = t0 + u * kBlock16, i = t / DIM, d = t - i * DIM;
-        v[u] = t >= n * DIM ? 0.0f : a.pos_last ? a.pos_last[t] : a.pos_seq[((int64_t)i * a.T + a.T - 1) * DIM + d];
+        const int t = min(t0 + u * kBlock16, n * DIM - 1), i = t / DIM, d = t - i * DIM;
+        v[u] = src[(int64_t)i * stride + d];
       }
 #pragma unroll
       for (int u = 0; u < kPosBatch; ++u) {
@@ -762,6 +782,7 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
         if (t < n * DIM) sp[d * n + i] = v[u];
       }
     }
+    if ((int)threadIdx.x <= n_ex) exs[threadIdx.x] = (int32_t)exv;
   }
 
   if (a.use_emb) {  // :287-290 type embedding
@@ -773,8 +794,9 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
         if (f > nvel && f < nvel + 1 + a.emb_dim) fr0[q][c] = a.emb_w[ptype * a.emb_dim + (f - nvel - 1)];
       }
   }
-  // weights of layer 0's edge MLP, of Encoder.edge_fn and of Encoder.node_fn (VGPR-resident), issued after the
-  // positions (loads complete in order) and in flight during the radius queries
+  // weights of layer 0's edge MLP and of Encoder.edge_fn (LDS images after the radius search), issued after
+  // the positions (loads complete in order) and in flight during the radius queries; Encoder.node_fn's
+  // (VGPR-resident) follow the queries, under the LDS staging and the tile CSR
   EdgeStage st0;
   st0.load(a.lay[0]);
   f32x4 sx[kStagePer];
@@ -784,7 +806,7 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   NodeW<2, 0> E;
   f32x4 w1f[KQF];
   f32x4 vb1;
-  {
+  auto load_encoder = [&]() {
     Node16Args nd{};
     nd.w2 = a.xn_w2; nd.b2 = a.xn_b2; nd.g = a.xn_g; nd.bb = a.xn_bb;
     nd.we = a.lay[0].ew1; nd.be = a.lay[0].eb1; nd.dim = DIM;
@@ -798,13 +820,16 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
         w1f[q][c] = f < a.feat ? a.xn_w1[(int64_t)urow * a.feat + f] : 0.0f;
       }
     vb1 = ld4(a.xn_b1 + 16 * b + 4 * g);
-  }
+  };
   __syncthreads();
+  mark(56);  // probe: positions staged
   {
     int32_t* kw = kw_all + b * 64;
+    const float r2 = a.r2;  // a local: the LDS stores below would make the compiler re-load the argument
+    const int loop = a.loop, n_ex = a.n_ex;
     for (int rl = b; rl < cnt; rl += kWaves16) {
       const int i = i0 + rl;
-      int lo = 0, hi = a.n_ex - 1;  // example of i: largest e with ex_ptr[e] <= i
+      int lo = 0, hi = n_ex - 1;  // example of i: largest e with ex_ptr[e] <= i
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (exs[mid] <= i) lo = mid; else hi = mid - 1;
@@ -814,27 +839,38 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
 #pragma unroll
       for (int d = 0; d < DIM; ++d) pi[d] = sp[d * n + i];
       int c = 0;
-      for (int base = jb; base < je && c < cap; base += 64) {
-        const int jj = base + l;
-        bool in = false;
-        if (jj < je) {
+      // four 64-candidate chunks per round: their LDS reads are in flight together, then the chunks
+      // are taken in index order (the first `cap` in range are kept; a round may test up to three
+      // chunks past the cap, harmlessly)
+      constexpr int kRound = 4;
+      for (int base = jb; base < je && c < cap; base += 64 * kRound) {
+        float pc[kRound][DIM];
+#pragma unroll
+        for (int u = 0; u < kRound; ++u) {
+          const int jj = min(base + 64 * u + l, je - 1);
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) pc[u][d] = sp[d * n + jj];
+        }
+#pragma unroll
+        for (int u = 0; u < kRound; ++u) {
+          const int jj = base + 64 * u + l;
           float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
 #pragma unroll
           for (int d = 0; d < DIM; ++d) {
-            const float t = __fsub_rn(sp[d * n + jj], pi[d]);
+            const float t = __fsub_rn(pc[u][d], pi[d]);
             s = __fadd_rn(s, __fmul_rn(t, t));
           }
-          in = s < a.r2;
+          const bool in = jj < je && s < r2;
+          const uint64_t bal = __ballot(in);
+          const int slot = c + (int)__popcll(bal & ((1ull << l) - 1ull));
+          if (in && slot < cap) kw[slot] = jj;
+          c += (int)__popcll(bal);
         }
-        const uint64_t bal = __ballot(in);
-        const int slot = c + (int)__popcll(bal & ((1ull << l) - 1ull));
-        if (in && slot < cap) kw[slot] = jj;
-        c += (int)__popcll(bal);
       }
       wave_lds_sync();
       c = min(c, cap);
       int top = l < c ? kw[l] : INT32_MAX;
-      if (!a.loop) {  // torch_cluster: K+1 first-by-index, then the self loop dropped
+      if (!loop) {  // torch_cluster: K+1 first-by-index, then the self loop dropped
         const uint64_t self = __ballot(l < c && top == i);
         if (self) {
           const int at = __ffsll((long long)self) - 1;
@@ -849,11 +885,13 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     }
   }
   mark(1);
+  load_encoder();
   // LDS images of the staged weights (the radius phase never touches them)
   st0.store(lds + cv.sw0, lds + cv.sw1, lds + cv.svec, 1.0f);
   stage_w64_store(lds + cv.sxw, sx, 1.0f);
   sxv.store(lds + cv.sxv, 4);
   __syncthreads();
+  mark(58);  // probe: weights in LDS
   // tile CSR (receiver-sorted, senders ascending) from the kept lists; sender-tile mask
   if (b == 0) {
     const int dg = l < cnt ? ldeg[l] : 0;
@@ -872,8 +910,10 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   for (int t = threadIdx.x; t < cnt * cap; t += kBlock16) {
     const int k = t / cap, q = t - k * cap;
     if (q < ldeg[k]) {
-      const int32_t sv = nbr_l[k * cap + q];
-      const int e = lpre[k] + q;
+      int32_t sv = nbr_l[k * cap + q];
+      SGNN_BOUNDS(sv, 0, n, "step16 sender");
+      int e = lpre[k] + q;
+      SGNN_BOUNDS(e, 0, nt * cap, "step16 tile edge");
       lsend[e] = sv;
       lrecv[e] = i0 + k;
       const int st = sv / nt;
@@ -882,13 +922,18 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     }
   }
   __syncthreads();
+  mark(59);  // probe: CSR built
   if (b == 0) {  // the mask as a list (wave_lds_sync-free: one wave, in order)
     int base = 0;
     for (int t0 = 0; t0 < (int)gridDim.x; t0 += 64) {
       const int t = t0 + l;
       const bool on = t < (int)gridDim.x && ((mask[t >> 5] >> (t & 31)) & 1u);
       const uint64_t bal = __ballot(on);
-      if (on) deps[base + (int)__popcll(bal & ((1ull << l) - 1ull))] = t;
+      if (on) {
+        int slot = base + (int)__popcll(bal & ((1ull << l) - 1ull));
+        SGNN_BOUNDS(slot, 0, kMaxGrid, "step16 dependency list");
+        deps[slot] = t;
+      }
       base += (int)__popcll(bal);
     }
     if (l == 0) *ndeps_l = base;

@@ -50,14 +50,20 @@ print(f"{wl}: n={n} grid={grid} nt={nt} L={L}; wave life (to layer {nl - 1}'s en
 
 
 def show(a, b, nm, sel=None):
-    sel = np.ones(t.shape[0], bool) if sel is None else sel
+    sel = (t[:, a] > 0) & (t[:, b] > 0) if sel is None else sel & (t[:, a] > 0) & (t[:, b] > 0)
+    if not sel.any():
+        print(f"  {nm:28s} (no wave reaches it)")
+        return
     d = t[sel, b] - t[sel, a]
     print(f"  {nm:28s} p10 {np.percentile(d, 10):8.0f}  p50 {np.percentile(d, 50):8.0f}  p90 {np.percentile(d, 90):8.0f}"
           f"  max {d.max():8.0f}")
 
 
-show(0, 1, "radius search")
-show(1, 2, "stage + CSR + encoder")
+show(0, 56, "positions staged")
+show(56, 1, "radius scan")
+show(1, 58, "weights to LDS")
+show(58, 59, "tile CSR")
+show(59, 2, "node encoder")
 for k in range(nl):
     s0 = 3 + 8 * k
     show(2 if k == 0 else s0 - 1, s0, f"L{k} layer boundary")
