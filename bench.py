@@ -80,6 +80,12 @@ HBM_PEAK = 8.0e12         # MI355X HBM3E bytes/s (MI355X_MICROARCH.md)
 DATA = "synthetic (0.5 mm Taylor-bar lattice + random-walk frames; random-init weights)"
 
 
+def progress(msg):
+    """One progress line on stderr per bench leg (a long default run keeps
+    writing, and the log shows where time went)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def lattice(dims):
     return synthetic.lattice_2d(*dims) if len(dims) == 2 else synthetic.lattice_3d(*dims)
 
@@ -199,12 +205,19 @@ def cpu_threads(n=None) -> dict:
 
 
 def thread_counts():
-    """The CPU-leg thread counts to try: the box's share (OMP_NUM_THREADS) and
-    every CPU of the affinity mask, when they differ."""
+    """The CPU-leg thread counts: the box's share (OMP_NUM_THREADS) and every
+    CPU of the affinity mask (BASELINE.md §3's os.cpu_count()), when they
+    differ -- the affinity leg only while it is at most 4x the share: on the GPU
+    box the mask shows the whole host (256 CPUs) but the job gets a 16-CPU
+    share, and 256 OpenMP threads on 16 CPUs did not finish one step in 3
+    minutes.  Returns (counts, note on any leg left out)."""
     aff = len(os.sched_getaffinity(0))
     omp = os.environ.get("OMP_NUM_THREADS")
     share = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
-    return sorted({share, aff})
+    if aff > 4 * share:
+        return [share], (f"affinity leg ({aff} threads) not timed: {aff} OpenMP threads on this job's "
+                         f"{share}-CPU share (OMP_NUM_THREADS) oversubscribe it")
+    return sorted({share, aff}), None
 
 
 def profiled(workload, mode, kernel):
@@ -308,8 +321,10 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload, min_seconds=0.
     n = window.shape[0]
     types_ = torch.zeros(n, dtype=torch.long)
     legs = []
-    for nthreads in thread_counts():
+    counts, skipped = thread_counts()
+    for nthreads in counts:
         info = cpu_threads(nthreads)
+        progress(f"  cpu rollout leg: {nthreads} threads")
         cur = window.cpu()
         with torch.no_grad():
             nxt, _ = osim.predict_positions(cur, [n], types_)
@@ -326,7 +341,8 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload, min_seconds=0.
                      "M_edge_messages_per_s": edges * L * done / dt / 1e6})
     cpu_threads()
     best = max(legs, key=lambda r: r["value"])
-    return {**best, "legs": [{k: r[k] for k in ("cores", "value", "steps", "seconds")} for r in legs],
+    extra = {"legs_note": skipped} if skipped else {}
+    return {**best, **extra, "legs": [{k: r[k] for k in ("cores", "value", "steps", "seconds")} for r in legs],
             "sample": f"{best['steps']} autoregressive oracle rollout steps after 1 warm-up (torch CPU fp32 "
                       f"restatement of the reference ops + C cell-list radius search), {n} particles{sample}; "
                       f"fastest of the thread counts tried (legs)"}
@@ -352,6 +368,7 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps,
     every step; no host round trip).  Warm-up: full untimed rollouts.  The
     dominant kernel's launch time comes from a second, event-timed pass."""
     from sgnn_amd import engine
+    progress(f"rollout {workload}")
     dims, radius, H, L = WORKLOADS[workload]
     dim = len(dims)
     feat = (T_SEQ - 1) * dim + 1
@@ -439,6 +456,7 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps,
            "roofline": roofline(kernel, flops, kernel_s, workload, "rollout", alg_bytes, exe)}
     out["roofline"]["share_of_step"] = kernel_s * (1 if one_launch else L) / (dt / steps)
     if cpu_steps > 0 and rank == 0 and world == 1:
+        progress(f"rollout {workload}: cpu baseline")
         out["cpu_baseline"] = cpu_rollout_baseline(sim, window0, radius, L, cpu_steps, workload, cpu_seconds)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
     return out
@@ -492,6 +510,7 @@ def bench_train(mode, steps, warmup, world, rank, device, seed, cpu_steps):
     One step = Trainer.train_step: fused noise, saved-activation forward, fused
     loss + backward, SUM all-reduce of the flat gradient over RCCL, Adam, LR."""
     from sgnn_amd.train import Trainer, split_batch
+    progress(mode)
     if mode == "train":
         dims, radius, H, L = WORKLOADS["c2"]
         all_graphs = [dims] * world
@@ -559,6 +578,7 @@ def bench_train(mode, steps, warmup, world, rank, device, seed, cpu_steps):
     }
     res["roofline"]["share_of_step"] = float(np.sum([a.elapsed_time(b) for a, b in timers[dom]])) / (dt_ev * 1e3)
     if rank == 0 and world == 1 and cpu_steps > 0:
+        progress(f"{mode}: cpu baseline")
         res["cpu_baseline"] = cpu_train_baseline(state0, graphs, radius, L, max(3, cpu_steps // 2),
                                                  sim._normalization_stats)
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
@@ -633,6 +653,7 @@ def cpu_ms_train_baseline(sim, cfg, steps):
 
 def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps):
     from sgnn_amd.multi_scale.ms_training import MultiScaleTrainer
+    progress(f"ms-train {workload}")
     sim, seq, edges, desc, cfg = ms_setup(workload, device, seed, rank, T_SEQ + 1)
     n = seq.shape[0]
     H, L, nmlp = cfg[4], cfg[5], cfg[6]
@@ -679,6 +700,7 @@ def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps
         "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and cpu_steps > 0:
+        progress(f"ms-train {workload}: cpu baseline")
         res["cpu_baseline"] = cpu_ms_train_baseline(sim, cfg, max(3, cpu_steps // 2))
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     return res

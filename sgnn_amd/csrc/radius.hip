@@ -301,19 +301,21 @@ __global__ __launch_bounds__(256) void k_cell_scatter(int64_t n, const int32_t* 
 constexpr int kTX = 64;
 constexpr int kQBlock = 256;
 constexpr int kLdsCand = 3072;   // staged candidates (48 KB of float4)
-constexpr int kMaxCap = 32;
-
-SGNN_DEV void sorted_insert(int (&top)[kMaxCap], int x) {
+// register-list lengths of the query kernel: 32 covers the reference's caps
+// (20, 24, +1 without self loops); 64 serves caps 33..64 (torch_cluster's
+// default max_num_neighbors = 32 with loop = False asks for 33)
+template <int MAXCAP>
+SGNN_DEV void sorted_insert(int (&top)[MAXCAP], int x) {
   // keep top[] ascending: x shifts the larger entries one slot up
 #pragma unroll
-  for (int s = kMaxCap - 1; s > 0; --s) {
+  for (int s = MAXCAP - 1; s > 0; --s) {
     const int lo = top[s - 1];
     top[s] = x < lo ? lo : (x < top[s] ? x : top[s]);
   }
   top[0] = x < top[0] ? x : top[0];
 }
 
-template <int DIM>
+template <int DIM, int kMaxCap>
 __global__ __launch_bounds__(kQBlock) void k_radius_query_lds(
     const f32x4* cpos, const int32_t* start, const uint32_t* bbox, int n_ex, float r2, int cap, int loop,
     int32_t* nbr, int32_t* deg, int64_t n) {
@@ -438,8 +440,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_radius_small(sgnn::RadiusSmallA
 // deg -> rowptr (exclusive scan, rowptr[n] = E) and the padded lists ->
 // receiver-sorted CSR.  n <= kSmallN: every workgroup scans all of deg in LDS
 // (8 rows per thread) -- cheaper than a grid-wide scan's extra launches --
-// then copies the rows of its own 32-row slice (thread = (row, slot), cap <=
-// 32); workgroup 0 writes rowptr.
+// then copies the rows of its own 32-row slice (thread = (row, slot), slots
+// t and t + 32 for caps up to 64); workgroup 0 writes rowptr.
 __global__ __launch_bounds__(1024) void k_csr_small(int n, int cap, const int32_t* nbr,
                                                     const int32_t* deg, int32_t* rowptr,
                                                     int32_t* send, int32_t* recv) {
@@ -474,10 +476,10 @@ __global__ __launch_bounds__(1024) void k_csr_small(int n, int cap, const int32_
     for (int i = threadIdx.x; i <= n; i += blockDim.x) rowptr[i] = srow[i];
   const int i = blockIdx.x * 32 + (threadIdx.x >> 5), t = threadIdx.x & 31;
   if (i < n) {
-    const int r0 = srow[i];
-    if (t < srow[i + 1] - r0) {
-      send[r0 + t] = nbr[i * cap + t];
-      recv[r0 + t] = i;
+    const int r0 = srow[i], dg = srow[i + 1] - r0;
+    for (int tt = t; tt < dg; tt += 32) {
+      send[r0 + tt] = nbr[i * cap + tt];
+      recv[r0 + tt] = i;
     }
   }
 }
@@ -595,7 +597,7 @@ extern "C" int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n
   const int cap = K + (loop ? 0 : 1);
   if (n < 0 || dim < 1 || dim > 3 || n_ex < 1 || K < 1 || !(radius > 0.0f))
     return set_error(SGNN_ERR_INVALID, "radius_graph: bad n/dim/n_ex/K/radius");
-  if (cap > 32) return set_error(SGNN_ERR_UNSUPPORTED, "radius_graph: K (+1 without loop) > 32");
+  if (cap > kRadiusMaxCap) return set_error(SGNN_ERR_UNSUPPORTED, "radius_graph: K (+1 without loop) > 64");
   if (edge_cap < n * cap) return set_error(SGNN_ERR_INVALID, "radius_graph: edge_cap < n*cap");
   if (n > (int64_t)1 << 26) return set_error(SGNN_ERR_UNSUPPORTED, "radius_graph: n > 2^26");
   if (n == 0) {
@@ -633,15 +635,19 @@ extern "C" int sgnn_radius_graph(const float* pos, int64_t pos_stride, int64_t n
   // LDS-binned query over cell tiles (persistent grid: the tile count lives on the device)
   // about one tile per workgroup at lattice densities (~1.5 particles per cell, 64-cell tiles)
   const unsigned qgrid = (unsigned)std::min<int64_t>(std::max<int64_t>((n + 63) / 64, 1), 4096);
-  if (dim == 1)
-    hipLaunchKernelGGL(k_radius_query_lds<1>, dim3(qgrid), dim3(kQBlock), 0, stream, w.cpos, w.start, w.bbox,
-                       n_ex, r2, cap, loop, w.nbr, w.deg, n);
-  else if (dim == 2)
-    hipLaunchKernelGGL(k_radius_query_lds<2>, dim3(qgrid), dim3(kQBlock), 0, stream, w.cpos, w.start, w.bbox,
-                       n_ex, r2, cap, loop, w.nbr, w.deg, n);
-  else
-    hipLaunchKernelGGL(k_radius_query_lds<3>, dim3(qgrid), dim3(kQBlock), 0, stream, w.cpos, w.start, w.bbox,
-                       n_ex, r2, cap, loop, w.nbr, w.deg, n);
+  auto query = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(qgrid), dim3(kQBlock), 0, stream, w.cpos, w.start, w.bbox, n_ex, r2, cap, loop,
+                       w.nbr, w.deg, n);
+  };
+  if (cap <= 32) {
+    if (dim == 1) query(k_radius_query_lds<1, 32>);
+    else if (dim == 2) query(k_radius_query_lds<2, 32>);
+    else query(k_radius_query_lds<3, 32>);
+  } else {
+    if (dim == 1) query(k_radius_query_lds<1, kRadiusMaxCap>);
+    else if (dim == 2) query(k_radius_query_lds<2, kRadiusMaxCap>);
+    else query(k_radius_query_lds<3, kRadiusMaxCap>);
+  }
   st = scan_exclusive(w.deg, rowptr, n + 1, w.partials, stream);
   if (st) return st;
   const int64_t tot = n * cap;

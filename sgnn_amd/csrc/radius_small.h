@@ -16,6 +16,7 @@ namespace sgnn {
 
 constexpr int kSmallN = 8192;
 constexpr int kSmallBlock = 512;  // 8 query waves per workgroup
+constexpr int kRadiusMaxCap = 64;  // neighbour cap K (+1 without self loops): one kept slot per lane
 
 struct RadiusSmallArgs {
   const float* pos;
@@ -31,7 +32,7 @@ struct RadiusSmallArgs {
 
 // LDS bytes of the body: positions [DIM][n] + the per-wave kept lists.
 inline size_t radius_small_lds(int n, int dim) {
-  return sizeof(float) * (size_t)n * dim + sizeof(int32_t) * (kSmallBlock / 64) * 32;
+  return sizeof(float) * (size_t)n * dim + sizeof(int32_t) * (kSmallBlock / 64) * kRadiusMaxCap;
 }
 
 // Launches k_csr_small (deg -> rowptr, padded lists -> receiver-sorted CSR);
@@ -58,7 +59,7 @@ SGNN_DEV void radius_small_body(const RadiusSmallArgs& a, float* lds, int blk, i
   }
   __syncthreads();
   const int lane = lane_id(), w = wave_id();
-  int32_t* kw = kept_all + w * 32;
+  int32_t* kw = kept_all + w * kRadiusMaxCap;
   const int cap = a.cap;
   for (int i = blk * (kSmallBlock / 64) + w; i < n; i += nblk * (kSmallBlock / 64)) {
     int lo = 0, hi = a.n_ex - 1;  // example of i: largest b with ex_ptr[b] <= i

@@ -121,6 +121,36 @@ def test_radius_graph_random_vs_bruteforce():
         np.testing.assert_array_equal(got.numpy(), ref.numpy(), err_msg=f"trial {trial}")
 
 
+@pytest.mark.parametrize("K,loop", [(32, False), (48, True), (64, False)])
+def test_radius_graph_caps_above_32(K, loop):
+    """Neighbour caps past 32: torch_cluster's default max_num_neighbors = 32
+    with loop = False asks for 33 candidates (INTEGRATION.md's stub), up to 64
+    here.  Dense random clouds so the cap binds, both paths (n <= 8192: LDS
+    brute force; above: the cell-list pipeline with the 64-slot register
+    list), several examples, bit-exact against the brute-force oracle."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import engine
+    g = torch.Generator().manual_seed(11 + K)
+    for trial, (n, dim, r) in enumerate([(3000, 2, 1.2), (2500, 3, 1.6), (12000, 2, 0.7), (10000, 3, 0.9)]):
+        side = 10.0 if dim == 2 else 6.0
+        pos = torch.rand(n, dim, generator=g) * side
+        counts = [n // 2, n - n // 2]
+        ref = O.radius_graph(pos, counts, r, loop=loop, max_num_neighbors=K, method="bruteforce")
+        deg = torch.bincount(ref[1], minlength=n)
+        assert int(deg.max()) == K, "the cap should bind in this cloud"
+        ws = engine.StepWorkspace(n, 2, dim, 64, K, loop, torch.device("cuda"))
+        engine.radius_graph(ws, pos.cuda(), 0, dim, engine.ex_ptr_tensor(counts, "cuda"), 2, r)
+        e = ws.num_edges()
+        got = torch.stack([ws.send[:e], ws.recv[:e]]).cpu().to(torch.int64)
+        np.testing.assert_array_equal(got.numpy(), ref.numpy(), err_msg=f"K={K} loop={loop} trial {trial}")
+    # the static-graph entry (torch_cluster.radius_graph(pos, r, max_num_neighbors=K, loop=...))
+    pos = torch.rand(4000, 2, generator=g) * 10.0
+    csr = engine.radius_graph_csr(pos.cuda(), 1.0, K, loop)
+    ref = O.radius_graph(pos, [4000], 1.0, loop=loop, max_num_neighbors=K, method="bruteforce")
+    e = csr.num_edges
+    np.testing.assert_array_equal(torch.stack([csr.send[:e], csr.recv[:e]]).cpu().to(torch.int64).numpy(), ref.numpy())
+
+
 def test_3d_h128_against_oracle():
     """Config-4 shapes (3D, H=128) at a size the oracle finishes quickly."""
     from oracle import sgnn_oracle as O
