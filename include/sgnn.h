@@ -405,6 +405,21 @@ int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32
                           const float* vel_std, float wall_max, float wall_div,
                           const sgnn_saves* saves, const sgnn_mlp* enc, float* slab,
                           int32_t nslab, void* stream);
+/* The same for more than 32 particle types (up to 256; ntypes x hidden <=
+ * 40960): the per-type sums G[ntypes][H] of the encoder's first-layer
+ * gradient are not kept in the slab but formed from per-node dh rows by a
+ * deterministic two-pass type sum (fixed node order per 256-node block, then
+ * fixed block order) and written to G; the slab's G block is left unused.
+ * workspace: sgnn_type_sums_workspace_bytes(n, hidden, ntypes) bytes.
+ * Replaces the same autograd path as sgnn_encode_nodes_bwd with an
+ * nn.Embedding(ntypes, emb) of any size (learned_simulator.py:51-52). */
+int sgnn_encode_nodes_bwd_typed(const float* g, const float* pos_seq, int64_t n, int32_t T,
+                                int32_t dim, const int64_t* types, const float* emb_w, int32_t emb_dim,
+                                int32_t ntypes, const float* vel_mean, const float* vel_std,
+                                float wall_max, float wall_div, const sgnn_saves* saves,
+                                const sgnn_mlp* enc, float* slab, int32_t nslab, float* G,
+                                void* workspace, void* stream);
+size_t sgnn_type_sums_workspace_bytes(int64_t n, int32_t hidden, int32_t ntypes);
 /* Particle-type embedding gradient (learned_simulator.py:287-290 under
  * autograd): the ENC_NODE slab's trailing G[32][H] block (per-type sums of the
  * encoder's first-layer gradient, reduced) times the embedding columns of

@@ -142,6 +142,11 @@ SIGNATURES = {
                                              c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                              c_void_p, c_void_p, c_float, c_float, P_SAVES,
                                              P_MLP, c_void_p, c_int32, c_void_p]),
+    "sgnn_encode_nodes_bwd_typed": (ctypes.c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                                   c_void_p, c_void_p, c_int32, c_int32,
+                                                   c_void_p, c_void_p, c_float, c_float, P_SAVES,
+                                                   P_MLP, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "sgnn_type_sums_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int32, c_int32]),
     "sgnn_edge_latent_grad": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64,
                                              c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "sgnn_embedding_grad": (ctypes.c_int, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32,

@@ -1173,6 +1173,7 @@ struct EncNodeBwdArgs {
   const int64_t* types;  // particle types (use_emb) -> embedding features + per-type dh sums
   const float* emb_w;
   int emb_dim, use_emb;
+  float* dh_out;         // > 32 types: dh rows [n][H] out (k_type_sums forms G) instead of the one-hot G
 };
 
 template <int TH, int TKF, int NL>
@@ -1262,7 +1263,8 @@ __global__ __launch_bounds__(kBlock) void k_enc_node_bwd(EncNodeBwdArgs a) {
     __syncthreads();
     outer_tiles<NT1>(acc_w1, TH, TKF, bufA, ldh, 0, bufB, ldb, 0);
     __syncthreads();
-    if (a.use_emb) {
+    if (a.dh_out && valid) store_row_clayout<TH>(a.dh_out + i * H, dh);
+    if (a.use_emb && !a.dh_out) {
       // G[type][u] += dh[u] over this type's nodes (one-hot (x) dh); the
       // embedding gradient is G . W1[:, emb columns] (sgnn_embedding_grad)
       const int ty = valid ? (int)a.types[ic] : -1;
@@ -2332,13 +2334,49 @@ extern "C" int sgnn_decoder_loss_bwd(const float* pred, const float* pos_seq,
   return check_launch("decoder_loss_bwd");
 }
 
-extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
-                                     int32_t dim, const int64_t* types, const float* emb_w,
-                                     int32_t emb_dim, int32_t ntypes, int32_t use_emb,
-                                     const float* vel_mean, const float* vel_std,
-                                     float wall_max, float wall_div, const sgnn_saves* saves,
-                                     const sgnn_mlp* enc, float* slab, int32_t nslab,
-                                     void* stream) {
+namespace {
+constexpr int kTypeSumNodes = 256;   // nodes per k_type_sums workgroup
+constexpr int kMaxTypes = 256;
+
+// G[t][u] = sum over nodes i of type t of dh[i][u], deterministic: workgroup b
+// sums its node range in ascending order into LDS (thread u owns column u, so
+// no two threads touch one word), partials [b][t][u] are then summed over b in
+// ascending order by k_type_sums_reduce.
+__global__ __launch_bounds__(128) void k_type_sums(const float* dh, const int64_t* types, int64_t n, int H,
+                                                   int ntypes, float* partial) {
+  extern __shared__ float acc[];   // [ntypes][H]
+  for (int q = threadIdx.x; q < ntypes * H; q += blockDim.x) acc[q] = 0.0f;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kTypeSumNodes, i1 = min(i0 + kTypeSumNodes, n);
+  for (int u = threadIdx.x; u < H; u += blockDim.x)
+    for (int64_t i = i0; i < i1; ++i) {
+      const int64_t t = types[i];
+      if (t >= 0 && t < ntypes) acc[t * H + u] += dh[i * H + u];
+    }
+  __syncthreads();
+  for (int q = threadIdx.x; q < ntypes * H; q += blockDim.x)
+    partial[(int64_t)blockIdx.x * ntypes * H + q] = acc[q];
+}
+
+__global__ __launch_bounds__(256) void k_type_sums_reduce(const float* partial, int nblk, int count, float* G) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= count) return;
+  float s = 0.0f;
+  for (int b = 0; b < nblk; ++b) s += partial[(int64_t)b * count + q];
+  G[q] = s;
+}
+}  // namespace
+
+extern "C" size_t sgnn_type_sums_workspace_bytes(int64_t n, int32_t hidden, int32_t ntypes) {
+  const int64_t nblk = (n + kTypeSumNodes - 1) / kTypeSumNodes;
+  return sizeof(float) * ((size_t)n * hidden + (size_t)nblk * ntypes * hidden);
+}
+
+static int encode_nodes_bwd_impl(const float* g, const float* pos_seq, int64_t n, int32_t T, int32_t dim,
+                                 const int64_t* types, const float* emb_w, int32_t emb_dim, int32_t ntypes,
+                                 int32_t use_emb, const float* vel_mean, const float* vel_std, float wall_max,
+                                 float wall_div, const sgnn_saves* saves, const sgnn_mlp* enc, float* slab,
+                                 int32_t nslab, void* stream, float* dh_out) {
   using namespace sgnn;
   if (!enc || !g || !pos_seq || !vel_mean || !vel_std || !saves || !saves->h || !saves->yhat ||
       !saves->rstd || !slab || nslab < 1 || n <= 0)
@@ -2349,13 +2387,15 @@ extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64
   const int H = enc->hidden;
   const int feat = (T - 1) * dim + 1 + (use_emb ? emb_dim : 0);
   if (enc->in_dim != feat) return set_error(SGNN_ERR_INVALID, "encode_nodes_bwd: encoder input width");
-  if (use_emb && (!types || !emb_w || ntypes < 1 || ntypes > 32))
-    return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd: embeddings need types, weights, ntypes <= 32");
+  if (use_emb && (!types || !emb_w || ntypes < 1 || ntypes > (dh_out ? kMaxTypes : 32)))
+    return set_error(SGNN_ERR_UNSUPPORTED, dh_out ? "encode_nodes_bwd: embeddings need types, weights, ntypes <= 256"
+                                                  : "encode_nodes_bwd: embeddings need types, weights, ntypes <= 32 "
+                                                    "(sgnn_encode_nodes_bwd_typed: <= 256)");
   const int tkf = (feat + 31) / 32;
   EncNodeBwdArgs a{g, pos_seq, n, T, dim, feat, vel_mean, vel_std, wall_max, wall_div, saves->h,
                    saves->h2, saves->yhat, saves->rstd, last_w(enc), mid_w(enc), enc->ln_g, slab,
                    sgnn_bwd_slab_floats(SGNN_SLAB_ENC_NODE, H, feat, enc->nlin), types, emb_w,
-                   use_emb ? emb_dim : 0, use_emb};
+                   use_emb ? emb_dim : 0, use_emb, dh_out};
   const size_t lds = bwd_lds(SGNN_SLAB_ENC_NODE, H, tkf, enc->nlin);
   if (tkf == 1) {
     SGNN_BWD_DISPATCH(H, enc->nlin, (launch_bwd(k_enc_node_bwd<TH_, 1, NL_>, nslab, lds, stream, a)));
@@ -2365,6 +2405,44 @@ extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64
     return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd: > 64 node features");
   }
   return check_launch("encode_nodes_bwd");
+}
+
+extern "C" int sgnn_encode_nodes_bwd(const float* g, const float* pos_seq, int64_t n, int32_t T,
+                                     int32_t dim, const int64_t* types, const float* emb_w,
+                                     int32_t emb_dim, int32_t ntypes, int32_t use_emb,
+                                     const float* vel_mean, const float* vel_std,
+                                     float wall_max, float wall_div, const sgnn_saves* saves,
+                                     const sgnn_mlp* enc, float* slab, int32_t nslab,
+                                     void* stream) {
+  return encode_nodes_bwd_impl(g, pos_seq, n, T, dim, types, emb_w, emb_dim, ntypes, use_emb, vel_mean, vel_std,
+                               wall_max, wall_div, saves, enc, slab, nslab, stream, nullptr);
+}
+
+extern "C" int sgnn_encode_nodes_bwd_typed(const float* g, const float* pos_seq, int64_t n, int32_t T,
+                                           int32_t dim, const int64_t* types, const float* emb_w,
+                                           int32_t emb_dim, int32_t ntypes, const float* vel_mean,
+                                           const float* vel_std, float wall_max, float wall_div,
+                                           const sgnn_saves* saves, const sgnn_mlp* enc, float* slab,
+                                           int32_t nslab, float* G, void* workspace, void* stream) {
+  using namespace sgnn;
+  if (!G || !workspace || !enc) return set_error(SGNN_ERR_INVALID, "encode_nodes_bwd_typed: bad arguments");
+  const int H = enc->hidden;
+  float* dh = static_cast<float*>(workspace);
+  int st = encode_nodes_bwd_impl(g, pos_seq, n, T, dim, types, emb_w, emb_dim, ntypes, 1, vel_mean, vel_std,
+                                 wall_max, wall_div, saves, enc, slab, nslab, stream, dh);
+  if (st) return st;
+  if ((size_t)ntypes * H * sizeof(float) > 160 * 1024)
+    return set_error(SGNN_ERR_UNSUPPORTED, "encode_nodes_bwd_typed: ntypes x hidden > 40960");
+  const int nblk = (int)((n + kTypeSumNodes - 1) / kTypeSumNodes);
+  float* partial = dh + n * H;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t lds = sizeof(float) * (size_t)ntypes * H;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_type_sums), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  hipLaunchKernelGGL(k_type_sums, dim3(nblk), dim3(128), lds, s, dh, types, n, H, ntypes, partial);
+  const int count = ntypes * H;
+  hipLaunchKernelGGL(k_type_sums_reduce, dim3((count + 255) / 256), dim3(256), 0, s, partial, nblk, count, G);
+  return check_launch("encode_nodes_bwd_typed");
 }
 
 extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_t pos_stride,
@@ -2473,7 +2551,7 @@ extern "C" int sgnn_embedding_grad(const float* G, int32_t ntypes, int32_t hidde
                                    int32_t w1_ld, int32_t col0, int32_t emb_dim, float* demb,
                                    int32_t accumulate, void* stream) {
   using namespace sgnn;
-  if (!G || !w1 || !demb || ntypes < 1 || ntypes > 32 || hidden < 1 || emb_dim < 1)
+  if (!G || !w1 || !demb || ntypes < 1 || ntypes > 256 || hidden < 1 || emb_dim < 1)
     return set_error(SGNN_ERR_INVALID, "embedding_grad: bad arguments");
   hipLaunchKernelGGL(k_embedding_grad, dim3((ntypes * emb_dim + 255) / 256), dim3(256), 0,
                      static_cast<hipStream_t>(stream), G, ntypes, hidden, w1, w1_ld, col0, emb_dim,

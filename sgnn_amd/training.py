@@ -370,8 +370,8 @@ def check_trainable(epd: nn.Module, nparticle_types: int) -> None:
                                   "run inference only, on the width-generic kernels)")
     if epd.nmlp_layers not in (1, 2):
         raise NotImplementedError("HIP training path: nmlp_layers must be 1 or 2")
-    if nparticle_types > 32:
-        raise NotImplementedError("HIP training path: at most 32 particle types")
+    if nparticle_types > MAX_TYPES:
+        raise NotImplementedError(f"HIP training path: at most {MAX_TYPES} particle types")
 
 
 class _Timer:
@@ -399,10 +399,47 @@ def emb_args(inp: engine.StepInputs, emb_weight: Optional[torch.Tensor]):
     return inp.types.data_ptr(), emb_weight.data_ptr(), int(emb_weight.shape[1]), 1
 
 
+MAX_TYPES = 256   # particle types the training path differentiates (sgnn_encode_nodes_bwd_typed)
+
+
+def typed_embedding(emb_weight: Optional[torch.Tensor], use_emb: bool) -> bool:
+    """More than 32 particle types: the per-type sums G come from
+    sgnn_encode_nodes_bwd_typed (dh rows + a deterministic type sum) instead of
+    the encoder slab's one-hot G[32][H] block."""
+    return use_emb and int(emb_weight.shape[0]) > 32
+
+
+def encode_nodes_backward(tw, g: torch.Tensor, inp: engine.StepInputs, n: int, T: int, d: int,
+                          emb_weight: Optional[torch.Tensor], wall_max: float, wall_div: float,
+                          saves: SgnnSaves, enc: "ctypes.Structure", slab: int, nslab: int, stream: int) -> None:
+    """Encoder node-MLP backward (+ the per-type sums for the embedding
+    gradient): sgnn_encode_nodes_bwd, or its typed form past 32 types."""
+    L = lib()
+    ty, ew, ed, ue = emb_args(inp, emb_weight)
+    if typed_embedding(emb_weight, bool(ue)):
+        nt = int(emb_weight.shape[0])
+        need = int(L.sgnn_type_sums_workspace_bytes(n, tw.H, nt))
+        if getattr(tw, "type_ws", None) is None or tw.type_ws.numel() < need or tw.emb_gt.shape[0] != nt:
+            tw.type_ws = torch.empty(need, dtype=torch.uint8, device=g.device)
+            tw.emb_gt = torch.zeros(nt, tw.H, dtype=torch.float32, device=g.device)
+        check(L.sgnn_encode_nodes_bwd_typed(g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, ty, ew, ed, nt,
+                                            inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(wall_max),
+                                            float(wall_div), ctypes.byref(saves), ctypes.byref(enc), slab, nslab,
+                                            tw.emb_gt.data_ptr(), tw.type_ws.data_ptr(), stream),
+              "sgnn_encode_nodes_bwd_typed")
+        return
+    check(L.sgnn_encode_nodes_bwd(g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, ty, ew, ed,
+                                  int(emb_weight.shape[0]) if ue else 0, ue, inp.vel_mean.data_ptr(),
+                                  inp.vel_std.data_ptr(), float(wall_max), float(wall_div), ctypes.byref(saves),
+                                  ctypes.byref(enc), slab, nslab, stream), "sgnn_encode_nodes_bwd")
+
+
 def embedding_backward(tw, enc_w1: torch.Tensor, emb_weight: torch.Tensor, demb: torch.Tensor,
                        nvel: int, stream: int) -> None:
-    """dEmb = G . W1[:, emb columns] after the slab reduction filled tw.emb_g."""
-    check(lib().sgnn_embedding_grad(tw.emb_g.data_ptr(), int(emb_weight.shape[0]), tw.H, enc_w1.data_ptr(),
+    """dEmb = G . W1[:, emb columns] after the slab reduction filled tw.emb_g
+    (or sgnn_encode_nodes_bwd_typed filled tw.emb_gt)."""
+    G = tw.emb_gt if typed_embedding(emb_weight, True) else tw.emb_g
+    check(lib().sgnn_embedding_grad(G.data_ptr(), int(emb_weight.shape[0]), tw.H, enc_w1.data_ptr(),
                                     int(enc_w1.shape[1]), nvel + 1, int(emb_weight.shape[1]),
                                     demb.data_ptr(), 0, stream), "sgnn_embedding_grad")
 
@@ -487,7 +524,7 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
     L = lib()
     pk = engine.ParamPack.get(epd)
     use_emb = emb_weight is not None and inp.types is not None
-    tw.descriptors(epd, grads, use_emb)
+    tw.descriptors(epd, grads, use_emb and not typed_embedding(emb_weight, use_emb))
     ws = tw.f
     n, T, d = ws.n, ws.T, ws.dim
     s = stream_ptr(inp.pos_seq.device)
@@ -550,15 +587,9 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
     # the edge-latent pass and the edge-encoder backward
     ev["g"].record(main)
     side.wait_event(ev["g"])
-    ty, ew, ed, ue = emb_args(inp, emb_weight)
-    check(L.sgnn_encode_nodes_bwd(tw.g.data_ptr(), inp.pos_seq.data_ptr(), n, T, d, ty, ew, ed,
-                                  int(emb_weight.shape[0]) if ue else 0, ue,
-                                  inp.vel_mean.data_ptr(), inp.vel_std.data_ptr(), float(radius), 1.0,
-                                  ctypes.byref(_saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd,
-                                                      h2=tw.enc_h2)),
-                                  ctypes.byref(pk.enc_node), tw.slab(_hip.SLAB_ENC_NODE),
-                                  tw.nslab_of[_hip.SLAB_ENC_NODE], side.cuda_stream),
-          "sgnn_encode_nodes_bwd")
+    encode_nodes_backward(tw, tw.g, inp, n, T, d, emb_weight, radius, 1.0,
+                          _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2), pk.enc_node,
+                          tw.slab(_hip.SLAB_ENC_NODE), tw.nslab_of[_hip.SLAB_ENC_NODE], side.cuda_stream)
     ev["enc"].record(side)
     if tw.latent_pass:   # dE0 = sum_k 2^k W1e_k^T dh_k (the dW1e halves ran per layer)
         check(L.sgnn_edge_latent_grad(tw._dh_ptrs, ctypes.byref(pk.edge_arr), tw._scales, tw.L,

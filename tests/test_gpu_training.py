@@ -226,3 +226,51 @@ def test_workspace_reuse_across_batch_sizes_is_exact():
     lb, gb = step(tb, seq2)
     assert len(ta._tw) == 1
     assert la == lb and torch.equal(ga, gb)
+
+
+@pytest.mark.parametrize("ntypes,H", [(40, 64), (200, 128)])
+def test_many_particle_types_gradients_against_oracle(ntypes, H):
+    """More than 32 particle types (nn.Embedding(ntypes, 16), learned_simulator.py:
+    51-52): the per-type sums of the encoder's first-layer gradient come from
+    sgnn_encode_nodes_bwd_typed (dh rows + deterministic type sums) instead of
+    the slab's 32-row one-hot block.  Loss, every gradient (the embedding's
+    included) vs oracle autograd; two identical steps give bitwise-equal
+    gradients."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import synthetic
+    from sgnn_amd.learned_simulator import LearnedSimulator
+    from sgnn_amd.train import Trainer
+    T, R, L, dim, emb = 6, 0.75, 3, 2, 16
+    seq = synthetic.trajectory(synthetic.lattice_2d(40, 30), T + 1, seed=8)
+    n = seq.shape[0]
+    st = synthetic.normalization_stats(dim, noise_std=0.02)
+    stats = {k: {kk: torch.from_numpy(vv) for kk, vv in v.items()} for k, v in st.items()}
+    torch.manual_seed(12)
+    sim = LearnedSimulator(dim, (T - 1) * dim + 1 + emb, dim + 1, H, L, 1, H, R, stats, ntypes, emb)
+    state = {k: v.detach().clone().requires_grad_(True) for k, v in sim.state_dict().items()}
+    pos, nxt = torch.from_numpy(seq[:, :T]), torch.from_numpy(seq[:, T])
+    types_ = torch.from_numpy(np.random.default_rng(4).integers(0, ntypes, n)).to(torch.long)
+    strain = torch.from_numpy(np.random.default_rng(2).normal(0, 1, n).astype(np.float32))
+    noise = O.random_walk_noise(pos, 0.02, generator=torch.Generator().manual_seed(3))
+    osim = O.OracleSimulator(state, dim, L, R, stats, ntypes)
+    pa, ta, ps = osim.predict_accelerations(nxt, noise, pos, [n], types_)
+    ref_loss = O.training_loss(pa, ta, ps, strain)
+    ref_loss.backward()
+    assert state["_particle_type_embedding.weight"].grad is not None
+    sim = sim.cuda()
+    state0 = {k: v.detach().clone() for k, v in sim.state_dict().items()}
+    grads = []
+    for _ in range(2):
+        sim.load_state_dict(state0)
+        tr = Trainer(sim, lr_init=1e-3)
+        out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), [n], particle_types=types_.cuda(),
+                            noise=noise.cuda())
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.clone() for k, p in sim.named_parameters()})
+    assert abs(float(out["loss"]) - ref_loss.item()) <= 2e-5 * abs(ref_loss.item())
+    worst = 0.0
+    for k, p in sim.named_parameters():
+        assert torch.equal(grads[0][k], grads[1][k]), f"{k}: not bitwise reproducible"
+        if state[k].grad is not None:
+            worst = max(worst, _grad_close(grads[1][k].cpu().numpy(), state[k].grad.numpy(), k, rel=5e-4))
+    print(f"ntypes={ntypes} H={H}: worst relative grad error {worst:.3e}")
