@@ -106,3 +106,15 @@ def test_multi_scale_validation():
         sim._validate_static_graph()
     with pytest.raises(ValueError, match="GPU"):
         sim.predict_positions(torch.zeros(5, 6, 2), [5], None)
+
+
+def test_every_module_compiles():
+    """Every Python source of the package, the bench and the tools parses (a
+    syntax error in a module only the GPU path imports must fail here, on CPU)."""
+    import pathlib
+    import py_compile
+    root = pathlib.Path(__file__).resolve().parents[1]
+    files = sorted(root.glob("sgnn_amd/**/*.py")) + [root / "bench.py", root / "__graft_entry__.py"] + \
+        sorted(root.glob("tools/*.py")) + sorted(root.glob("oracle/*.py"))
+    for f in files:
+        py_compile.compile(str(f), doraise=True)

@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "caps_above or bruteforce" > gpurun_out/t_cap.log 2>&1 || { tail -30 gpurun_out/t_cap.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_training.py -k "caps_above or bruteforce or many_particle or particle_types" > gpurun_out/t_cap.log 2>&1 || { tail -30 gpurun_out/t_cap.log; exit 1; }
 tail -2 gpurun_out/t_cap.log
 timeout -k 10 900 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
 cat gpurun_out/bench_default.json
