@@ -370,7 +370,12 @@ int sgnn_decoder_loss_bwd(const float* pred, const float* pos_seq, const float* 
 int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* saves, const float* x_in,
                         const sgnn_mlp* node_fn, float* dagg, float* dxp, float* slab,
                         int32_t nslab, float* scratch, void* stream);
-/* saves: h, yhat, rstd (+ h2) as edge_layer wrote them. */
+/* saves: h, yhat, rstd (+ h2) as edge_layer wrote them.  With de0t: this
+ * layer's dE0 term is written (de0_accumulate bit 0: added) and its dW1e
+ * formed in-layer.  de0t = NULL (H = 64): both are left to
+ * sgnn_edge_latent_grad, except that de0_accumulate bit 1 (value 2) at
+ * nmlp_layers 1 forms this layer's dW1e in the kernel (slab dW1e block), so
+ * only the dE0 pass remains. */
 int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, const int32_t* send,
                         const int32_t* recv, int64_t n, const sgnn_saves* saves, const float* e0t,
                         float e_scale, const sgnn_mlp* edge_fn, float* du, float* cin,

@@ -416,7 +416,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_bwd(EdgeBwdArgs a) {
       zero<TH>(de);
       matvec_t<TH, TH, GW>(de, WeT, lde, dh);
       float* dtile = a.de0t + tile * (32 * H);
-      if (a.de0_accumulate) {
+      if (a.de0_accumulate & 1) {
         f32x16 old[TH];
         load_tiled<TH>(old, dtile);
 #pragma unroll
@@ -598,6 +598,11 @@ SGNN_DEV void swz_matvec_t(f32x16 (&acc)[2], const float* wt, const f32x16 (&x)[
     }
 }
 
+// DW1E: this layer's dW1e = sum_e dh (x) e0 as well (the caller's
+// de0_accumulate bit 1), through the same two item images after the dWl
+// product: one more outer product per chunk instead of a separate
+// k_edge_w1e_grad launch that re-reads the dh rows.
+template <bool DW1E>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
 void k_edge_bwd64(EdgeBwdArgs a) {
   constexpr int TH = 2, H = 64;
@@ -611,9 +616,9 @@ void k_edge_bwd64(EdgeBwdArgs a) {
   float* sA = bufA + w * 32 * H;    // this wave's rows (w*32 + j; (row & 15) == (j & 15))
   float* sB = bufB + w * 32 * H;
   const int tu = w >> 1, tv = w & 1;   // the wave's dWl tile
-  f32x16 acc;
+  f32x16 acc, acc_e;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  for (int r = 0; r < 16; ++r) acc[r] = acc_e[r] = 0.0f;
   f32x4 s_dbl = {0.0f, 0.0f, 0.0f, 0.0f}, s_dg = s_dbl, s_db = s_dbl;   // units 4 (lane & 15) + c
   const int64_t E = a.rowptr[a.n];
   const int64_t nchunks = (E + kChunk - 1) / kChunk;
@@ -669,11 +674,24 @@ void k_edge_bwd64(EdgeBwdArgs a) {
     swz_matvec_t(dh, wt, dy);
     relu_mask<TH>(dh, h1, valid);
     store_row_clayout_if<TH>(buf_rsrc(a.dh_rows + base * H), j * (4 * H), valid, dh);
+    if constexpr (DW1E) {
+      // dW1e += dh (x) e0 (the 2^k of the latent is applied in the slab reduction)
+      f32x16 e0[TH];
+      if (nvalid > 0) load_tiled<TH>(e0, a.e0t + tile * (32 * H));
+      else zero<TH>(e0);
+      zero_if<TH>(e0, !valid);
+      swz_store_items(sA, j, dh);
+      swz_store_items(sB, j, e0);
+      __syncthreads();
+      swz_outer(acc_e, bufA, 32 * tu, bufB, 32 * tv);
+      __syncthreads();
+    }
     segment_sum_rows<TH>(dh, rv, valid, __builtin_amdgcn_readlane(nb, 0), __builtin_amdgcn_readlane(nb, 1),
                          tile, a.du, a.cin, a.cout);
   }
   float* slab = a.slab + blockIdx.x * a.slab_stride;
   store_tile_rowmajor(slab + (32 * tu) * H + 32 * tv, H, acc);
+  if constexpr (DW1E) store_tile_rowmajor(slab + H * H + (32 * tu) * H + 32 * tv, H, acc_e);
   float* v = slab + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, 2);
   if (l < 16) {
     st4(v + w * H + 4 * l, s_dbl);
@@ -1761,7 +1779,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
       zero<TH>(de);
       matvec_t<TH, TH, GW>(de, WeT, lde, dh);
       float* dtile = a.de0t + tile * (32 * H);
-      if (a.de0_accumulate) {
+      if (a.de0_accumulate & 1) {
         f32x16 old[TH];
         load_tiled<TH>(old, dtile);
 #pragma unroll
@@ -2229,7 +2247,8 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
     return check_launch("edge_layer_bwd");
   }
   if (H == 64 && edge_fn->nlin == 2 && !de0t) {  // single-scale training: two workgroups per CU
-    launch_bwd(k_edge_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
+    if (de0_accumulate & 2) launch_bwd(k_edge_bwd64<true>, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
+    else launch_bwd(k_edge_bwd64<false>, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
     return check_launch("edge_layer_bwd");
   }
   const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin) - (de0t ? 0 : 4 * (size_t)H * (H + 4));

@@ -399,6 +399,7 @@ def emb_args(inp: engine.StepInputs, emb_weight: Optional[torch.Tensor]):
     return inp.types.data_ptr(), emb_weight.data_ptr(), int(emb_weight.shape[1]), 1
 
 
+DW1E_IN_LAYER = False  # experiment switch (tools/exp_train_ablate.py): measured slower, see DESIGN §3
 MAX_TYPES = 256   # particle types the training path differentiates (sgnn_encode_nodes_bwd_typed)
 
 
@@ -540,6 +541,9 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
     side, ev = tw.side(inp.pos_seq.device)
     main = torch.cuda.current_stream(inp.pos_seq.device)
     main.wait_event(ev["tcsr"])          # tptr / tperm of this step's graph
+    # H = 64, nmlp_layers 1: each layer's dW1e in its edge backward (k_edge_bwd64<true>) instead
+    # of a k_edge_w1e_grad launch per layer on the side stream
+    dw1e_in_layer = tw.latent_pass and tw.H == 64 and tw.nlin == 2 and DW1E_IN_LAYER
     for k in range(tw.L - 1, -1, -1):
         nsv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], h2=tw.n_h2[k])
         check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, ctypes.byref(nsv), tw.xs[k].data_ptr(),
@@ -555,10 +559,10 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                     ctypes.byref(pk.edge[k]), tw.du.data_ptr(), ws.cin.data_ptr(),
                                     ws.cout.data_ptr(), dh_rows.data_ptr(),
                                     None if tw.latent_pass else tw.de0t.data_ptr(),
-                                    int(k != tw.L - 1), tw.slab(_hip.SLAB_EDGE, k), tw.nslab_of[_hip.SLAB_EDGE],
-                                    tw.scratch.data_ptr(), ws.edge_cap, s),
+                                    (2 if dw1e_in_layer else int(k != tw.L - 1)), tw.slab(_hip.SLAB_EDGE, k),
+                                    tw.nslab_of[_hip.SLAB_EDGE], tw.scratch.data_ptr(), ws.edge_cap, s),
               "sgnn_edge_layer_bwd")
-        if tw.latent_pass:
+        if tw.latent_pass and not dw1e_in_layer:
             # dW1e_k = sum_e dh_k e0^T needs only this layer's dh: side stream,
             # beside the node-level backward of the layers below
             ev["g"].record(main)

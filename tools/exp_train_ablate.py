@@ -34,11 +34,33 @@ def run(tag):
 
 
 run("baseline")
+def noop_when(fn, which):
+    """sgnn_edge_latent_grad@dw: only the per-layer dW1e launches (de0t = NULL);
+    @de0: only the dE0 pass (de0t set)."""
+    def f(*a):
+        is_dw = a[8] is None
+        if (which == "dw") == is_dw:
+            return 0
+        return fn(*a)
+    return f
+
+
+from sgnn_amd import training as _training
+
+
 for spec in sys.argv[1:]:
+    if spec.startswith("flag:"):   # flag:NAME=0|1 toggles a module switch of sgnn_amd.training
+        name, _, val = spec[5:].partition("=")
+        old = getattr(_training, name)
+        setattr(_training, name, bool(int(val)))
+        run(spec)
+        setattr(_training, name, old)
+        continue
     names = spec.split("+")
     for nm in names:
-        orig[nm] = getattr(L_, nm)
-        setattr(L_, nm, lambda *a, **k: 0)
+        base, _, which = nm.partition("@")
+        orig[nm] = getattr(L_, base)
+        setattr(L_, base, noop_when(orig[nm], which) if which else (lambda *a, **k: 0))
     run("without " + spec)
     for nm in names:
-        setattr(L_, nm, orig[nm])
+        setattr(L_, nm.partition("@")[0], orig[nm])
