@@ -68,7 +68,7 @@ const char* sgnn_last_error(void);
  * (fp32, dims summed in order), same example (ex_ptr), at most K kept
  * (first K ascending; K+1 then self dropped when loop == 0).  recv[e] = i.
  * The reference's edge_index = [send ; recv] (int64) in the same order.
- * Capacity: edge_cap >= n * (loop ? K : K + 1); K + !loop <= 32.
+ * Capacity: edge_cap >= n * (loop ? K : K + 1); K + !loop <= 64.
  * pos: particle i at pos + i * pos_stride (so the last frame of a [N,T,d]
  * sequence can be passed without a copy).  ex_ptr: device int64 [n_ex+1].
  * workspace: sgnn_radius_workspace_bytes(n, K, loop) bytes, 256-B aligned.
@@ -313,17 +313,6 @@ int sgnn_rollout(const sgnn_epd* model, const sgnn_step_in* in, float* win_a, fl
  *   sgnn_reduce_slabs                     -> parameter gradients
  * Each *_bwd launches `nslab` persistent workgroups and writes one partial
  * slab of sgnn_bwd_slab_floats(kind, H, feat, nlin) floats per workgroup.
- * Slab fold (two-level reduction in the producing kernel; H = 64 paths of
- * sgnn_edge_layer_bwd (nmlp 1, de0t NULL), sgnn_node_layer_bwd (nmlp 1),
- * sgnn_uv_bwd, sgnn_encode_edges_bwd (nmlp 1) and the per-layer dW1e of
- * sgnn_edge_latent_grad; the other paths return SGNN_ERR_UNSUPPORTED): pass
- * nslab | G << 16 with 1 < G < 256 and ceil(nslab / G) <= 64.  Workgroups
- * [gG, gG + G) then leave the sum of their G slabs (fixed member order, so
- * still deterministic) in slab gG, and sgnn_reduce_slabs is given
- * ceil(nslab / G) slabs at stride G * slab_floats.  The slab region must be
- * followed by 128 uint32 counters, zero before the first call (the kernels
- * reset them): 64 for the layer kernel, 64 for the per-layer dW1e that
- * fills the same SLAB_EDGE region.
  * Slab layouts (row-major, W = 4 waves per workgroup, vectors as W partial
  * rows; Wl = last Linear, Wm = middle Linear (nlin = 3 only, appended), W1 =
  * first):

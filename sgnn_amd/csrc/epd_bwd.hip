@@ -129,51 +129,6 @@ SGNN_DEV void zero_acc(f32x16 (&acc)[NT]) {
     for (int r = 0; r < 16; ++r) acc[q][r] = 0.0f;
 }
 
-// Two-level slab reduction inside the producing kernel (the caller passes
-// nslab | G << 16 with G > 1; include/sgnn.h "slab fold"): workgroups
-// [gG, gG + G) form group g; the last of them to finish -- an agent-scope
-// counter ctr[g] -- sums the group's slabs over the ranges THIS kernel wrote,
-// member by member in index order, into the first member's slab and resets
-// ctr[g] for the next launch.  sgnn_reduce_slabs then reads ceil(nslab / G)
-// slabs at stride G x slab_stride instead of nslab.  Deterministic: the sum
-// order is fixed whichever member finishes last.  Counters: 64 per kernel
-// after the nslab slabs of the region (`which` selects the kernel's block of
-// 64 when two kernels fill one region, as the edge backward and its dW1e do).
-struct Fold {
-  uint32_t* ctr;   // null: no fold
-  int G;
-};
-
-SGNN_HOST_DEV inline Fold make_fold(float* slab, int nslab, int64_t stride, int G, int which) {
-  return G > 1 ? Fold{reinterpret_cast<uint32_t*>(slab + (int64_t)nslab * stride) + 64 * which, G} : Fold{nullptr, 1};
-}
-
-// off / len: NR ranges of the slab (floats, multiples of 4, 16-B aligned)
-template <int NR>
-SGNN_DEV void fold_slabs(float* slabs, int64_t stride, const int64_t (&off)[NR], const int64_t (&len)[NR], Fold f) {
-  if (!f.ctr) return;
-  __shared__ int s_last;
-  __threadfence();   // every wave: its slab stores performed and visible at agent scope before the count
-  __syncthreads();
-  const int nslab = (int)gridDim.x, g = (int)blockIdx.x / f.G;
-  const int members = min(f.G, nslab - g * f.G);
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(f.ctr + g, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-             (uint32_t)(members - 1);
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();   // acquire: the other members' slabs
-  float* dst = slabs + (int64_t)g * f.G * stride;
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-    for (int64_t i = 4 * (int64_t)threadIdx.x; i < len[r]; i += 4 * (int64_t)blockDim.x) {
-      f32x4 acc = ld4(dst + off[r] + i);
-      for (int m = 1; m < members; ++m) acc += ld4(dst + m * stride + off[r] + i);
-      st4(dst + off[r] + i, acc);
-    }
-  if (threadIdx.x == 0) __hip_atomic_store(f.ctr + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // per-wave lane-unit vector partial -> slab row (wave w)
 template <int TH>
 SGNN_DEV void store_lane_vec(float* dst, const float (&acc)[TH / 2 > 0 ? TH / 2 : 1]) {
@@ -347,7 +302,6 @@ struct EdgeBwdArgs {
   int de0_accumulate;
   float* slab;
   int64_t slab_stride;
-  Fold fold;   // k_edge_bwd64 only
 };
 
 // W1E: this layer's dE0 / dW1e products run in-layer (de0t != NULL, the
@@ -738,16 +692,12 @@ void k_edge_bwd64(EdgeBwdArgs a) {
   float* slab = a.slab + blockIdx.x * a.slab_stride;
   store_tile_rowmajor(slab + (32 * tu) * H + 32 * tv, H, acc);
   if constexpr (DW1E) store_tile_rowmajor(slab + H * H + (32 * tu) * H + 32 * tv, H, acc_e);
-  const int64_t vb = slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, 2);
-  float* v = slab + vb;
+  float* v = slab + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, 2);
   if (l < 16) {
     st4(v + w * H + 4 * l, s_dbl);
     st4(v + kWaves * H + w * H + 4 * l, s_dg);
     st4(v + 2 * kWaves * H + w * H + 4 * l, s_db);
   }
-  // this kernel's ranges: dWl (+ dW1e) and the three vectors
-  const int64_t off[2] = {0, vb}, len[2] = {(DW1E ? 2 : 1) * H * H, 3 * kWaves * H};
-  fold_slabs<2>(a.slab, a.slab_stride, off, len, a.fold);
 }
 
 // ===========================================================================
@@ -760,7 +710,6 @@ struct NodeBwdArgs {
   float *dagg, *dxp;
   float* slab;
   int64_t slab_stride;
-  Fold fold;   // k_node_bwd64 only
 };
 
 template <int TH, int NL>
@@ -881,7 +830,6 @@ struct UvBwdArgs {
   float* g;
   float* slab;
   int64_t slab_stride;
-  Fold fold;   // k_uv_bwd64 only
 };
 
 // H = 64 variant sized for two workgroups per CU (512 workgroups: every
@@ -940,8 +888,6 @@ void k_uv_bwd64(UvBwdArgs a) {
   store_tile_rowmajor(slab + (32 * tu) * 2 * H + 32 * tv, 2 * H, acc_i);
   store_tile_rowmajor(slab + H + (32 * tu) * 2 * H + 32 * tv, 2 * H, acc_j);
   if (l < 16) st4(slab + 2 * H * H + w * H + 4 * l, s_db1);
-  const int64_t off[1] = {0}, len[1] = {a.slab_stride};
-  fold_slabs<1>(a.slab, a.slab_stride, off, len, a.fold);
 }
 
 // matvec_t's global (L2) mode at H = 64 with one 16-unit k-group of weights
@@ -1070,8 +1016,6 @@ void k_node_bwd64(NodeBwdArgs a) {
     st4(v + 2 * kWaves * H + w * H + 4 * l, s_dg);
     st4(v + 3 * kWaves * H + w * H + 4 * l, s_db);
   }
-  const int64_t off[1] = {0}, len[1] = {a.slab_stride};
-  fold_slabs<1>(a.slab, a.slab_stride, off, len, a.fold);
 }
 
 // ===========================================================================
@@ -1379,7 +1323,6 @@ struct EncEdgeBwdArgs {
   const float *w1, *b1, *wl, *wm, *gamma;
   float* slab;
   int64_t slab_stride;
-  Fold fold;   // k_enc_edge_bwd64 only
 };
 
 template <int TH, int NL>
@@ -1642,8 +1585,6 @@ void k_enc_edge_bwd64(EncEdgeBwdArgs a) {
     st4(v + 2 * kWaves * H + w * H + 4 * l, s_dg);
     st4(v + 3 * kWaves * H + w * H + 4 * l, s_db);
   }
-  const int64_t off[1] = {0}, len[1] = {a.slab_stride};
-  fold_slabs<1>(a.slab, a.slab_stride, off, len, a.fold);
 }
 
 // ===========================================================================
@@ -2339,13 +2280,6 @@ const float* mid_w(const sgnn_mlp* m) { return m->nlin == 3 ? m->w2 : nullptr; }
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// nslab arguments of the backward entry points: low 16 bits the slab count, bits 16..23 the fold
-// group G (0 / 1: no fold; include/sgnn.h "slab fold").
-static int split_nslab(int32_t v, int* G) {
-  *G = (v >> 16) & 0xff;
-  return v & 0xffff;
-}
-
 extern "C" int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat, int32_t nlin) {
   if (kind < 0 || kind > SGNN_SLAB_ENC_EDGE || (nlin != 2 && nlin != 3) || hidden <= 0) return -1;
   const int64_t fpad = 32 * ((feat + 31) / 32);
@@ -2372,8 +2306,6 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
                                    int32_t de0_accumulate, float* slab, int32_t nslab,
                                    float* scratch, int64_t edge_cap, void* stream) {
   using namespace sgnn;
-  int fold_g = 0;
-  nslab = split_nslab(nslab, &fold_g);
   if (!edge_fn || !dagg || !rowptr || !send || !recv || !saves || !saves->h || !saves->yhat ||
       !saves->rstd || !e0t || !du || !cin || !cout || !dh_rows || !slab || nslab < 1 || n <= 0 ||
       (!de0t && edge_fn->hidden == 128))
@@ -2389,7 +2321,6 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
                 cin, cout, dh_rows, de0t, de0_accumulate, slab,
                 sgnn_bwd_slab_floats(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin)};
   if (H == 128) {
-    if (fold_g > 1) return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer_bwd: slab fold only on the H = 64 nmlp 1 path");
     if (!scratch || edge_cap < 1) return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: H=128 needs scratch");
     const int nl = edge_fn->nlin;
     const int64_t pad = 32 * ((edge_cap + 31) / 32);
@@ -2407,13 +2338,10 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
     return check_launch("edge_layer_bwd");
   }
   if (H == 64 && edge_fn->nlin == 2 && !de0t) {  // single-scale training: two workgroups per CU
-    if (fold_g > 1 && (nslab + fold_g - 1) / fold_g > 64) return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer_bwd: nslab > 64 G");
-    a.fold = make_fold(slab, nslab, a.slab_stride, fold_g, 0);
     if (de0_accumulate & 2) launch_bwd(k_edge_bwd64<true>, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
     else launch_bwd(k_edge_bwd64<false>, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
     return check_launch("edge_layer_bwd");
   }
-  if (fold_g > 1) return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer_bwd: slab fold only on the H = 64 nmlp 1 path");
   const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin) - (de0t ? 0 : 4 * (size_t)H * (H + 4));
   if (de0t) SGNN_BWD_DISPATCH(H, edge_fn->nlin, (launch_bwd(k_edge_bwd<TH_, NL_, true>, nslab, lds, stream, a)));
   else SGNN_BWD_DISPATCH(H, edge_fn->nlin, (launch_bwd(k_edge_bwd<TH_, NL_, false>, nslab, lds, stream, a)));
@@ -2425,8 +2353,6 @@ extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* 
                                    float* dxp, float* slab, int32_t nslab, float* scratch,
                                    void* stream) {
   using namespace sgnn;
-  int fold_g = 0;
-  nslab = split_nslab(nslab, &fold_g);
   if (!node_fn || !g || !saves || !saves->yhat || !saves->rstd || !saves->h || !saves->agg ||
       !x_in || !dagg || !dxp || !slab || nslab < 1 || n <= 0)
     return set_error(SGNN_ERR_INVALID, "node_layer_bwd: bad arguments");
@@ -2437,8 +2363,6 @@ extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* 
   NodeBwdArgs a{g, n, saves->yhat, saves->rstd, saves->h, saves->h2, saves->agg, x_in, node_fn->w1,
                 last_w(node_fn), mid_w(node_fn), node_fn->ln_g, dagg, dxp, slab,
                 sgnn_bwd_slab_floats(SGNN_SLAB_NODE, H, 0, node_fn->nlin)};
-  if (fold_g > 1 && !(H == 64 && node_fn->nlin == 2))
-    return set_error(SGNN_ERR_UNSUPPORTED, "node_layer_bwd: slab fold only on the H = 64 nmlp 1 path");
   if (H == 128) {
     if (!scratch) return set_error(SGNN_ERR_INVALID, "node_layer_bwd: H=128 needs scratch");
     const int nl = node_fn->nlin;
@@ -2458,8 +2382,6 @@ extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* 
     return check_launch("node_layer_bwd");
   }
   if (H == 64 && node_fn->nlin == 2) {  // two workgroups per CU
-    if (fold_g > 1 && (nslab + fold_g - 1) / fold_g > 64) return set_error(SGNN_ERR_UNSUPPORTED, "node_layer_bwd: nslab > 64 G");
-    a.fold = make_fold(slab, nslab, a.slab_stride, fold_g, 0);
     launch_bwd(k_node_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
     return check_launch("node_layer_bwd");
   }
@@ -2474,8 +2396,6 @@ extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, 
                            const sgnn_mlp* edge_fn, float* g, float* slab, int32_t nslab,
                            float* scratch, void* stream) {
   using namespace sgnn;
-  int fold_g = 0;
-  nslab = split_nslab(nslab, &fold_g);
   if (!edge_fn || !dxp || !du || !cin || !cout || !rowptr || !dh_rows || !tptr || !tperm ||
       !x_in || !g || !slab || nslab < 1 || n <= 0)
     return set_error(SGNN_ERR_INVALID, "uv_bwd: bad arguments");
@@ -2485,7 +2405,6 @@ extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, 
   UvBwdArgs a{dxp, du, cin, cout, rowptr, dh_rows, tptr, tperm, x_in, n, edge_fn->w1, g, slab,
               sgnn_bwd_slab_floats(SGNN_SLAB_UV, H, 0, edge_fn->nlin)};
   if (H == 128) {
-    if (fold_g > 1) return set_error(SGNN_ERR_UNSUPPORTED, "uv_bwd: slab fold only at H = 64");
     if (!scratch) return set_error(SGNN_ERR_INVALID, "uv_bwd: H=128 needs scratch");
     UvItemsArgs p{a, scratch, scratch + n * H};
     launch_bwd(k_uv_items, nslab, 0, stream, p);
@@ -2494,8 +2413,6 @@ extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, 
     run_wgrad<4, 4>(wg(p.dv_out, 0, H, x_in, 0, H, slab, H, 2 * H, -1, ss, n, nullptr), nslab, stream);
     return check_launch("uv_bwd");
   }
-  if (fold_g > 1 && (nslab + fold_g - 1) / fold_g > 64) return set_error(SGNN_ERR_UNSUPPORTED, "uv_bwd: nslab > 64 G");
-  a.fold = make_fold(slab, nslab, a.slab_stride, fold_g, 0);
   launch_bwd(k_uv_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
   return check_launch("uv_bwd");
 }
@@ -2645,8 +2562,6 @@ extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_
                                      int32_t nslab, float* scratch, int64_t edge_cap,
                                      void* stream) {
   using namespace sgnn;
-  int fold_g = 0;
-  nslab = split_nslab(nslab, &fold_g);
   if (!enc || !de0t || !pos || !rowptr || !send || !recv || !saves || !saves->yhat ||
       !saves->rstd || !slab || nslab < 1 || n <= 0)
     return set_error(SGNN_ERR_INVALID, "encode_edges_bwd: bad arguments");
@@ -2657,8 +2572,6 @@ extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_
   EncEdgeBwdArgs a{de0t, pos, pos_stride, dim, radius, rowptr, send, recv, n, saves->h2,
                    saves->yhat, saves->rstd, enc->w1, enc->b1, last_w(enc), mid_w(enc), enc->ln_g,
                    slab, sgnn_bwd_slab_floats(SGNN_SLAB_ENC_EDGE, H, 0, enc->nlin)};
-  if (fold_g > 1 && !(H == 64 && enc->nlin == 2 && dim <= 3))
-    return set_error(SGNN_ERR_UNSUPPORTED, "encode_edges_bwd: slab fold only on the H = 64 nmlp 1 path");
   if (H == 128) {
     if (!scratch || edge_cap < 1) return set_error(SGNN_ERR_INVALID, "encode_edges_bwd: H=128 needs scratch");
     const int nl = enc->nlin;
@@ -2679,8 +2592,6 @@ extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_
     return check_launch("encode_edges_bwd");
   }
   if (H == 64 && enc->nlin == 2 && dim <= 3) {  // single-scale training: two workgroups per CU
-    if (fold_g > 1 && (nslab + fold_g - 1) / fold_g > 64) return set_error(SGNN_ERR_UNSUPPORTED, "encode_edges_bwd: nslab > 64 G");
-    a.fold = make_fold(slab, nslab, a.slab_stride, fold_g, 0);
     launch_bwd(k_enc_edge_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
     return check_launch("encode_edges_bwd");
   }
@@ -2776,7 +2687,6 @@ struct EdgeLatentGradArgs {
   const float* e0t;
   float* de0t;
   int64_t slab_stride;
-  Fold fold;   // k_edge_w1e_grad (the region's second counter block)
 };
 
 // One pass over the edges after the layer backwards (H = 64), per 128-edge
@@ -2917,8 +2827,6 @@ __global__ __launch_bounds__(kBlock) void k_edge_w1e_grad(EdgeLatentGradArgs a) 
     }
   }
   store_outer<NT>(a.slab[0] + blockIdx.x * a.slab_stride + H * H, H, TH, TH, acc);
-  const int64_t off[1] = {H * H}, len[1] = {H * H};
-  fold_slabs<1>(a.slab[0], a.slab_stride, off, len, a.fold);
 }
 
 // dE0 = sum_k 2^k W1e_k^T dh_k over L <= 5 layers (H = 64): the L swizzled
@@ -2991,8 +2899,6 @@ extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp
                                      int64_t n, int64_t edge_cap, const float* e0t, float* de0t,
                                      float* const* slabs, int32_t nslab, void* stream) {
   using namespace sgnn;
-  int fold_g = 0;
-  nslab = split_nslab(nslab, &fold_g);
   if (!dh_rows || !edge_fns || !scales || !rowptr || !e0t || (!de0t && !slabs) || nslab < 1 ||
       nlayers < 1 || n <= 0 || edge_cap < 1)
     return set_error(SGNN_ERR_INVALID, "edge_latent_grad: bad arguments");
@@ -3024,15 +2930,11 @@ extern "C" int sgnn_edge_latent_grad(const float* const* dh_rows, const sgnn_mlp
       b.slab[0] = a.slab[k];
       b.scale[0] = a.scale[k];
       b.nlayers = 1;
-      // the region's second counter block (the edge backward folds its own ranges with the first)
-      if (fold_g > 1 && (nslab + fold_g - 1) / fold_g > 64) return set_error(SGNN_ERR_UNSUPPORTED, "edge_latent_grad: nslab > 64 G");
-      b.fold = make_fold(a.slab[k], nslab, a.slab_stride, fold_g, 1);
       launch_bwd(k_edge_w1e_grad<2>, nslab, 4 * (size_t)(2 * kChunk * (H + 4)), stream, b);
     }
     return check_launch("edge_latent_grad");
   }
   const bool dw = slabs != nullptr;
-  if (dw && fold_g > 1) return set_error(SGNN_ERR_UNSUPPORTED, "edge_latent_grad: slab fold only for the per-layer dW1e");
   switch (nlayers) {
     case 1: launch_latent<1>(a, nslab, stream, dw); break;
     case 2: launch_latent<2>(a, nslab, stream, dw); break;

@@ -25,11 +25,6 @@ WIDE_NSLAB = 256     # the other single-scale variants (H = 64 with nmlp_layers 
                      # one workgroup per CU, so 512 would run in two rounds
 MS_NSLAB = 256      # multi-scale (H = 128 items / weight-gradient kernels, one workgroup per CU)
 NODE_NSLAB = 256     # node-level backward kernels (128 measured slower: fewer CUs busy)
-SLAB_FOLD = 0        # two-level slab reduction group (include/sgnn.h "slab fold"): > 1 makes the H = 64,
-#                      nmlp 1 backward kernels sum their slabs G at a time in-kernel.  Off: at G = 16 the
-#                      C2 step measured 2.44 -> 5.19 ms (every wave's agent-scope release writes back its
-#                      XCD's L2 before the group count)
-FOLD_CTR_FLOATS = 128  # counter blocks after a folded slab region (64 per kernel, two kernels per EDGE region)
 
 
 class FlatParams:
@@ -81,11 +76,9 @@ class GradLayout:
     uploaded once per (slab arena, gradient buffers)."""
 
     def __init__(self, H: int, nl: int, feat: int, dim: int, arena: torch.Tensor,
-                 slab_off: Dict[tuple, int], slab_floats: Dict[int, int], nslab_of: Dict[int, int],
-                 fold_of: Optional[Dict[int, int]] = None):
+                 slab_off: Dict[tuple, int], slab_floats: Dict[int, int], nslab_of: Dict[int, int]):
         self.H, self.nl, self.feat, self.dim = H, nl, feat, dim
         self.arena, self.slab_off, self.slab_floats, self.nslab_of = arena, slab_off, slab_floats, nslab_of
-        self.fold_of = fold_of or {}
         self.descs: List[SgnnReduceDesc] = []
 
     def add(self, kind, k, offset, dst, nrows, ncols, src_ld, dst_ld=None, nrep=1, rep_stride=0,
@@ -93,12 +86,10 @@ class GradLayout:
         d = SgnnReduceDesc()
         d.src = self.arena.data_ptr() + 4 * self.slab_off[(kind, k)]
         d.dst = dst.data_ptr() + 4 * dst_off
-        G = self.fold_of.get(kind, 1)
-        # folded kinds: the kernels left the group sums in every G-th slab
-        d.slab_stride = self.slab_floats[kind] * G
+        d.slab_stride = self.slab_floats[kind]
         d.offset = offset
         d.rep_stride = rep_stride
-        d.nslab, d.nrep, d.src_ld = -(-self.nslab_of[kind] // G), nrep, src_ld
+        d.nslab, d.nrep, d.src_ld = self.nslab_of[kind], nrep, src_ld
         d.nrows, d.ncols = nrows, ncols
         d.dst_ld = dst_ld if dst_ld is not None else ncols
         d.accumulate = 0
@@ -214,35 +205,22 @@ class SlabArena:
     """One fp32 arena holding every backward kernel's per-workgroup partial slabs."""
 
     def __init__(self, H: int, nl: int, feat: int, keys: List[tuple], nslab_of: Dict[int, int],
-                 device: torch.device, fold_of: Optional[Dict[int, int]] = None):
+                 device: torch.device):
         L = lib()
         self.slab_floats = {k: int(L.sgnn_bwd_slab_floats(k, H, feat, nl)) for k in range(6)}
         self.nslab_of = nslab_of
-        self.fold_of = {k: g for k, g in (fold_of or {}).items() if g > 1}
         self.slab_off: Dict[Tuple[int, int], int] = {}
         off = 0
-        tails = []
         for key in keys:
             self.slab_off[key] = off
             off += nslab_of[key[0]] * self.slab_floats[key[0]]
-            if key[0] in self.fold_of:    # the fold counters follow the region's slabs
-                tails.append(off)
-                off += FOLD_CTR_FLOATS
         self.arena = torch.empty(max(off, 1), dtype=torch.float32, device=device)
-        for t in tails:                    # counters start at zero; the kernels reset them after use
-            self.arena[t:t + FOLD_CTR_FLOATS].zero_()
 
     def ptr(self, kind: int, k: int = 0) -> int:
         return self.arena.data_ptr() + 4 * self.slab_off[(kind, k)]
 
-    def nslab_arg(self, kind: int) -> int:
-        """The nslab argument of the backward entry points: count | fold group << 16."""
-        G = self.fold_of.get(kind, 1)
-        return self.nslab_of[kind] | ((G << 16) if G > 1 else 0)
-
     def layout(self, H, nl, feat, dim) -> GradLayout:
-        return GradLayout(H, nl, feat, dim, self.arena, self.slab_off, self.slab_floats, self.nslab_of,
-                          self.fold_of)
+        return GradLayout(H, nl, feat, dim, self.arena, self.slab_off, self.slab_floats, self.nslab_of)
 
 
 def default_nslab(H: int, nlin: int) -> int:
@@ -325,10 +303,7 @@ class TrainWorkspace:
         keys = [(_hip.SLAB_DECODER, 0)] + [(_hip.SLAB_NODE, k) for k in range(nl)] + \
                [(_hip.SLAB_EDGE, k) for k in range(nl)] + [(_hip.SLAB_UV, k) for k in range(nl)] + \
                [(_hip.SLAB_ENC_NODE, 0), (_hip.SLAB_ENC_EDGE, 0)]
-        # H = 64, nmlp_layers 1: the *_bwd64 kernels (and the per-layer dW1e) fold their slabs in-kernel
-        fold = SLAB_FOLD if (H == 64 and self.nlin == 2 and SLAB_FOLD > 1) else 1
-        self.fold_of = {_hip.SLAB_EDGE: fold, _hip.SLAB_NODE: fold, _hip.SLAB_UV: fold, _hip.SLAB_ENC_EDGE: fold}
-        self.slabs = SlabArena(H, self.nlin, self.feat, keys, self.nslab_of, device, self.fold_of)
+        self.slabs = SlabArena(H, self.nlin, self.feat, keys, self.nslab_of, device)
         self.arena = self.slabs.arena
         self.loss_out = torch.zeros(8, **f32)
         self.emb_g = torch.zeros(32, H, **f32)   # per-type dh sums (particle-type embeddings)
@@ -357,9 +332,6 @@ class TrainWorkspace:
 
     def slab(self, kind: int, k: int = 0) -> int:
         return self.slabs.ptr(kind, k)
-
-    def nslab_arg(self, kind: int) -> int:
-        return self.slabs.nslab_arg(kind)
 
     def tws_ptr(self) -> int:
         return (self.tws.data_ptr() + 255) & ~255
@@ -576,7 +548,7 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
         nsv = _saves(h=tw.n_h[k], yhat=tw.n_yh[k], rstd=tw.n_rstd[k], agg=tw.n_agg[k], h2=tw.n_h2[k])
         check(L.sgnn_node_layer_bwd(tw.g.data_ptr(), n, ctypes.byref(nsv), tw.xs[k].data_ptr(),
                                     ctypes.byref(pk.node[k]), tw.dagg.data_ptr(), tw.dxp.data_ptr(),
-                                    tw.slab(_hip.SLAB_NODE, k), tw.nslab_arg(_hip.SLAB_NODE),
+                                    tw.slab(_hip.SLAB_NODE, k), tw.nslab_of[_hip.SLAB_NODE],
                                     tw.scratch.data_ptr(), s),
               "sgnn_node_layer_bwd")
         with _Timer(timers, "k_edge_bwd"):
@@ -588,7 +560,7 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                     ws.cout.data_ptr(), dh_rows.data_ptr(),
                                     None if tw.latent_pass else tw.de0t.data_ptr(),
                                     (2 if dw1e_in_layer else int(k != tw.L - 1)), tw.slab(_hip.SLAB_EDGE, k),
-                                    tw.nslab_arg(_hip.SLAB_EDGE), tw.scratch.data_ptr(), ws.edge_cap, s),
+                                    tw.nslab_of[_hip.SLAB_EDGE], tw.scratch.data_ptr(), ws.edge_cap, s),
               "sgnn_edge_layer_bwd")
         if tw.latent_pass and not dw1e_in_layer:
             # dW1e_k = sum_e dh_k e0^T needs only this layer's dh: side stream,
@@ -600,12 +572,12 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                           ctypes.addressof(pk.edge_arr) + ctypes.sizeof(_hip.SgnnMlp) * k,
                                           ctypes.addressof(tw._scales) + 4 * k, 1, ws.rowptr.data_ptr(), n,
                                           ws.edge_cap, ws.e0t.data_ptr(), None, slab_k,
-                                          tw.nslab_arg(_hip.SLAB_EDGE), side.cuda_stream),
+                                          tw.nslab_of[_hip.SLAB_EDGE], side.cuda_stream),
                   "sgnn_edge_latent_grad")
         check(L.sgnn_uv_bwd(tw.dxp.data_ptr(), tw.du.data_ptr(), ws.cin.data_ptr(), ws.cout.data_ptr(),
                             ws.rowptr.data_ptr(), dh_rows.data_ptr(), tw.tptr.data_ptr(),
                             tw.tperm.data_ptr(), tw.xs[k].data_ptr(), n, ctypes.byref(pk.edge[k]),
-                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_arg(_hip.SLAB_UV),
+                            tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, k), tw.nslab_of[_hip.SLAB_UV],
                             tw.scratch.data_ptr(), s),
               "sgnn_uv_bwd")
         # layer k's slabs (NODE, EDGE + its dW1e on the side stream, UV) are
@@ -633,7 +605,7 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                                   ws.recv.data_ptr(), n,
                                   ctypes.byref(_saves(yhat=tw.ee_yh, rstd=tw.ee_rstd, h2=tw.ee_h2)),
                                   ctypes.byref(pk.enc_edge), tw.slab(_hip.SLAB_ENC_EDGE),
-                                  tw.nslab_arg(_hip.SLAB_ENC_EDGE), tw.scratch.data_ptr(), ws.edge_cap, s),
+                                  tw.nslab_of[_hip.SLAB_ENC_EDGE], tw.scratch.data_ptr(), ws.edge_cap, s),
           "sgnn_encode_edges_bwd")
     main.wait_event(ev["enc"])
     check(L.sgnn_reduce_slabs(tw._descs_dev.data_ptr(), tw._block_start.data_ptr(), tw._ndesc,
