@@ -85,6 +85,18 @@ class DataParallel:
     def global_count(self, n_local: int, device) -> int:
         return self.layout(n_local, device)[0]
 
+    def overlaps_buckets(self) -> bool:
+        """Per-layer gradient buckets all-reduced on the side stream while the
+        layers below run their backward (device collectives only: gloo stages
+        device buffers through host memory, so it keeps the one collective)."""
+        return OVERLAP_BUCKETS and self.world > 1 and not self.host_staging
+
+    def allreduce_async(self, t: torch.Tensor, stream: torch.cuda.Stream):
+        """SUM all-reduce of `t` ordered after the work queued on `stream`; the
+        returned handle's wait() orders the caller's current stream after it."""
+        with torch.cuda.stream(stream):
+            return dist.all_reduce(t, group=self.group, async_op=True)
+
     def allreduce_(self, *tensors: torch.Tensor) -> None:
         """SUM all-reduce (RCCL over xGMI on MI355X; gloo in CPU tests)."""
         if self.world == 1:
@@ -112,6 +124,28 @@ def split_batch(idx: Sequence[int], rank: int, world: int) -> Optional[List[int]
     q, r = divmod(len(idx), world)
     start = rank * q + min(rank, r)
     return idx[start:start + q + (1 if rank < r else 0)]
+
+
+OVERLAP_BUCKETS = True   # DataParallel.overlaps_buckets
+
+
+def layer_ranges(epd, flat: training.FlatParams) -> Tuple[List[Tuple[int, int]], Tuple[int, int]]:
+    """[start, end) of every interaction layer's parameters in the flat
+    gradient buffer (module.parameters() order keeps each layer contiguous),
+    and the span [lo, hi) they cover together: the buckets of the overlapped
+    all-reduce are the layers, then [0, lo) (embedding, encoder) and [hi, end)
+    (decoder, loss sums)."""
+    out = []
+    for layer in epd._processor.gnn_stacks:
+        offs = sorted(flat.offsets[id(p)] for p in layer.parameters())
+        s, e = offs[0][0], offs[-1][0] + offs[-1][1]
+        if e - s != sum(n for _, n in offs):
+            raise RuntimeError("interaction layer parameters are not contiguous in the flat buffer")
+        out.append((s, e))
+    lo, hi = min(r[0] for r in out), max(r[1] for r in out)
+    if hi - lo != sum(e - s for s, e in out):
+        raise RuntimeError("interaction layers are not contiguous in the flat buffer")
+    return out, (lo, hi)
 
 
 class Trainer:
@@ -181,12 +215,26 @@ class Trainer:
         radius = self.sim._connectivity_radius
         emb = self.sim._particle_type_embedding.weight if self.sim._nparticle_types > 1 else None
         training.train_forward(self.epd, radius, inp, tw, timers=timers, emb_weight=emb)
+        works, layer_done = [], None
+        if self.dp.overlaps_buckets():
+            ranges, (lo, hi) = layer_ranges(self.epd, self.flat)
+
+            def layer_done(k, stream):   # layer k's gradients are final once its slab reduction ran
+                works.append(self.dp.allreduce_async(self.flat.comm[ranges[k][0]:ranges[k][1]], stream))
         training.train_backward(self.epd, radius, inp, tw, self.grads, timers=timers,
                                 next_pos=next_position.to(torch.float32).contiguous(), noise=noise,
                                 next_strain=next_strain.to(torch.float32).contiguous(),
                                 w_pos=self.w_pos, w_strain=self.w_strain, inv_count=1.0 / n_global,
-                                emb_weight=emb, emb_grad=self.grads.get("_particle_type_embedding.weight"))
-        self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
+                                emb_weight=emb, emb_grad=self.grads.get("_particle_type_embedding.weight"),
+                                layer_done=layer_done)
+        if layer_done is None:
+            self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
+        else:
+            # the layers' buckets went out during the backward; embedding / encoder and decoder / loss
+            # sums after the final slab reduction, then the launch stream waits for all of them
+            self.dp.allreduce_(self.flat.comm[:lo], self.flat.comm[hi:])
+            for w in works:
+                w.wait()
         self.opt.step()
         # train.py:276-278: LR for the NEXT step, computed from the pre-increment step
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6

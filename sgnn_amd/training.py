@@ -517,8 +517,11 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
                    next_strain: Optional[torch.Tensor] = None, w_pos: float = 1.0,
                    w_strain: float = 1.0, inv_count: float = 1.0, timers: Optional[dict] = None,
                    emb_weight: Optional[torch.Tensor] = None,
-                   emb_grad: Optional[torch.Tensor] = None) -> None:
+                   emb_grad: Optional[torch.Tensor] = None, layer_done=None) -> None:
     """Gradients of every parameter into `grads` (name -> tensor views);
+    layer_done(k, side_stream), when given, is called as soon as layer k's
+    slab reduction is queued on the side stream (its gradients are final
+    there: the data-parallel trainer starts that layer's all-reduce);
     with emb_weight, the particle-type embedding gradient into emb_grad.
     With dpred: dL/dpred is given (autograd path); otherwise the loss of
     train.py:257-268 is differentiated in-kernel (its sums land in tw.loss_out)."""
@@ -587,6 +590,8 @@ def train_backward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tr
         side.wait_event(ev["g"])
         dd, bs, nd, nb = tw._reduce_layer[k]
         check(L.sgnn_reduce_slabs(dd.data_ptr(), bs.data_ptr(), nd, nb, side.cuda_stream), "sgnn_reduce_slabs")
+        if layer_done is not None:
+            layer_done(k, side)
     # the encoder-node backward needs only g = dL/dx_0: side stream, beside
     # the edge-latent pass and the edge-encoder backward
     ev["g"].record(main)

@@ -49,14 +49,20 @@ def _result(tr, losses):
             "param": tr.flat.param.detach().cpu().clone()}
 
 
-def run_single_scale(graph_ids):
+def run_single_scale(graph_ids, overlap=False):
     """STEPS Trainer steps on the concatenation of `graph_ids` (this process's
-    share of the global batch); DP bookkeeping from the default process group."""
+    share of the global batch); DP bookkeeping from the default process group.
+    overlap: the per-layer gradient buckets go out asynchronously on the side
+    stream during the backward (the RCCL path), here through gloo's own
+    device-tensor all-reduce instead of the host staging."""
     from sgnn_amd.learned_simulator import LearnedSimulator
     from sgnn_amd.train import Trainer
     torch.manual_seed(7)
     sim = LearnedSimulator(2, 21, 3, 64, 5, 1, 64, 0.6, _stats(), 1, 9).cuda()
     tr = Trainer(sim, lr_init=LR)
+    if overlap:
+        tr.dp.host_staging = False
+        assert tr.dp.world == 1 or tr.dp.overlaps_buckets()
     wins = [_window(nx, ny, T_SS, 100 + g) for g, (nx, ny) in enumerate(SS_GRAPHS)]
     losses = []
     for s in range(STEPS):
@@ -92,4 +98,9 @@ def run_multi_scale(graph_ids):
     return _result(tr, losses)
 
 
-CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, MS_GRAPHS, MS_RANKS)}
+def run_single_scale_overlap(graph_ids):
+    return run_single_scale(graph_ids, overlap=True)
+
+
+CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, MS_GRAPHS, MS_RANKS),
+         "ss_overlap": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS)}

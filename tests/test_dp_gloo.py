@@ -156,3 +156,32 @@ def test_dp_epoch_with_odd_sample_count_has_matching_collectives():
     steps = [[p is not None for p in plan] for plan in plans]
     assert steps[0] == steps[1]                            # same number of collectives per rank
     assert steps[0].count(False) == 1 and steps[0][-1] is False
+
+
+def test_layer_buckets_tile_the_flat_gradient():
+    """The overlapped data-parallel all-reduce sends each interaction layer's
+    gradient slice as soon as its slab reduction is queued, then [0, lo) and
+    [hi, end): the buckets must be contiguous, disjoint, in layer order, and
+    cover the flat buffer (gradients + loss tail) exactly once."""
+    import torch
+    from sgnn_amd import synthetic, training
+    from sgnn_amd.learned_simulator import LearnedSimulator
+    from sgnn_amd.train import layer_ranges
+    st = synthetic.normalization_stats(2, noise_std=0.02)
+    stats = {k: {kk: torch.from_numpy(vv) for kk, vv in v.items()} for k, v in st.items()}
+    for ntypes, emb in ((1, 9), (3, 4)):
+        sim = LearnedSimulator(2, 21 + (emb if ntypes > 1 else 0), 3, 64, 5, 1, 64, 0.6, stats, ntypes, emb)
+        flat = training.FlatParams(sim)
+        ranges, (lo, hi) = layer_ranges(sim._encode_process_decode, flat)
+        assert len(ranges) == 5 and ranges[0][0] == lo and ranges[-1][1] == hi
+        for (s0, e0), (s1, e1) in zip(ranges, ranges[1:]):
+            assert e0 == s1 and s0 < e0
+        cover = torch.zeros(flat.comm.numel(), dtype=torch.int32)
+        for s, e in [(0, lo)] + ranges + [(hi, flat.comm.numel())]:
+            cover[s:e] += 1
+        assert bool((cover == 1).all())
+        # every processor parameter's gradient view lies inside its own layer's bucket
+        for k, layer in enumerate(sim._encode_process_decode._processor.gnn_stacks):
+            for p in layer.parameters():
+                off, n = flat.offsets[id(p)]
+                assert ranges[k][0] <= off and off + n <= ranges[k][1]

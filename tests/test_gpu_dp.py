@@ -32,7 +32,7 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("case", ["ss", "ms"])
+@pytest.mark.parametrize("case", ["ss", "ms", "ss_overlap"])
 def test_two_ranks_match_one_process(case, tmp_path):
     from tests.dp_cases import CASES, LR, STEPS
     run, _, ranks = CASES[case]
