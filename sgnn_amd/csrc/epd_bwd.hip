@@ -1701,21 +1701,21 @@ constexpr int kHalfChunk = 64;
 // One 64-item chunk of U units (starting at unit u0 of a USRC-unit operand) in
 // registers: thread t holds float4 groups t, t + 256, ... (NPT of them), so the
 // next chunk's loads are in flight during this chunk's MFMAs.
-template <int U>
+template <int U, int NTH>
 struct ChunkRegs {
-  static constexpr int NPT = kHalfChunk * U / 4 / kBlock;
+  static constexpr int NPT = kHalfChunk * U / 4 / NTH;
   f32x4 v[NPT];
 };
 
-template <int U, int USRC>
-SGNN_DEV void fetch_sub(ChunkRegs<U>& r, const float* src, int tiled, int ld, int u0, int64_t item0,
+template <int U, int USRC, int NTH>
+SGNN_DEV void fetch_sub(ChunkRegs<U, NTH>& r, const float* src, int tiled, int ld, int u0, int64_t item0,
                         int64_t nitems) {
-  constexpr int per_tile = (U / 32) * 4 * 64;
+  constexpr int per_tile = (U / 32) * 4 * 64;   // float4 groups per 32-item tile (tiled layout)
   constexpr int Q = U / 4;
   const int g0 = (u0 / 32) * 4;
 #pragma unroll
-  for (int k = 0; k < ChunkRegs<U>::NPT; ++k) {
-    const int idx = threadIdx.x + k * kBlock;
+  for (int k = 0; k < ChunkRegs<U, NTH>::NPT; ++k) {
+    const int idx = threadIdx.x + k * NTH;
     f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
     if (tiled) {
       const int q = idx / per_tile, rem = idx - q * per_tile;
@@ -1730,12 +1730,13 @@ SGNN_DEV void fetch_sub(ChunkRegs<U>& r, const float* src, int tiled, int ld, in
   }
 }
 
-template <int U>
-SGNN_DEV void put_sub(float* img, const ChunkRegs<U>& r, int tiled) {
+// The registers of fetch_sub as an LDS image [item][unit] (ld U + 4).
+template <int U, int NTH>
+SGNN_DEV void put_sub(float* img, const ChunkRegs<U, NTH>& r, int tiled) {
   constexpr int ldi = U + 4, per_tile = (U / 32) * 4 * 64, Q = U / 4;
 #pragma unroll
-  for (int k = 0; k < ChunkRegs<U>::NPT; ++k) {
-    const int idx = threadIdx.x + k * kBlock;
+  for (int k = 0; k < ChunkRegs<U, NTH>::NPT; ++k) {
+    const int idx = threadIdx.x + k * NTH;
     int item, unit;
     if (tiled) {
       const int q = idx / per_tile, rem = idx - q * per_tile;
@@ -1751,16 +1752,20 @@ SGNN_DEV void put_sub(float* img, const ChunkRegs<U>& r, int tiled) {
 }
 
 // TAG only names the launch for the profiler: 1 = the edge layer's weight gradients (bench.py reads
-// their per-launch bytes from the rocprofv3 summary), 0 = every other caller
-template <int TV, int TAG>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_wgrad_half(WgradOp op, int nslab) {
+// their per-launch bytes from the rocprofv3 summary), 0 = every other caller.  NWV waves per
+// workgroup: 8 at 128 x 128 (one output tile per wave, four waves per SIMD across the two
+// workgroups of a CU, so one wave's loads wait under three others' MFMAs), 4 at 128 x 32.
+template <int TV, int TAG, int NWV>
+__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV / 2)))
+void k_wgrad_half(WgradOp op, int nslab) {
+  constexpr int NTH = 64 * NWV;
   constexpr int AU = 64, BU = 32 * TV, lda = AU + 4, ldb = BU + 4;
-  constexpr int TU = 2, NT = (TU * TV + kWaves - 1) / kWaves;
-  constexpr int RPW = kHalfChunk / kWaves;   // items per wave in the column sums
+  constexpr int TU = 2, NT = (TU * TV + NWV - 1) / NWV;
+  constexpr int RPW = kHalfChunk / NWV;   // items per wave in the column sums
   extern __shared__ float lds[];
   float* imA = lds;
   float* imB = imA + kHalfChunk * lda;
-  const int l = lane_id(), w = wave_id();
+  const int l = lane_id(), w = (int)threadIdx.x / 64;
   const int half = blockIdx.x >= (unsigned)nslab ? 1 : 0;
   const int slab = (int)blockIdx.x - half * nslab;
   f32x16 acc[NT];
@@ -1769,23 +1774,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const int64_t nitems = op.nitems_dev ? (int64_t)*op.nitems_dev : op.nitems;
   const int64_t nch = (nitems + kHalfChunk - 1) / kHalfChunk;
   const int64_t c0 = nch * slab / nslab, c1 = nch * (slab + 1) / nslab;
-  ChunkRegs<AU> ra;
-  ChunkRegs<BU> rb;
+  ChunkRegs<AU, NTH> ra;
+  ChunkRegs<BU, NTH> rb;
   if (c0 < c1) {
-    fetch_sub<AU, 128>(ra, op.A, op.a_tiled, op.a_ld, AU * half, c0 * kHalfChunk, nitems);
-    fetch_sub<BU, BU>(rb, op.B, op.b_tiled, op.b_ld, 0, c0 * kHalfChunk, nitems);
+    fetch_sub<AU, 128, NTH>(ra, op.A, op.a_tiled, op.a_ld, AU * half, c0 * kHalfChunk, nitems);
+    fetch_sub<BU, BU, NTH>(rb, op.B, op.b_tiled, op.b_ld, 0, c0 * kHalfChunk, nitems);
   }
   for (int64_t c = c0; c < c1; ++c) {
-    put_sub<AU>(imA, ra, op.a_tiled);
-    put_sub<BU>(imB, rb, op.b_tiled);
+    put_sub<AU, NTH>(imA, ra, op.a_tiled);
+    put_sub<BU, NTH>(imB, rb, op.b_tiled);
     __syncthreads();
-    if (c + 1 < c1) {
-      fetch_sub<AU, 128>(ra, op.A, op.a_tiled, op.a_ld, AU * half, (c + 1) * kHalfChunk, nitems);
-      fetch_sub<BU, BU>(rb, op.B, op.b_tiled, op.b_ld, 0, (c + 1) * kHalfChunk, nitems);
+    if (c + 1 < c1) {   // the next chunk's loads fly under this chunk's MFMAs
+      fetch_sub<AU, 128, NTH>(ra, op.A, op.a_tiled, op.a_ld, AU * half, (c + 1) * kHalfChunk, nitems);
+      fetch_sub<BU, BU, NTH>(rb, op.B, op.b_tiled, op.b_ld, 0, (c + 1) * kHalfChunk, nitems);
     }
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
-      const int tile = w + kWaves * q;
+      const int tile = w + NWV * q;
       if (tile < TU * TV) {
         const int tu = tile / TV, tv = tile - tu * TV;
         mfma_outer<kHalfChunk>(acc[q], imA, lda, 32 * tu, imB, ldb, 32 * tv);
@@ -1798,8 +1803,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
     __syncthreads();
   }
-  store_outer<NT>(op.dst + slab * op.slab_stride + (int64_t)(AU * half) * op.dst_ld, op.dst_ld, TU, TV, acc);
-  if (op.colsum) op.colsum[slab * op.slab_stride + w * 128 + AU * half + l] = cs;
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    const int tile = w + NWV * q;
+    if (tile < TU * TV) {
+      const int tu = tile / TV, tv = tile - tu * TV;
+      store_tile_rowmajor(op.dst + slab * op.slab_stride + (int64_t)(AU * half + 32 * tu) * op.dst_ld + 32 * tv,
+                          op.dst_ld, acc[q]);
+    }
+  }
+  if (op.colsum) {
+    // kWaves partial rows per slab: waves w and w + 4 (NWV = 8) add theirs through LDS, in that order
+    if constexpr (NWV > kWaves) {
+      if (w >= kWaves) lds[(w - kWaves) * 64 + l] = cs;
+      __syncthreads();
+      if (w < kWaves) cs += lds[w * 64 + l];
+    }
+    if (w < kWaves) op.colsum[slab * op.slab_stride + w * 128 + AU * half + l] = cs;
+  }
 }
 
 // ---- edge layer, H = 128 ---------------------------------------------------
@@ -2244,11 +2265,12 @@ void launch_bwd(K kernel, int nslab, size_t lds, void* stream, const A& a) {
 
 template <int TU, int TV, int TAG = 0>
 void run_wgrad(const WgradOp& op, int nslab, void* stream) {
-  if constexpr (TU == 4 && TV == 4) {   // 128 x 128: two half-row workgroups per slab, two per CU
+  if constexpr (TU == 4) {   // 128 rows: two half-row workgroups per slab, two per CU
+    constexpr int NWV = TV == 4 ? 8 : 4;
     const size_t lds = 4 * (size_t)kHalfChunk * ((64 + 4) + (32 * TV + 4));
-    auto kern = k_wgrad_half<TV, TAG>;
+    auto kern = k_wgrad_half<TV, TAG, NWV>;
     set_lds(kern, lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(2 * nslab)), dim3(kBlock), lds,
+    hipLaunchKernelGGL(kern, dim3((unsigned)(2 * nslab)), dim3(64 * NWV), lds,
                        static_cast<hipStream_t>(stream), op, nslab);
     return;
   }
