@@ -685,7 +685,7 @@ def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps
     # (exact kernel names as rocprofv3 lists them: the profile summary's per-launch bytes and time
     # of the composite come from the same names)
     kname = "k_edge_bwd64" if (H == 64 and nmlp == 1) else \
-        (f"k_edge_items<{H // 32}, {nmlp + 1}> + {nmlp + 1} k_wgrad_half<{H // 32}, 1>" if H == 128 else
+        (f"k_edge_items<{H // 32}, {nmlp + 1}> + {nmlp + 1} k_wgrad_half<{H // 32}, 1, 8>" if H == 128 else
          f"k_edge_items<{H // 32}, {nmlp + 1}> + {nmlp + 1} k_wgrad<{H // 32}, {H // 32}>")
     res = {
         "metric": "particle-steps/sec (multi-scale training fwd+bwd+Adam)",

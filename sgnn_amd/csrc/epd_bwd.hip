@@ -1593,7 +1593,7 @@ void k_enc_edge_bwd64(EncEdgeBwdArgs a) {
 // accumulators (192-256 registers) next to the per-item state, which does not
 // fit the 512-entry register file without spilling.  At H = 128 the per-item
 // kernels (wave-independent, no workgroup barriers) therefore write the
-// pre-activation gradients (dy, d2, dh) to scratch, and k_wgrad forms every
+// pre-activation gradients (dy, d2, dh) to scratch, and k_wgrad_half forms every
 // dW = sum_items A (x) B (plus the bias sums = column sums of A) as a split-K
 // MFMA GEMM over LDS-staged 128-item chunks, into the same slab layouts.
 
@@ -1617,85 +1617,14 @@ struct WgradOp {
   const int32_t* nitems_dev;  // if set: nitems = *nitems_dev (edge count = rowptr[n])
 };
 
-// Stage items [item0, item0 + kChunk) x U units of a tiled or row-major
-// operand as an LDS image [item][unit] (ld U + 4); items >= nitems are zero.
-template <int U>
-SGNN_DEV void stage_items(float* img, const float* src, int tiled, int ld, int64_t item0,
-                          int64_t nitems) {
-  constexpr int ldi = U + 4, Q = U / 4;
-  if (tiled) {
-    constexpr int per_tile = (U / 32) * 4 * 64;  // f32x4 groups per 32-item tile
-    for (int idx = threadIdx.x; idx < 4 * per_tile; idx += blockDim.x) {
-      const int q = idx / per_tile, rem = idx - q * per_tile;
-      const int grp = rem >> 6, lane = rem & 63;
-      const int item = q * 32 + (lane & 31);
-      const int unit = 32 * (grp >> 2) + 8 * (grp & 3) + 4 * (lane >> 5);
-      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-      const int64_t t0 = item0 + q * 32;
-      if (t0 < nitems) {
-        v = ld4(src + (t0 / 32) * (32 * U) + grp * 256 + lane * 4);
-        if (item0 + item >= nitems) v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      }
-      st4(img + item * ldi + unit, v);
-    }
-  } else {
-    for (int idx = threadIdx.x; idx < kChunk * Q; idx += blockDim.x) {
-      const int item = idx / Q, quad = idx - item * Q;
-      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (item0 + item < nitems) v = ld4(src + (item0 + item) * ld + 4 * quad);
-      st4(img + item * ldi + 4 * quad, v);
-    }
-  }
-}
-
-template <int TU, int TV>
-__global__ __launch_bounds__(kBlock) void k_wgrad(WgradOp op) {
-  constexpr int AU = 32 * TU, BU = 32 * TV, lda = AU + 4, ldb = BU + 4;
-  constexpr int NT = (TU * TV + kWaves - 1) / kWaves;
-  constexpr int CPL = AU >= 64 ? AU / 64 : 1;  // column-sum units per lane
-  extern __shared__ float lds[];
-  float* imA = lds;
-  float* imB = imA + kChunk * lda;
-  const int l = lane_id(), w = wave_id();
-  f32x16 acc[NT];
-  zero_acc<NT>(acc);
-  float cs[CPL];
-#pragma unroll
-  for (int q = 0; q < CPL; ++q) cs[q] = 0.0f;
-  const int64_t nitems = op.nitems_dev ? (int64_t)*op.nitems_dev : op.nitems;
-  const int64_t nch = (nitems + kChunk - 1) / kChunk;
-  const int64_t c0 = nch * blockIdx.x / gridDim.x, c1 = nch * (blockIdx.x + 1) / gridDim.x;
-  for (int64_t c = c0; c < c1; ++c) {
-    const int64_t item0 = c * kChunk;
-    stage_items<AU>(imA, op.A, op.a_tiled, op.a_ld, item0, nitems);
-    stage_items<BU>(imB, op.B, op.b_tiled, op.b_ld, item0, nitems);
-    __syncthreads();
-    outer_tiles<NT>(acc, TU, TV, imA, lda, 0, imB, ldb, 0);
-    if (op.colsum) {
-#pragma unroll
-      for (int q = 0; q < CPL; ++q) {
-        const int u = l + 64 * q;
-        if (u < AU) cs[q] += lane_sum(imA + w * 32 * lda, lda, 32, u);
-      }
-    }
-    __syncthreads();
-  }
-  store_outer<NT>(op.dst + blockIdx.x * op.slab_stride, op.dst_ld, TU, TV, acc);
-  if (op.colsum) {
-    float* v = op.colsum + blockIdx.x * op.slab_stride + w * AU;
-#pragma unroll
-    for (int q = 0; q < CPL; ++q)
-      if (l + 64 * q < AU) v[l + 64 * q] = cs[q];
-  }
-}
-
-// k_wgrad for 128-row gradients (TU = 4), split over two workgroups per slab:
-// workgroup b < nslab forms rows [0, 64) and b + nslab rows [64, 128) of slab
-// b's gradient over the same item range, from 64-item chunks.  The two images
-// (A half 17 KB + B 34 KB) let two workgroups share a CU, so one stages its
-// next chunk while the other's MFMAs run: the one-workgroup-per-CU k_wgrad<4,
-// TV> (135 KB of images) serialised staging and MFMAs (C5: 0.27 of fp32 MFMA
-// peak per launch).  Same sums per output element, same item order.
+// Weight-gradient GEMM dW = sum_items A (x) B for 128-row gradients (TU = 4),
+// split over two workgroups per slab: workgroup b < nslab forms rows [0, 64)
+// and b + nslab rows [64, 128) of slab b's gradient over the same item range,
+// from 64-item chunks.  The two images (A half 17 KB + B 34 KB) let two
+// workgroups share a CU; the next chunk's operands are loaded into registers
+// while the current chunk's MFMAs run.  (Round 2's one-workgroup-per-slab form
+// with 128-item chunks -- 135 KB of images, staging and MFMAs serialised --
+// ran at 0.27 of fp32 MFMA peak per C5 launch.)
 constexpr int kHalfChunk = 64;
 
 // One 64-item chunk of U units (starting at unit u0 of a USRC-unit operand) in
@@ -2265,17 +2194,14 @@ void launch_bwd(K kernel, int nslab, size_t lds, void* stream, const A& a) {
 
 template <int TU, int TV, int TAG = 0>
 void run_wgrad(const WgradOp& op, int nslab, void* stream) {
-  if constexpr (TU == 4) {   // 128 rows: two half-row workgroups per slab, two per CU
-    constexpr int NWV = TV == 4 ? 8 : 4;
-    const size_t lds = 4 * (size_t)kHalfChunk * ((64 + 4) + (32 * TV + 4));
-    auto kern = k_wgrad_half<TV, TAG, NWV>;
-    set_lds(kern, lds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(2 * nslab)), dim3(64 * NWV), lds,
-                       static_cast<hipStream_t>(stream), op, nslab);
-    return;
-  }
-  const size_t lds = 4 * (size_t)kChunk * ((32 * TU + 4) + (32 * TV + 4));
-  launch_bwd(k_wgrad<TU, TV>, nslab, lds, stream, op);
+  static_assert(TU == 4, "weight-gradient GEMMs of 128-row gradients (the H = 128 backward)");
+  // two half-row workgroups per slab, two per CU
+  constexpr int NWV = TV == 4 ? 8 : 4;
+  const size_t lds = 4 * (size_t)kHalfChunk * ((64 + 4) + (32 * TV + 4));
+  auto kern = k_wgrad_half<TV, TAG, NWV>;
+  set_lds(kern, lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(2 * nslab)), dim3(64 * NWV), lds, static_cast<hipStream_t>(stream), op,
+                     nslab);
 }
 
 WgradOp wg(const float* A, int a_tiled, int a_ld, const float* B, int b_tiled, int b_ld,
