@@ -168,6 +168,7 @@ class Trainer:
         self.nslab = nslab
         self.step = 0
         self._tw: Dict[tuple, training.TrainWorkspace] = {}
+        self._buckets = None   # layer_ranges(...) of the overlapped all-reduce, computed once
 
     def workspace(self, n: int, T: int, device) -> training.TrainWorkspace:
         cap = training.capacity(n)
@@ -217,7 +218,9 @@ class Trainer:
         training.train_forward(self.epd, radius, inp, tw, timers=timers, emb_weight=emb)
         works, layer_done = [], None
         if self.dp.overlaps_buckets():
-            ranges, (lo, hi) = layer_ranges(self.epd, self.flat)
+            if self._buckets is None:
+                self._buckets = layer_ranges(self.epd, self.flat)
+            ranges, (lo, hi) = self._buckets
 
             def layer_done(k, stream):   # layer k's gradients are final once its slab reduction ran
                 works.append(self.dp.allreduce_async(self.flat.comm[ranges[k][0]:ranges[k][1]], stream))
