@@ -31,3 +31,32 @@ def test_gpus_flag_must_agree_with_world_size():
     p = _run(["--gpus", "4", "--selftest-launch"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "--gpus 4 but WORLD_SIZE=2" in p.stderr
+
+
+def test_every_roofline_kernel_resolves_in_this_rounds_profiles():
+    """The dominant kernel each bench leg names must be found in a committed
+    rocprofv3 summary of the same workload (its `traffic` and
+    `profiled_avg_us` come from there): a renamed template (e.g. a new
+    template argument) would otherwise leave the line's traffic null."""
+    import bench
+    cases = [("c1_r15", "rollout", "k_step16"), ("c1_r06", "rollout", "k_step16"),
+             ("t4800", "rollout", "k_layer16"), ("t6400", "rollout", "k_layer16"), ("t8000", "rollout", "k_layer16"),
+             ("c2", "rollout", "k_edge_layer"), ("c4", "rollout", "k_edge_layer"),
+             ("c2", "train", "k_edge_bwd64"), ("c3", "train", "k_edge_bwd64"),
+             ("c5", "train", "k_edge_items<4, 3> + 3 k_wgrad_half<4, 1, 8>")]
+    for wl, mode, kernel in cases:
+        prof = bench.profiled(wl, mode, kernel)
+        assert prof is not None, (wl, mode, kernel)
+        assert prof["bytes"] > 0 and prof["avg_us"] > 0
+        assert "r03_" in prof["source"], prof["source"]
+
+
+def test_cpu_thread_counts_skip_an_oversubscribed_affinity_leg(monkeypatch):
+    import bench
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    counts, note = bench.thread_counts()
+    assert counts == [16] and "256" in note
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(8)))
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.thread_counts() == ([8], None)
