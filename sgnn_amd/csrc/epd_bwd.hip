@@ -1786,6 +1786,10 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
   }
   float* gam = q;
   stage_vec(gam, a.gamma, H, H);
+  // H = 128: the last Linear's W^T image fits in the LDS the wave slices leave (kItemsLdsW): one of the
+  // per-tile products reads LDS instead of L2
+  float* wlt = gam + H + kWaves * 32 * ldh;
+  if (GW) stage_matrix_t(wlt, ldh, a.wl, H, H, H, H, H);
   __syncthreads();
   const int l = lane_id(), j = l & 31, w = wave_id();
   float* sl = gam + H + w * 32 * ldh;
@@ -1824,13 +1828,13 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
     if constexpr (NL == 3) {
       f32x16 d2[TH], act[TH];
       zero<TH>(d2);
-      matvec_t<TH, TH, GW>(d2, WlT, ldl, dy);
+      matvec_t<TH, TH, false>(d2, GW ? wlt : WlT, ldh, dy);
       load_tiled<TH>(act, a.hs2 + tile * (32 * H));
       relu_mask<TH>(d2, act, valid);
       store_tiled<TH>(p.d2_out + tile * (32 * H), d2);
       matvec_t<TH, TH, GW>(dh, WmT, ldl, d2);
     } else {
-      matvec_t<TH, TH, GW>(dh, WlT, ldl, dy);
+      matvec_t<TH, TH, false>(dh, GW ? wlt : WlT, ldh, dy);
     }
     {
       f32x16 act[TH];
@@ -1882,6 +1886,8 @@ __global__ __launch_bounds__(kBlock) void k_node_items(NodeItemsArgs p) {
   extern __shared__ float lds[];
   float* gam = lds;
   stage_vec(gam, a.gamma, H, H);
+  float* wlt = gam + H + kWaves * 32 * ldh;   // the last Linear's W^T image (kItemsLdsW)
+  stage_matrix_t(wlt, ldh, a.wl, H, H, H, H, H);
   __syncthreads();
   const int l = lane_id(), j = l & 31, w = wave_id();
   float* sl = gam + H + w * 32 * ldh;
@@ -1915,13 +1921,13 @@ __global__ __launch_bounds__(kBlock) void k_node_items(NodeItemsArgs p) {
     if constexpr (NL == 3) {
       f32x16 d2[TH], act[TH];
       zero<TH>(d2);
-      matvec_t<TH, TH, true>(d2, a.wl, H, dy);
+      matvec_t<TH, TH, false>(d2, wlt, ldh, dy);
       load_row_clayout<TH>(act, a.hn2 + ic * H);
       relu_mask<TH>(d2, act, valid);
       if (valid) store_row_clayout<TH>(p.d2_out + i * H, d2);
       matvec_t<TH, TH, true>(dh, a.wm, H, d2);
     } else {
-      matvec_t<TH, TH, true>(dh, a.wl, H, dy);
+      matvec_t<TH, TH, false>(dh, wlt, ldh, dy);
     }
     {
       f32x16 act[TH];
@@ -2212,6 +2218,7 @@ WgradOp wg(const float* A, int a_tiled, int a_ld, const float* B, int b_tiled, i
 }
 
 constexpr size_t kItemsLds = 4 * (128 + (size_t)kWaves * 32 * (128 + 4));  // gamma + wave slices
+constexpr size_t kItemsLdsW = kItemsLds + 4 * (size_t)128 * (128 + 4);    // + the last Linear's W^T image
 
 // LDS bytes per kind: weight images (H = 64 only) + vectors + the two
 // [128 items][H+4] operand images of the outer products.
@@ -2306,8 +2313,8 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
     const int64_t vb = slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, nl), W = kWaves, ss = a.slab_stride;
     const int32_t* Edev = rowptr + n;
     const float* hl = nl == 3 ? saves->h2 : saves->h;
-    if (nl == 3) launch_bwd(k_edge_items<4, 3>, nslab, kItemsLds, stream, p);
-    else launch_bwd(k_edge_items<4, 2>, nslab, kItemsLds, stream, p);
+    if (nl == 3) launch_bwd(k_edge_items<4, 3>, nslab, kItemsLdsW, stream, p);
+    else launch_bwd(k_edge_items<4, 2>, nslab, kItemsLdsW, stream, p);
     run_wgrad<4, 4, 1>(wg(p.dy_out, 1, 0, hl, 1, 0, slab, 0, H, vb, ss, 0, Edev), nslab, stream);
     run_wgrad<4, 4, 1>(wg(dh_rows, 0, H, e0t, 1, 0, slab, H * H, H, -1, ss, 0, Edev), nslab, stream);
     if (nl == 3)
@@ -2345,8 +2352,8 @@ extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* 
     if (!scratch) return set_error(SGNN_ERR_INVALID, "node_layer_bwd: H=128 needs scratch");
     const int nl = node_fn->nlin;
     NodeItemsArgs p{a, scratch, scratch + n * H, scratch + 2 * n * H};
-    if (nl == 3) launch_bwd(k_node_items<3>, nslab, kItemsLds, stream, p);
-    else launch_bwd(k_node_items<2>, nslab, kItemsLds, stream, p);
+    if (nl == 3) launch_bwd(k_node_items<3>, nslab, kItemsLdsW, stream, p);
+    else launch_bwd(k_node_items<2>, nslab, kItemsLdsW, stream, p);
     const int64_t vb = slab_nmat_floats(SGNN_SLAB_NODE, H, 0, nl), W = kWaves, ss = a.slab_stride;
     const float* hl = nl == 3 ? saves->h2 : saves->h;
     run_wgrad<4, 4>(wg(p.dy_out, 0, H, hl, 0, H, slab, 0, H, vb + W * H, ss, n, nullptr), nslab, stream);
