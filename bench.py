@@ -252,28 +252,59 @@ def profiled(workload, mode, kernel):
     return best
 
 
-def roofline(kernel, flops, avg_s, workload, mode, alg_bytes=None, executed_flops=None):
-    """`achieved` / `frac`: ALGORITHMIC FLOPs per launch (SURVEY.md §8(d)'s
-    count, as BASELINE.md §3 asks) / the live average launch time, against the
-    dense fp32 MFMA peak; `executed_frac` the same for the FLOPs the kernel
-    actually multiplies (the u/v factorisation removes 2H^2 of every edge's
-    first Linear); `traffic` per launch from this round's rocprofv3 passes."""
+def roofline(kernel, flops, avg_s, workload, mode, alg_bytes=None, executed_flops=None, whole=True):
+    """The dominant kernel against the dense fp32 MFMA peak.  `whole`: the launch
+    does whole layers / the whole step (k_step16, k_layer16), so `frac` is
+    SURVEY.md §8(d)'s ALGORITHMIC FLOPs per launch / the live average launch
+    time, with `exe_frac` the FLOPs it actually multiplies (the
+    u/v factorisation removes 2H^2 of every edge's first Linear).  A split kernel
+    (k_edge_layer: the node kernel forms the u/v half of the first edge Linear;
+    the backward kernels) is charged only what it executes: `frac` = executed
+    FLOPs / time (§8(d) per edge inflated the edge kernel past the
+    peak); the whole-step §8(d) figure sits beside it in the leg (`alg_step_frac`).
+    `traffic` = HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE) and
+    `prof_us` the trace-mode duration, both from this round's profiles/ summary."""
     prof = profiled(workload, mode, kernel)
-    r = {"bound": "mfma", "kernel": kernel, "achieved": flops / avg_s / 1e12, "peak": MFMA_F32_PEAK / 1e12,
-         "unit": "TFLOP/s", "frac": flops / avg_s / MFMA_F32_PEAK,
-         "traffic": prof["bytes"] if prof else None,
-         "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-         "traffic_source": prof["source"] if prof else None,
-         "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops, "flops_count": "SURVEY.md §8(d) algorithmic"}
-    if executed_flops is not None:
-        r["executed_flops_per_launch"] = executed_flops
-        r["executed_frac"] = executed_flops / avg_s / MFMA_F32_PEAK
+    exe = flops if executed_flops is None else executed_flops
+    charged = flops if whole else exe
+    frac = charged / avg_s / MFMA_F32_PEAK
+    if frac > 1.0:
+        raise RuntimeError(f"roofline of {kernel}: {frac:.3f} of peak -- the FLOP count or the timing is wrong")
+    r = {"bound": "mfma", "kernel": kernel, "achieved": charged / avg_s / 1e12, "peak": MFMA_F32_PEAK / 1e12,
+         "unit": "TFLOP/s", "frac": frac, "flops": "8d" if whole else "executed",
+         "exe_frac": exe / avg_s / MFMA_F32_PEAK, "flops_per_launch": charged,
+         "traffic": prof["bytes"] if prof else None, "live_us": avg_s * 1e6}
     if prof:
-        r["hbm_frac"] = prof["bytes"] / avg_s / HBM_PEAK          # achieved HBM fraction (live duration)
-        r["profiled_avg_us"] = prof["avg_us"]
+        r["prof_us"] = prof["avg_us"]
+        r["src"] = os.path.basename(prof["source"])
     if alg_bytes is not None:
-        r["algorithmic_bytes"] = alg_bytes
+        r["alg_bytes"] = alg_bytes
     return r
+
+
+def _r(x):
+    """4 significant digits (the JSON line stays a few KB)."""
+    if isinstance(x, float):
+        return float(f"{x:.4g}")
+    if isinstance(x, dict):
+        return {k: _r(v) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_r(v) for v in x]
+    return x
+
+
+def leg(r):
+    """An extra leg of the line, numbers only (the contract keys live at the top level)."""
+    out = {k: r[k] for k in ("value", "ms_per_step", "M_edge_messages_per_s", "particles", "edges",
+                             "hbm_peak_gib", "final_loss", "alg_step_frac", "scaling") if k in r}
+    if "roofline" in r:
+        rf = r["roofline"]
+        out["rf"] = {k: rf[k] for k in ("kernel", "frac", "flops", "exe_frac", "traffic", "alg_bytes", "live_us",
+                                        "prof_us", "src") if k in rf}
+    if "cpu_baseline" in r:
+        out["cpu"] = {k: r["cpu_baseline"][k] for k in ("value", "cores", "sample")}
+        out["x_cpu"] = r["speedup_vs_cpu"]
+    return out
 
 
 # ----------------------------------------------------------------------------- models / data
@@ -315,8 +346,7 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload, min_seconds=0.
     sample = ""
     if workload in CPU_SAMPLE_DIMS:
         window = torch.from_numpy(synthetic.trajectory(lattice(CPU_SAMPLE_DIMS[workload]), T_SEQ, seed=7))
-        sample = (f" (a {'x'.join(map(str, CPU_SAMPLE_DIMS[workload]))} sample of the same lattice, "
-                  f"spacing, radius and model: per-particle rate, not the full config size)")
+        sample = f" ({'x'.join(map(str, CPU_SAMPLE_DIMS[workload]))} sample: per-particle rate)"
     osim = O.OracleSimulator(state, window.shape[2], L, radius, sim._normalization_stats)
     n = window.shape[0]
     types_ = torch.zeros(n, dtype=torch.long)
@@ -341,11 +371,13 @@ def cpu_rollout_baseline(sim, window, radius, L, steps, workload, min_seconds=0.
                      "M_edge_messages_per_s": edges * L * done / dt / 1e6})
     cpu_threads()
     best = max(legs, key=lambda r: r["value"])
-    extra = {"legs_note": skipped} if skipped else {}
-    return {**best, **extra, "legs": [{k: r[k] for k in ("cores", "value", "steps", "seconds")} for r in legs],
-            "sample": f"{best['steps']} autoregressive oracle rollout steps after 1 warm-up (torch CPU fp32 "
-                      f"restatement of the reference ops + C cell-list radius search), {n} particles{sample}; "
-                      f"fastest of the thread counts tried (legs)"}
+    out = {k: best[k] for k in ("value", "unit", "cores", "kind")}
+    out["sample"] = f"{best['steps']} oracle rollout steps, {n} particles{sample}, {best['cores']} threads"
+    out["host"] = {"cpu_model": best["cpu_model"], "os_cpu_count": best["os_cpu_count"],
+                   "affinity_cpus": best["affinity_cpus"], "legs": {str(r["cores"]): r["value"] for r in legs}}
+    if skipped:
+        out["host"]["note"] = skipped
+    return out
 
 
 def step_flops(n, E, H, L, dim, feat):
@@ -395,13 +427,12 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps,
             torch.cuda._sleep(2_000_000)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-            runner.run(w0)
+            runner.run(w0, check_step=False)
             ev1.record()
+            runner.ws.check_step(device)   # raises SgnnError if a tile timed out (after ev1: not timed)
             torch.cuda.synchronize()
             kernel_s = ev0.elapsed_time(ev1) * 1e-3 / steps
             edges = [runner.ws.step_edges()]
-            if runner.ws.step_timeout():
-                raise RuntimeError("k_step16: a workgroup timed out waiting for its sender tiles")
         else:
             # event-timed pass (same kernels, launched from Python per step)
             inp, use_emb = sim._step_inputs(w0, [n], types_)
@@ -451,9 +482,12 @@ def bench_rollout(workload, steps, warmup, world, rank, device, seed, cpu_steps,
            "value": n * steps * world / dt, "unit": "particle-steps/s",
            "ms_per_step": dt / steps * 1e3,
            "M_edge_messages_per_s": E_all * L * steps / dt / 1e6,
-           "path": (f"one launch per step (k_step16, {grid} workgroups of {nt} receivers)" if one_launch
-                    else "kernel sequence"),
-           "roofline": roofline(kernel, flops, kernel_s, workload, "rollout", alg_bytes, exe)}
+           "path": (f"k_step16 x{grid}x{nt}" if one_launch else "kernel sequence"),
+           # the whole step by §8(d)'s count over the step time (algorithmic; beside a split kernel's
+           # executed `frac`)
+           "alg_step_frac": alg_step / (dt / steps) / MFMA_F32_PEAK,
+           "roofline": roofline(kernel, flops, kernel_s, workload, "rollout", alg_bytes, exe,
+                                whole=kernel != "k_edge_layer")}
     out["roofline"]["share_of_step"] = kernel_s * (1 if one_launch else L) / (dt / steps)
     if cpu_steps > 0 and rank == 0 and world == 1:
         progress(f"rollout {workload}: cpu baseline")
@@ -492,10 +526,9 @@ def cpu_train_baseline(state, graphs, radius, L, steps, stats):
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "particle-steps/s", **info, "seconds": dt,
-            "sample": f"{steps} oracle training steps after 1 warm-up (noise + forward + torch autograd "
-                      f"backward + Adam, torch CPU fp32 restatement of the reference ops), {n} particles "
-                      f"in {len(counts)} graph(s) (training steps are ~2.5 s each at 50k: bounded to ~25 s)"}
+    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": info["cores"], "kind": "port",
+            "sample": f"{steps} oracle training steps (noise+fwd+autograd+Adam), {n} particles, "
+                      f"{info['cores']} threads"}
 
 
 def _train_graph(dims, seed):
@@ -572,8 +605,11 @@ def bench_train(mode, steps, warmup, world, rank, device, seed, cpu_steps):
                    "parallelism": f"dp{world} (whole-graph, RCCL all-reduce)" if world > 1 else "single GPU"},
         "M_edge_messages_per_s": E_all * L * steps / dt / 1e6,
         "final_loss": float(out["loss"]),
+        # fwd + bwd ~ 3x the forward by §8(d)'s count, over the step time (algorithmic)
+        "alg_step_frac": 3 * step_flops(n_global, E_all, H, L, 2, (T_SEQ - 1) * 2 + 1)[0] / (dt / steps)
+        / MFMA_F32_PEAK / world,
         "roofline": roofline(kname, flops_bwd, kstats[dom], "c2" if mode == "train" else "c3", "train",
-                             executed_flops=flops_bwd),
+                             whole=False),
         "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
     }
     res["roofline"]["share_of_step"] = float(np.sum([a.elapsed_time(b) for a, b in timers[dom]])) / (dt_ev * 1e3)
@@ -644,11 +680,9 @@ def cpu_ms_train_baseline(sim, cfg, steps):
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "particle-steps/s", **info, "seconds": dt,
-            "sample": f"{steps} oracle multi-scale training steps after 1 warm-up (forward + torch autograd + "
-                      f"Adam, torch CPU fp32 restatement of sgnn/multi_scale) on a "
-                      f"{'x'.join(map(str, sdims))} lattice = {n} particles, same model (per-particle rate "
-                      f"of a bounded sample, not the 1M config)"}
+    return {"value": n * steps / dt, "unit": "particle-steps/s", "cores": info["cores"], "kind": "port",
+            "sample": f"{steps} oracle multi-scale training steps, {'x'.join(map(str, sdims))} sample = {n} "
+                      f"particles (per-particle rate), {info['cores']} threads"}
 
 
 def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps):
@@ -698,8 +732,7 @@ def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps
         "M_edge_messages_per_s": eb * steps * world / dt / 1e6,
         "final_loss": float(out["loss"]),
         "hbm_peak_gib": torch.cuda.max_memory_allocated(device) / 2 ** 30,
-        "roofline": roofline(kname, flops_bwd, kstats.get(dom, float("nan")), workload, "train",
-                             executed_flops=flops_bwd),
+        "roofline": roofline(kname, flops_bwd, kstats.get(dom, float("nan")), workload, "train", whole=False),
         "kernel_avg_us": {k: v * 1e6 for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and cpu_steps > 0:
@@ -740,10 +773,11 @@ def headline(r, args, world, metric, parallel):
            "warmup": args.warmup, "ms_per_step": r["ms_per_step"], "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": DATA,
            "config": {"workload": r["workload"] + ", autoregressive rollout (radius graph + features + EPD + "
-                                                  "Euler + window shift per step)",
+                                                  "Euler + window shift per step), one sgnn_rollout call",
                       "particles_per_gpu": r["particles"], "edges_per_gpu": r["edges"],
                       "parallelism": parallel},
-           "M_edge_messages_per_s": r["M_edge_messages_per_s"], "roofline": r["roofline"]}
+           "M_edge_messages_per_s": r["M_edge_messages_per_s"], "alg_step_frac": r["alg_step_frac"],
+           "roofline": r["roofline"]}
     if "cpu_baseline" in r:
         res["cpu_baseline"] = r["cpu_baseline"]
         res["speedup_vs_cpu"] = r["speedup_vs_cpu"]
@@ -776,14 +810,15 @@ def main(argv=None):
                           args.cpu_seconds)
         res = headline(r, args, world, "particle-steps/sec (2D Taylor-impact rollout)", parallel)
         if not args.no_extras:
-            res["training"] = bench_train("train", 10, 3, world, rank, device, args.seed, cs)
-            res["training_c3"] = bench_train("train-c3", 10, 3, world, rank, device, args.seed, 0)
+            # extras: numbers only (leg()), so the whole line stays a few KB
+            res["training"] = leg(bench_train("train", 10, 3, world, rank, device, args.seed, cs))
+            res["training_c3"] = leg(bench_train("train-c3", 10, 3, world, rank, device, args.seed, 0))
             res["rollout_extra"] = {}
             for wl, st in (("c2", 20), ("c1_r06", 20), ("t4800", 20), ("t6400", 20), ("t8000", 20), ("c4", 10)):
-                res["rollout_extra"][wl] = bench_rollout(wl, st, 3, world, rank, device, args.seed, cs)
-            res["multi_scale_c5_train"] = bench_ms_train("c5", 3, 1, world, rank, device, args.seed, cs)
+                res["rollout_extra"][wl] = leg(bench_rollout(wl, st, 3, world, rank, device, args.seed, cs))
+            res["multi_scale_c5_train"] = leg(bench_ms_train("c5", 3, 1, world, rank, device, args.seed, cs))
     if rank == 0:
-        print(json.dumps(res))
+        print(json.dumps(_r(res), separators=(",", ":")))
     if world > 1:
         torch.distributed.destroy_process_group()
     return 0

@@ -26,7 +26,9 @@ typedef enum sgnn_status {
   SGNN_OK = 0,
   SGNN_ERR_INVALID = 1,     /* bad pointer / size / dimension */
   SGNN_ERR_UNSUPPORTED = 2, /* shape this build has no kernel for (e.g. hidden != 64/128) */
-  SGNN_ERR_HIP = 3          /* a HIP launch failed; see sgnn_last_error() */
+  SGNN_ERR_HIP = 3,         /* a HIP launch failed; see sgnn_last_error() */
+  SGNN_ERR_STEP_TIMEOUT = 4 /* sgnn_step_check: a workgroup of the one-launch step gave up waiting for
+                               its sender tiles; that call's outputs are invalid */
 } sgnn_status;
 
 /* One build_mlp(...) (+ optional LayerNorm) parameter set,
@@ -284,6 +286,8 @@ typedef struct sgnn_step_ws { /* device buffers of one (n, T, dim, H, K) shape *
                            the kernel's LDS */
   uint32_t* step_flags; /* [512] per-workgroup phase counters + error word (zeroed per call) */
   int32_t* step_deg;    /* [n] neighbours kept per receiver */
+  int32_t step_poll_limit; /* 0: default (~1 s of polling per wait before the error word is set);
+                              < 0: test hook, every tile records a timeout at its first wait */
 } sgnn_step_ws;
 
 int sgnn_predict_positions(const sgnn_epd* model, const sgnn_step_in* in, const float* pos_seq,
@@ -293,6 +297,17 @@ int sgnn_predict_positions(const sgnn_epd* model, const sgnn_step_in* in, const 
  * they run the per-kernel sequence; (*nt, *grid) = receivers per workgroup and workgroups. */
 int sgnn_step_path(const sgnn_epd* model, const sgnn_step_in* in, const sgnn_step_ws* ws, int32_t* nt,
                    int32_t* grid);
+/* Co-residency.  The one-launch step hands data between its workgroups through per-tile counters, so
+ * every workgroup of a launch must be resident at once (grid <= CUs x the kernel's occupancy, checked
+ * per call).  Within this process a call takes the one-launch path only when no one-launch step of an
+ * earlier call on ANOTHER stream of the device may still be running (else it runs the per-kernel
+ * sequence: same results).  Across processes nothing can be checked: two one-launch steps sharing the
+ * device's CUs can each hold CUs the other's waiting tiles need; their bounded waits then expire and
+ * the error word is set.  sgnn_step_check reads that word once the call's work is done (it
+ * synchronises `stream`, the one entry point that does) and returns SGNN_ERR_STEP_TIMEOUT when set --
+ * the caller must treat that call's outputs as invalid.  The Python wrappers call it after every
+ * predict_positions / rollout (learned_simulator.py:413-438, evaluate.py:117-145 sync on .cpu() too). */
+int sgnn_step_check(const sgnn_step_ws* ws, void* stream);
 /* Steps alternate win_a -> win_b -> win_a ...; step k writes out_pred[k][n][dim+1]
  * (normalised acceleration + strain) and out_pos[k][n][dim]. */
 int sgnn_rollout(const sgnn_epd* model, const sgnn_step_in* in, float* win_a, float* win_b,

@@ -14,7 +14,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_lib", "libsgnn_hip.so")
 
-SGNN_OK, SGNN_ERR_INVALID, SGNN_ERR_UNSUPPORTED, SGNN_ERR_HIP = 0, 1, 2, 3
+SGNN_OK, SGNN_ERR_INVALID, SGNN_ERR_UNSUPPORTED, SGNN_ERR_HIP, SGNN_ERR_STEP_TIMEOUT = 0, 1, 2, 3, 4
 
 c_void_p, c_int64, c_int32, c_float = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
 
@@ -56,7 +56,7 @@ class SgnnStepWs(ctypes.Structure):
                 ("edge_cap", c_int64), ("e0t", c_void_p), ("x_a", c_void_p), ("x_b", c_void_p),
                 ("u", c_void_p), ("v", c_void_p), ("agg", c_void_p), ("cin", c_void_p), ("cout", c_void_p),
                 ("u2", c_void_p), ("v2", c_void_p), ("uvl", c_void_p), ("step_flags", c_void_p),
-                ("step_deg", c_void_p)]
+                ("step_deg", c_void_p), ("step_poll_limit", c_int32)]
 
 
 class SgnnReduceDesc(ctypes.Structure):
@@ -164,6 +164,7 @@ SIGNATURES = {
     "sgnn_edge_features": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_int64,
                                           c_int64, c_void_p, c_void_p]),
     "sgnn_step_path": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sgnn_step_check": (ctypes.c_int, [c_void_p, c_void_p]),
     "sgnn_rollout": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                     c_void_p, c_void_p]),
     "sgnn_random_walk_noise": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_float, ctypes.c_uint64,

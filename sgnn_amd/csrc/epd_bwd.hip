@@ -1615,6 +1615,9 @@ struct WgradOp {
   float* colsum;         // workgroup-0 slab + [W][32*TU] vector offset, or null
   int64_t slab_stride, nitems;
   const int32_t* nitems_dev;  // if set: nitems = *nitems_dev (edge count = rowptr[n])
+  // extents in floats (from A, B, dst, colsum): what the bounds-checked build (SGNN_DEBUG_BOUNDS) tests
+  // every operand load and slab store against
+  int64_t a_len, b_len, dst_len, colsum_len;
 };
 
 // Weight-gradient GEMM dW = sum_items A (x) B for 128-row gradients (TU = 4),
@@ -1638,7 +1641,8 @@ struct ChunkRegs {
 
 template <int U, int USRC, int NTH>
 SGNN_DEV void fetch_sub(ChunkRegs<U, NTH>& r, const float* src, int tiled, int ld, int u0, int64_t item0,
-                        int64_t nitems) {
+                        int64_t nitems, int64_t len) {
+  (void)len;
   constexpr int per_tile = (U / 32) * 4 * 64;   // float4 groups per 32-item tile (tiled layout)
   constexpr int Q = U / 4;
   const int g0 = (u0 / 32) * 4;
@@ -1650,10 +1654,18 @@ SGNN_DEV void fetch_sub(ChunkRegs<U, NTH>& r, const float* src, int tiled, int l
       const int q = idx / per_tile, rem = idx - q * per_tile;
       const int grp = rem >> 6, lane = rem & 63;
       const int64_t t0 = item0 + q * 32;
-      if (t0 + (lane & 31) < nitems) v = ld4(src + (t0 / 32) * (32 * USRC) + (g0 + grp) * 256 + lane * 4);
+      if (t0 + (lane & 31) < nitems) {
+        int64_t off = (t0 / 32) * (32 * USRC) + (g0 + grp) * 256 + lane * 4;
+        SGNN_BOUNDS(off, 0, len - 3, "wgrad tiled operand");
+        v = ld4(src + off);
+      }
     } else {
       const int item = idx / Q, quad = idx - item * Q;
-      if (item0 + item < nitems) v = ld4(src + (item0 + item) * ld + u0 + 4 * quad);
+      if (item0 + item < nitems) {
+        int64_t off = (item0 + item) * ld + u0 + 4 * quad;
+        SGNN_BOUNDS(off, 0, len - 3, "wgrad row operand");
+        v = ld4(src + off);
+      }
     }
     r.v[k] = v;
   }
@@ -1676,7 +1688,9 @@ SGNN_DEV void put_sub(float* img, const ChunkRegs<U, NTH>& r, int tiled) {
       item = idx / Q;
       unit = 4 * (idx - item * Q);
     }
-    st4(img + item * ldi + unit, r.v[k]);
+    int o = item * ldi + unit;
+    SGNN_BOUNDS(o, 0, kHalfChunk * ldi - 3, "wgrad LDS image");
+    st4(img + o, r.v[k]);
   }
 }
 
@@ -1706,16 +1720,16 @@ void k_wgrad_half(WgradOp op, int nslab) {
   ChunkRegs<AU, NTH> ra;
   ChunkRegs<BU, NTH> rb;
   if (c0 < c1) {
-    fetch_sub<AU, 128, NTH>(ra, op.A, op.a_tiled, op.a_ld, AU * half, c0 * kHalfChunk, nitems);
-    fetch_sub<BU, BU, NTH>(rb, op.B, op.b_tiled, op.b_ld, 0, c0 * kHalfChunk, nitems);
+    fetch_sub<AU, 128, NTH>(ra, op.A, op.a_tiled, op.a_ld, AU * half, c0 * kHalfChunk, nitems, op.a_len);
+    fetch_sub<BU, BU, NTH>(rb, op.B, op.b_tiled, op.b_ld, 0, c0 * kHalfChunk, nitems, op.b_len);
   }
   for (int64_t c = c0; c < c1; ++c) {
     put_sub<AU, NTH>(imA, ra, op.a_tiled);
     put_sub<BU, NTH>(imB, rb, op.b_tiled);
     __syncthreads();
     if (c + 1 < c1) {   // the next chunk's loads fly under this chunk's MFMAs
-      fetch_sub<AU, 128, NTH>(ra, op.A, op.a_tiled, op.a_ld, AU * half, (c + 1) * kHalfChunk, nitems);
-      fetch_sub<BU, BU, NTH>(rb, op.B, op.b_tiled, op.b_ld, 0, (c + 1) * kHalfChunk, nitems);
+      fetch_sub<AU, 128, NTH>(ra, op.A, op.a_tiled, op.a_ld, AU * half, (c + 1) * kHalfChunk, nitems, op.a_len);
+      fetch_sub<BU, BU, NTH>(rb, op.B, op.b_tiled, op.b_ld, 0, (c + 1) * kHalfChunk, nitems, op.b_len);
     }
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
@@ -1737,8 +1751,12 @@ void k_wgrad_half(WgradOp op, int nslab) {
     const int tile = w + NWV * q;
     if (tile < TU * TV) {
       const int tu = tile / TV, tv = tile - tu * TV;
-      store_tile_rowmajor(op.dst + slab * op.slab_stride + (int64_t)(AU * half + 32 * tu) * op.dst_ld + 32 * tv,
-                          op.dst_ld, acc[q]);
+      const int64_t o = slab * op.slab_stride + (int64_t)(AU * half + 32 * tu) * op.dst_ld + 32 * tv;
+#ifdef SGNN_DEBUG_BOUNDS
+      int64_t hi = o + 31 * (int64_t)op.dst_ld + 31;   // the tile's last element
+      SGNN_BOUNDS(hi, 0, op.dst_len, "wgrad slab tile");
+#endif
+      store_tile_rowmajor(op.dst + o, op.dst_ld, acc[q]);
     }
   }
   if (op.colsum) {
@@ -1748,7 +1766,11 @@ void k_wgrad_half(WgradOp op, int nslab) {
       __syncthreads();
       if (w < kWaves) cs += lds[w * 64 + l];
     }
-    if (w < kWaves) op.colsum[slab * op.slab_stride + w * 128 + AU * half + l] = cs;
+    if (w < kWaves) {
+      int64_t o = slab * op.slab_stride + w * 128 + AU * half + l;
+      SGNN_BOUNDS(o, 0, op.colsum_len, "wgrad column sums");
+      op.colsum[o] = cs;
+    }
   }
 }
 
@@ -2210,11 +2232,14 @@ void run_wgrad(const WgradOp& op, int nslab, void* stream) {
                      nslab);
 }
 
-WgradOp wg(const float* A, int a_tiled, int a_ld, const float* B, int b_tiled, int b_ld,
-           float* slab, int64_t mat_off, int dst_ld, int64_t vec_off, int64_t slab_stride,
-           int64_t nitems, const int32_t* nitems_dev) {
+// a_len / b_len: the operands' extents in floats; the slab region holds nslab x slab_stride floats.
+WgradOp wg(const float* A, int a_tiled, int a_ld, int64_t a_len, const float* B, int b_tiled, int b_ld,
+           int64_t b_len, float* slab, int64_t mat_off, int dst_ld, int64_t vec_off, int64_t slab_stride,
+           int nslab, int64_t nitems, const int32_t* nitems_dev) {
+  const int64_t slab_len = (int64_t)nslab * slab_stride;
   return WgradOp{A, B, a_tiled, b_tiled, a_ld, b_ld, slab + mat_off, dst_ld,
-                 vec_off >= 0 ? slab + vec_off : nullptr, slab_stride, nitems, nitems_dev};
+                 vec_off >= 0 ? slab + vec_off : nullptr, slab_stride, nitems, nitems_dev,
+                 a_len, b_len, slab_len - mat_off, vec_off >= 0 ? slab_len - vec_off : 0};
 }
 
 constexpr size_t kItemsLds = 4 * (128 + (size_t)kWaves * 32 * (128 + 4));  // gamma + wave slices
@@ -2310,15 +2335,17 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
     const int nl = edge_fn->nlin;
     const int64_t pad = 32 * ((edge_cap + 31) / 32);
     EdgeItemsArgs p{a, scratch, scratch + pad * H};
+    const int64_t tl = pad * H;   // floats of one tiled [edge_cap][H] array
     const int64_t vb = slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, nl), W = kWaves, ss = a.slab_stride;
     const int32_t* Edev = rowptr + n;
     const float* hl = nl == 3 ? saves->h2 : saves->h;
     if (nl == 3) launch_bwd(k_edge_items<4, 3>, nslab, kItemsLdsW, stream, p);
     else launch_bwd(k_edge_items<4, 2>, nslab, kItemsLdsW, stream, p);
-    run_wgrad<4, 4, 1>(wg(p.dy_out, 1, 0, hl, 1, 0, slab, 0, H, vb, ss, 0, Edev), nslab, stream);
-    run_wgrad<4, 4, 1>(wg(dh_rows, 0, H, e0t, 1, 0, slab, H * H, H, -1, ss, 0, Edev), nslab, stream);
+    run_wgrad<4, 4, 1>(wg(p.dy_out, 1, 0, tl, hl, 1, 0, tl, slab, 0, H, vb, ss, nslab, 0, Edev), nslab, stream);
+    run_wgrad<4, 4, 1>(wg(dh_rows, 0, H, edge_cap * H, e0t, 1, 0, tl, slab, H * H, H, -1, ss, nslab, 0, Edev), nslab,
+                       stream);
     if (nl == 3)
-      run_wgrad<4, 4, 1>(wg(p.d2_out, 1, 0, saves->h, 1, 0, slab, 2 * H * H, H, vb + 3 * W * H, ss, 0, Edev),
+      run_wgrad<4, 4, 1>(wg(p.d2_out, 1, 0, tl, saves->h, 1, 0, tl, slab, 2 * H * H, H, vb + 3 * W * H, ss, nslab, 0, Edev),
                       nslab, stream);
     return check_launch("edge_layer_bwd");
   }
@@ -2352,17 +2379,18 @@ extern "C" int sgnn_node_layer_bwd(const float* g, int64_t n, const sgnn_saves* 
     if (!scratch) return set_error(SGNN_ERR_INVALID, "node_layer_bwd: H=128 needs scratch");
     const int nl = node_fn->nlin;
     NodeItemsArgs p{a, scratch, scratch + n * H, scratch + 2 * n * H};
+    const int64_t nH = n * H;
     if (nl == 3) launch_bwd(k_node_items<3>, nslab, kItemsLdsW, stream, p);
     else launch_bwd(k_node_items<2>, nslab, kItemsLdsW, stream, p);
     const int64_t vb = slab_nmat_floats(SGNN_SLAB_NODE, H, 0, nl), W = kWaves, ss = a.slab_stride;
     const float* hl = nl == 3 ? saves->h2 : saves->h;
-    run_wgrad<4, 4>(wg(p.dy_out, 0, H, hl, 0, H, slab, 0, H, vb + W * H, ss, n, nullptr), nslab, stream);
-    run_wgrad<4, 4>(wg(p.dh_out, 0, H, saves->agg, 0, H, slab, H * H, 2 * H, vb, ss, n, nullptr), nslab,
+    run_wgrad<4, 4>(wg(p.dy_out, 0, H, nH, hl, 0, H, nH, slab, 0, H, vb + W * H, ss, nslab, n, nullptr), nslab, stream);
+    run_wgrad<4, 4>(wg(p.dh_out, 0, H, nH, saves->agg, 0, H, nH, slab, H * H, 2 * H, vb, ss, nslab, n, nullptr), nslab,
                     stream);
-    run_wgrad<4, 4>(wg(p.dh_out, 0, H, x_in, 0, H, slab, H * H + H, 2 * H, -1, ss, n, nullptr), nslab,
+    run_wgrad<4, 4>(wg(p.dh_out, 0, H, nH, x_in, 0, H, nH, slab, H * H + H, 2 * H, -1, ss, nslab, n, nullptr), nslab,
                     stream);
     if (nl == 3)
-      run_wgrad<4, 4>(wg(p.d2_out, 0, H, saves->h, 0, H, slab, 3 * H * H, H, vb + 4 * W * H, ss, n, nullptr),
+      run_wgrad<4, 4>(wg(p.d2_out, 0, H, nH, saves->h, 0, H, nH, slab, 3 * H * H, H, vb + 4 * W * H, ss, nslab, n, nullptr),
                       nslab, stream);
     return check_launch("node_layer_bwd");
   }
@@ -2392,10 +2420,12 @@ extern "C" int sgnn_uv_bwd(const float* dxp, const float* du, const float* cin, 
   if (H == 128) {
     if (!scratch) return set_error(SGNN_ERR_INVALID, "uv_bwd: H=128 needs scratch");
     UvItemsArgs p{a, scratch, scratch + n * H};
+    const int64_t nH = n * H;
     launch_bwd(k_uv_items, nslab, 0, stream, p);
     const int64_t ss = a.slab_stride;
-    run_wgrad<4, 4>(wg(p.du_out, 0, H, x_in, 0, H, slab, 0, 2 * H, 2 * H * H, ss, n, nullptr), nslab, stream);
-    run_wgrad<4, 4>(wg(p.dv_out, 0, H, x_in, 0, H, slab, H, 2 * H, -1, ss, n, nullptr), nslab, stream);
+    run_wgrad<4, 4>(wg(p.du_out, 0, H, nH, x_in, 0, H, nH, slab, 0, 2 * H, 2 * H * H, ss, nslab, n, nullptr), nslab,
+                    stream);
+    run_wgrad<4, 4>(wg(p.dv_out, 0, H, nH, x_in, 0, H, nH, slab, H, 2 * H, -1, ss, nslab, n, nullptr), nslab, stream);
     return check_launch("uv_bwd");
   }
   launch_bwd(k_uv_bwd64, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
@@ -2563,16 +2593,19 @@ extern "C" int sgnn_encode_edges_bwd(const float* de0t, const float* pos, int64_
     const int64_t pad = 32 * ((edge_cap + 31) / 32);
     EncEdgeItemsArgs p{a, scratch, scratch + pad * H, scratch + 2 * pad * H, scratch + 3 * pad * H,
                        scratch + 4 * pad * H};
+    const int64_t tl = pad * H;
     const size_t lds = kItemsLds + 4 * (size_t)(128 * 5 + 128);
     if (nl == 3) launch_bwd(k_enc_edge_items<3>, nslab, lds, stream, p);
     else launch_bwd(k_enc_edge_items<2>, nslab, lds, stream, p);
     const int64_t vb = slab_nmat_floats(SGNN_SLAB_ENC_EDGE, H, 0, nl), W = kWaves, ss = a.slab_stride;
     const int32_t* Edev = rowptr + n;
     const float* hl = nl == 3 ? saves->h2 : p.h1_out;
-    run_wgrad<4, 4>(wg(p.dy_out, 1, 0, hl, 1, 0, slab, 0, H, vb + W * H, ss, 0, Edev), nslab, stream);
-    run_wgrad<4, 1>(wg(p.dh_out, 1, 0, p.f_out, 0, 32, slab, H * H, 32, vb, ss, 0, Edev), nslab, stream);
+    run_wgrad<4, 4>(wg(p.dy_out, 1, 0, tl, hl, 1, 0, tl, slab, 0, H, vb + W * H, ss, nslab, 0, Edev), nslab, stream);
+    run_wgrad<4, 1>(wg(p.dh_out, 1, 0, tl, p.f_out, 0, 32, pad * 32, slab, H * H, 32, vb, ss, nslab, 0, Edev), nslab,
+                    stream);
     if (nl == 3)
-      run_wgrad<4, 4>(wg(p.d2_out, 1, 0, p.h1_out, 1, 0, slab, H * H + H * 32, H, vb + 4 * W * H, ss, 0, Edev),
+      run_wgrad<4, 4>(wg(p.d2_out, 1, 0, tl, p.h1_out, 1, 0, tl, slab, H * H + H * 32, H, vb + 4 * W * H, ss, nslab, 0,
+                         Edev),
                       nslab, stream);
     return check_launch("encode_edges_bwd");
   }

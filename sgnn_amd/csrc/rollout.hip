@@ -7,6 +7,10 @@
 #include "radius_small.h"
 #include "step16.h"
 
+#include <stdio.h>
+
+#include <mutex>
+
 namespace {
 
 // An MLP of nmlp_layers 1 with these widths (and a LayerNorm when `ln`).
@@ -72,17 +76,63 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   if (a.nt > kStep16MaxNT || (n + a.nt - 1) / a.nt > cus) return false;
   a.ecap_t = a.nt * cap;
   a.e0_hbm = 0;
+  a.poll_limit = ws->step_poll_limit;
   size_t lds = step16_lds_bytes(a);
   if (lds > kStep16MaxLds) {  // the tile's e0 rows do not fit in LDS: keep them in HBM (ws->uvl's tail)
     a.e0_hbm = 1;
     lds = step16_lds_bytes(a);
   }
   if (lds == 0 || lds > kStep16MaxLds) return false;
+  // co-residency: every workgroup of the launch must be on the device at once (include/sgnn.h)
+  if (step16_resident(a) < (n + a.nt - 1) / a.nt) return false;
   *out = a;
   return true;
 }
 
 constexpr size_t kStepFlagBytes = 512 * sizeof(uint32_t);
+constexpr int kMaxDevices = 64;
+
+// In-process co-residency guard (include/sgnn.h, "Co-residency"): per device, the stream and an event
+// recorded after the last call that ran the one-launch step.  A call holds the lock while it decides
+// and launches, so two host threads cannot both launch one-launch steps on different streams.
+struct Step16Guard {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+};
+std::mutex g_guard_mu;
+Step16Guard g_guard[kMaxDevices];
+
+class Step16Call {
+ public:
+  explicit Step16Call(hipStream_t s) : lk_(g_guard_mu), s_(s) {
+    if (hipGetDevice(&dev_) != hipSuccess || dev_ < 0 || dev_ >= kMaxDevices) {
+      dev_ = -1;
+      return;
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    capturing_ = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+    // (no event query while capturing: the graph's replays are ordered on their own stream)
+    const Step16Guard& g = g_guard[dev_];
+    allow_ = capturing_ || !g.done || g.stream == s || hipEventQuery(g.done) != hipErrorNotReady;
+  }
+  bool allow() const { return allow_ && dev_ >= 0; }
+  // after the call's launches: remember them if any was a one-launch step
+  void launched_step16() {
+    if (dev_ < 0 || capturing_) return;
+    Step16Guard& g = g_guard[dev_];
+    if (!g.done && hipEventCreateWithFlags(&g.done, hipEventDisableTiming) != hipSuccess) {
+      g.done = nullptr;
+      return;
+    }
+    if (hipEventRecord(g.done, s_) == hipSuccess) g.stream = s_;
+  }
+
+ private:
+  std::lock_guard<std::mutex> lk_;
+  hipStream_t s_;
+  int dev_ = -1;
+  bool capturing_ = false, allow_ = false;
+};
 
 }  // namespace
 
@@ -99,22 +149,30 @@ extern "C" int sgnn_step_path(const sgnn_epd* m, const sgnn_step_in* in, const s
 // One predict_positions; `step` = index of this step within the call (the
 // one-launch step's phase counters are zeroed at step 0 and count on).
 // pos_last: optional contiguous copy of pos_seq's last frame (a rollout's previous next_pos).
+// allow16: the call's co-residency guard lets it use the one-launch step; *used16 is set when it did.
 static int predict_impl(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq, const sgnn_step_ws* ws,
                         float* pred, float* next_pos, float* window_out, void* stream, int32_t step,
-                        const float* pos_last = nullptr) {
+                        const float* pos_last, bool allow16, bool* used16) {
   using namespace sgnn;
   if (!m || !in || !pos_seq || !ws || !pred || !next_pos || m->nlayers < 1 || !m->edge || !m->node)
     return set_error(SGNN_ERR_INVALID, "predict_positions: bad arguments");
   if (window_out && window_out == pos_seq)
     return set_error(SGNN_ERR_INVALID, "predict_positions: window_out aliases pos_seq");
+  hipStream_t s = static_cast<hipStream_t>(stream);
   Step16Args sa{};
-  if (step16_plan(m, in, pos_seq, ws, pred, next_pos, window_out, &sa)) {
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (step == 0) (void)hipMemsetAsync(ws->step_flags, 0, kStepFlagBytes, s);
+  if (allow16 && step16_plan(m, in, pos_seq, ws, pred, next_pos, window_out, &sa)) {
+    // the phase counters and the error word start from zero in every call
+    if (step == 0 && hipMemsetAsync(ws->step_flags, 0, kStepFlagBytes, s) != hipSuccess)
+      return check_launch("predict_positions: zeroing the step counters");
     sa.epoch0 = (uint32_t)step * (uint32_t)(m->nlayers + 1);
     sa.pos_last = pos_last;
+    *used16 = true;
     return step16_launch(sa, s);
   }
+  // the per-kernel sequence: clear a previous call's error word so sgnn_step_check reads this call's
+  if (step == 0 && ws->step_flags &&
+      hipMemsetAsync(ws->step_flags + kStep16MaxGrid, 0, sizeof(uint32_t), s) != hipSuccess)
+    return check_launch("predict_positions: clearing the step error word");
   const int64_t n = in->n;
   const int T = in->T, d = in->dim;
   // radius graph on the most recent frame (learned_simulator.py:116-117); graphs of <= 2,560
@@ -202,7 +260,12 @@ static int predict_impl(const sgnn_epd* m, const sgnn_step_in* in, const float* 
 extern "C" int sgnn_predict_positions(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq,
                                       const sgnn_step_ws* ws, float* pred, float* next_pos,
                                       float* window_out, void* stream) {
-  return predict_impl(m, in, pos_seq, ws, pred, next_pos, window_out, stream, 0);
+  Step16Call call(static_cast<hipStream_t>(stream));
+  bool used16 = false;
+  const int st = predict_impl(m, in, pos_seq, ws, pred, next_pos, window_out, stream, 0, nullptr, call.allow(),
+                              &used16);
+  if (used16) call.launched_step16();
+  return st;
 }
 
 extern "C" int sgnn_rollout(const sgnn_epd* m, const sgnn_step_in* in, float* win_a, float* win_b,
@@ -213,13 +276,37 @@ extern "C" int sgnn_rollout(const sgnn_epd* m, const sgnn_step_in* in, float* wi
     return set_error(SGNN_ERR_INVALID, "rollout: bad arguments");
   const int64_t n = in ? in->n : 0;
   const int d = in ? in->dim : 0;
-  for (int32_t k = 0; k < nsteps; ++k) {
+  Step16Call call(static_cast<hipStream_t>(stream));
+  bool used16 = false;
+  int st = SGNN_OK;
+  for (int32_t k = 0; k < nsteps && st == SGNN_OK; ++k) {
     float* cur = (k & 1) ? win_b : win_a;
     float* nxt = (k & 1) ? win_a : win_b;
-    // step k's window ends with step k-1's prediction, already contiguous in out_pos
-    const int st = predict_impl(m, in, cur, ws, out_pred + (int64_t)k * n * (d + 1), out_pos + (int64_t)k * n * d,
-                                nxt, stream, k, k > 0 ? out_pos + (int64_t)(k - 1) * n * d : nullptr);
-    if (st) return st;
+    // step k's window ends with step k-1's prediction, already contiguous in out_pos; every step of
+    // the call takes the path its first step took
+    st = predict_impl(m, in, cur, ws, out_pred + (int64_t)k * n * (d + 1), out_pos + (int64_t)k * n * d, nxt,
+                      stream, k, k > 0 ? out_pos + (int64_t)(k - 1) * n * d : nullptr, call.allow() && (k == 0 || used16),
+                      &used16);
+  }
+  if (used16) call.launched_step16();
+  return st;
+}
+
+extern "C" int sgnn_step_check(const sgnn_step_ws* ws, void* stream) {
+  using namespace sgnn;
+  if (!ws) return set_error(SGNN_ERR_INVALID, "step_check: bad arguments");
+  if (!ws->step_flags) return SGNN_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t word = 0;
+  if (hipMemcpyAsync(&word, ws->step_flags + kStep16MaxGrid, sizeof(word), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return check_launch("step_check: reading the step error word");
+  if (word != 0) {
+    char msg[256];
+    snprintf(msg, sizeof(msg),
+             "one-launch step: a workgroup timed out waiting for its sender tiles (phase %u); this call's "
+             "outputs are invalid (another one-launch step shared the device's CUs?)", word);
+    return set_error(SGNN_ERR_STEP_TIMEOUT, msg);
   }
   return SGNN_OK;
 }

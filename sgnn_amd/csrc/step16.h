@@ -50,12 +50,15 @@ struct Step16Args {
   int nt;              // receivers per workgroup
   int ecap_t;          // edge rows per workgroup (nt * cap)
   int32_t *deg_out, *nbr_out;  // optional: the radius graph as padded lists [n], [n][cap]
+  int poll_limit;      // polls per wait before the error word is set (< 0: test hook, set it at the first wait)
   // outputs
   float *pred, *next_pos, *window_out;
 };
 
 // LDS bytes the kernel needs for these arguments (0 when it does not apply).
 size_t step16_lds_bytes(const Step16Args& a);
+// Workgroups of this launch's kernel variant the device holds at once (CUs x occupancy per CU).
+int64_t step16_resident(const Step16Args& a);
 // Launches the kernel (a.nt / a.ecap_t set by the caller; grid = ceil(n / nt)).
 int step16_launch(const Step16Args& a, hipStream_t s);
 

@@ -34,7 +34,12 @@
 // zeroed by the driver at the start of every call; phase p of step s is
 // epoch0 + p + 1 with epoch0 = s (L + 1).  Every spin is bounded: a tile that
 // times out records it in an error word and finishes (results are then
-// garbage; the driver's tests read the word).
+// garbage): sgnn_step_check returns SGNN_ERR_STEP_TIMEOUT for that call, and
+// the Python wrappers raise SgnnError.
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "common.h"
 #include "fwd16.h"
 #include "sgnn_internal.h"
@@ -132,11 +137,13 @@ struct TilePoll {
   SGNN_DEV void issue2(const int32_t* deps, int ndeps, const uint32_t* flags, uint32_t epoch, int lane) {
     read(w, deps, ndeps, flags, epoch, lane);
   }
-  SGNN_DEV void wait(const int32_t* deps, int ndeps, uint32_t* flags, uint32_t epoch, int lane) {
+  SGNN_DEV void wait(const int32_t* deps, int ndeps, uint32_t* flags, uint32_t epoch, int lane, int limit) {
+    if (limit < 0 && lane == 0)  // test hook (sgnn_step_ws.step_poll_limit < 0): the error path
+      __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ok(v, epoch) || ok(w, epoch)) return;
     for (int it = 0;; ++it) {
       if (ok(v, epoch)) break;
-      if (it >= kPollLimit) {
+      if (it >= limit) {
         if (lane == 0)
           __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -670,7 +677,7 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   if (ep.donor) ep.template prewait<FIRST, true>(xw1, hook);
   else ep.template prewait<FIRST, false>(xw1, hook);
   mark(ps < 0 ? -1 : ps + 3);
-  poll.wait(deps, ndeps, a.flags, ep_k, l);
+  poll.wait(deps, ndeps, a.flags, ep_k, l, a.poll_limit);
   mark(ps < 0 ? -1 : ps + 4);
   ep.postwait(ru, rv, k == 1);
   mark(ps < 0 ? -1 : ps + 5);
@@ -992,37 +999,66 @@ size_t step16_lds_bytes(const Step16Args& a) {
   return sizeof(float) * (size_t)carve(a.n, a.dim, a.nt, a.cap, a.e0_hbm != 0).total;
 }
 
-int step16_launch(const Step16Args& a, hipStream_t s) {
+namespace {
+using Step16Kernel = void (*)(Step16Args);
+
+// The kernel variant for these arguments (null when none applies).
+Step16Kernel step16_kernel(const Step16Args& a) {
+  const int kqf = (a.feat + 15) / 16;
+  if (kqf < 1 || kqf > 3 || a.dim < 1 || a.dim > 3) return nullptr;
+#define SGNN_S16(D_, G_) \
+  return kqf == 1 ? k_step16<D_, 1, G_> : kqf == 2 ? k_step16<D_, 2, G_> : k_step16<D_, 3, G_>
+  if (a.e0_hbm) {
+    if (a.dim == 1) SGNN_S16(1, true);
+    if (a.dim == 2) SGNN_S16(2, true);
+    SGNN_S16(3, true);
+  }
+  if (a.dim == 1) SGNN_S16(1, false);
+  if (a.dim == 2) SGNN_S16(2, false);
+  SGNN_S16(3, false);
+#undef SGNN_S16
+}
+
+// at least 81 KB: one workgroup per CU whatever the shape (the hand-off protocol's measured form)
+size_t step16_lds_request(const Step16Args& a) { return std::max<size_t>(step16_lds_bytes(a), 81 * 1024); }
+}  // namespace
+
+int64_t step16_resident(const Step16Args& a) {
+  const Step16Kernel kern = step16_kernel(a);
+  const size_t lds = step16_lds_bytes(a);
+  if (!kern || lds == 0 || lds > kStep16MaxLds) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  // the occupancy query per (device, variant, LDS request), once
+  static std::mutex mu;
+  static std::map<std::tuple<int, const void*, size_t>, int64_t> cache;
+  const auto key = std::make_tuple(dev, reinterpret_cast<const void*>(kern), step16_lds_request(a));
+  std::lock_guard<std::mutex> lk(mu);
+  const auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kStep16MaxLds);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kBlock16,
+                                                   std::get<2>(key)) != hipSuccess)
+    return 0;
+  return cache[key] = (int64_t)per_cu * cus;
+}
+
+int step16_launch(const Step16Args& a_in, hipStream_t s) {
+  Step16Args a = a_in;
+  if (a.poll_limit == 0) a.poll_limit = kPollLimit;
   const size_t lds = step16_lds_bytes(a);
   const int64_t grid = ((int64_t)a.n + a.nt - 1) / a.nt;
   if (lds == 0 || lds > kStep16MaxLds || grid < 1 || grid > kStep16MaxGrid || a.L < 2 || a.L > kStep16MaxL ||
       a.ecap_t != a.nt * a.cap)
     return set_error(SGNN_ERR_UNSUPPORTED, "step16: shape outside the one-launch step");
-  const int kqf = (a.feat + 15) / 16;
-  if (kqf < 1 || kqf > 3) return set_error(SGNN_ERR_UNSUPPORTED, "step16: more than 48 node features");
-  // at least 81 KB: one workgroup per CU whatever the shape (the hand-off protocol's measured form)
-  const size_t lds_req = std::max<size_t>(lds, 81 * 1024);
-  auto go = [&](auto kern) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kStep16MaxLds);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock16), lds_req, s, a);
-  };
-#define SGNN_S16(D_, G_)                                \
-  do {                                                  \
-    if (kqf == 1) go(k_step16<D_, 1, G_>);              \
-    else if (kqf == 2) go(k_step16<D_, 2, G_>);         \
-    else go(k_step16<D_, 3, G_>);                       \
-  } while (0)
-  if (a.e0_hbm) {
-    if (a.dim == 1) SGNN_S16(1, true);
-    else if (a.dim == 2) SGNN_S16(2, true);
-    else SGNN_S16(3, true);
-  } else {
-    if (a.dim == 1) SGNN_S16(1, false);
-    else if (a.dim == 2) SGNN_S16(2, false);
-    else SGNN_S16(3, false);
-  }
-#undef SGNN_S16
+  const Step16Kernel kern = step16_kernel(a);
+  if (!kern) return set_error(SGNN_ERR_UNSUPPORTED, "step16: more than 48 node features");
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kStep16MaxLds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock16), step16_lds_request(a), s, a);
   return check_launch("step16");
 }
 

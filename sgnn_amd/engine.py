@@ -25,8 +25,6 @@ from ._hip import SgnnMlp, check, lib, stream_ptr
 
 MAX_NUM_NEIGHBORS = 20  # learned_simulator.py:117
 FUSED_MAX_N = 8192      # fused per-layer kernel for graphs up to this size (sgnn_predict_positions)
-STEP1_MAX_N = 4096      # one-launch step (sgnn_step_path) for graphs up to this size
-STEP1_MAX_L = 10
 
 
 def _ptr(t: Optional[torch.Tensor]) -> int:
@@ -92,7 +90,7 @@ class StepWorkspace:
     """HBM buffers for one (n, T, dim, H, K, loop) step shape."""
 
     def __init__(self, n: int, T: int, dim: int, hidden: int, K: int, loop: bool,
-                 device: torch.device, nlayers: int = 0):
+                 device: torch.device, one_launch: bool = True):
         L = lib()
         self.n, self.T, self.dim, self.H, self.K, self.loop = n, T, dim, hidden, K, loop
         cap = K + (0 if loop else 1)
@@ -118,19 +116,47 @@ class StepWorkspace:
         self.agg = torch.empty(n, hidden, **f32)
         self.cin = torch.empty(ntiles, hidden, **f32)
         self.cout = torch.empty(ntiles, hidden, **f32)
-        # one-launch step (sgnn_step_path decides; the C driver falls back to the kernel sequence):
-        # every layer's node halves, the per-workgroup phase counters, the neighbour counts
-        one = hidden == 64 and n <= STEP1_MAX_N and 2 <= nlayers <= STEP1_MAX_L
-        self.uvl = torch.empty(nlayers * 2 * n * hidden + (n + 16) * K * (hidden + 4), **f32) if one else None
-        self.step_flags = torch.zeros(512, **i32) if one else None
-        self.step_deg = torch.zeros(n, **i32) if one else None
+        # one-launch step buffers: allocated by prepare_step the first time sgnn_step_path says a call
+        # takes that path (every layer's node halves, the per-workgroup phase counters, the neighbour counts)
+        self.uvl = self.step_flags = self.step_deg = None
         self.c = _hip.SgnnStepWs(radius_ws=self.radius_ws_ptr(), rowptr=self.rowptr.data_ptr(),
                                  send=self.send.data_ptr(), recv=self.recv.data_ptr(), edge_cap=self.edge_cap,
                                  e0t=self.e0t.data_ptr(), x_a=self.x_a.data_ptr(), x_b=self.x_b.data_ptr(),
                                  u=self.u.data_ptr(), v=self.v.data_ptr(), agg=self.agg.data_ptr(),
                                  cin=self.cin.data_ptr(), cout=self.cout.data_ptr(),
-                                 u2=_ptr(self.u2), v2=_ptr(self.v2), uvl=_ptr(self.uvl),
-                                 step_flags=_ptr(self.step_flags), step_deg=_ptr(self.step_deg))
+                                 u2=_ptr(self.u2), v2=_ptr(self.v2), uvl=0, step_flags=0, step_deg=0,
+                                 step_poll_limit=0)
+        self.device = device
+        self.one_launch = one_launch   # False: never allocate them (calls take the kernel sequence)
+
+    def prepare_step(self, epd_struct, sin) -> bool:
+        """Allocate the one-launch step's buffers when sgnn_step_path says calls with these
+        arguments take it (True then); the C driver still decides per call (its co-residency
+        guard may run the kernel sequence instead)."""
+        if self.step_flags is not None:
+            return True
+        if not self.one_launch:
+            return False
+        probe = _hip.SgnnStepWs.from_buffer_copy(self.c)
+        probe.uvl = probe.step_flags = probe.step_deg = 1   # only tested for NULL by sgnn_step_path
+        if not lib().sgnn_step_path(ctypes.byref(epd_struct), ctypes.byref(sin), ctypes.byref(probe), None, None):
+            return False
+        n, H, K = self.n, self.H, self.K
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.uvl = torch.empty(epd_struct.nlayers * 2 * n * H + (n + 16) * K * (H + 4), **f32)
+        self.step_flags = torch.zeros(512, dtype=torch.int32, device=self.device)
+        self.step_deg = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self.c.uvl, self.c.step_flags, self.c.step_deg = (self.uvl.data_ptr(), self.step_flags.data_ptr(),
+                                                          self.step_deg.data_ptr())
+        return True
+
+    def check_step(self, device) -> None:
+        """Raise SgnnError if the last call's one-launch step timed out waiting for its sender tiles
+        (sgnn_step_check: its outputs are invalid).  Synchronises the stream; skipped while a HIP
+        graph is being captured (the replays' caller checks) and when the step buffers do not exist."""
+        if self.step_flags is None or torch.cuda.is_current_stream_capturing():
+            return
+        check(lib().sgnn_step_check(ctypes.byref(self.c), stream_ptr(device)), "predict_positions")
 
     def radius_ws_ptr(self) -> int:
         p = self.radius_ws.data_ptr()
@@ -145,12 +171,13 @@ class StepWorkspace:
         return int(self.step_deg.sum().item())
 
     def step_timeout(self) -> bool:
-        """True if a workgroup of the one-launch step gave up waiting (its error word)."""
+        """True if a workgroup of the last one-launch step gave up waiting (its error word; tests)."""
         return self.step_flags is not None and int(self.step_flags[256].item()) != 0
 
 
 def step_path(epd_struct, sin, ws: StepWorkspace):
     """(one_launch, nodes per workgroup, workgroups) of sgnn_predict_positions for these arguments."""
+    ws.prepare_step(epd_struct, sin)
     nt, grid = ctypes.c_int32(0), ctypes.c_int32(0)
     one = lib().sgnn_step_path(ctypes.byref(epd_struct), ctypes.byref(sin), ctypes.byref(ws.c),
                                ctypes.byref(nt), ctypes.byref(grid))
@@ -301,9 +328,11 @@ def forward_step(epd: nn.Module, emb_weight: Optional[torch.Tensor], use_emb: bo
     pk = ParamPack.get(epd)
     if timers is None:
         sin = step_in(inp, ws, radius, emb_weight, use_emb)
+        ws.prepare_step(pk.epd, sin)
         check(L.sgnn_predict_positions(ctypes.byref(pk.epd), ctypes.byref(sin), inp.pos_seq.data_ptr(),
                                        ctypes.byref(ws.c), pred.data_ptr(), next_pos.data_ptr(),
                                        _ptr(window_out), stream_ptr(inp.pos_seq.device)), "sgnn_predict_positions")
+        ws.check_step(inp.pos_seq.device)
         return
     n, T, d = ws.n, ws.T, ws.dim
     s = stream_ptr(inp.pos_seq.device)
@@ -482,17 +511,22 @@ class DeviceRollout:
                  nsteps: int, keep=()):
         dev = window.device
         self.epd, self.sin, self.ws, self.keep = epd_struct, sin, ws, keep
+        ws.prepare_step(epd_struct, sin)
         self.n, self.dim, self.nsteps = n, dim, nsteps
         self.win = [window.to(torch.float32).contiguous().clone(), torch.empty_like(window, dtype=torch.float32)]
         self.out_pos = torch.empty(max(nsteps, 1), n, dim, dtype=torch.float32, device=dev)
         self.out_pred = torch.empty(max(nsteps, 1), n, dim + 1, dtype=torch.float32, device=dev)
 
-    def run(self, window: Optional[torch.Tensor] = None):
-        """Returns (positions [nsteps, n, dim], strain [nsteps, n]) on the device."""
+    def run(self, window: Optional[torch.Tensor] = None, check_step: bool = True):
+        """Returns (positions [nsteps, n, dim], strain [nsteps, n]) on the device.  With check_step
+        (default) the call ends with sgnn_step_check (a stream sync) and raises SgnnError when a
+        one-launch step timed out; a caller passing False must call ws.check_step itself."""
         if window is not None:
             self.win[0].copy_(window)
         check(lib().sgnn_rollout(ctypes.byref(self.epd), ctypes.byref(self.sin), self.win[0].data_ptr(),
                                  self.win[1].data_ptr(), ctypes.byref(self.ws.c), self.nsteps,
                                  self.out_pos.data_ptr(), self.out_pred.data_ptr(),
                                  stream_ptr(self.win[0].device)), "sgnn_rollout")
+        if check_step:
+            self.ws.check_step(self.win[0].device)
         return self.out_pos[:self.nsteps], self.out_pred[:self.nsteps, :, -1]

@@ -88,8 +88,7 @@ class LearnedSimulator(nn.Module):
                 self._ws_cache.clear()
             ws = engine.StepWorkspace(n, T, self._particle_dimensions,
                                       self._encode_process_decode.latent_dim,
-                                      self._max_num_neighbors, loop, device,
-                                      nlayers=len(self._encode_process_decode._processor.gnn_stacks))
+                                      self._max_num_neighbors, loop, device)
             self._ws_cache[key] = ws
         return ws
 

@@ -16,13 +16,13 @@ pytestmark = pytest.mark.gpu
 
 def _run(sim, pos, counts, types_, one_launch):
     """predict_positions with the one-launch step enabled or not (a workspace
-    without its buffers makes the driver take the per-kernel sequence)."""
+    that never allocates its buffers makes the driver take the per-kernel sequence)."""
     from sgnn_amd import engine
     inp, use_emb = sim._step_inputs(pos, counts, types_)
     n, T, d = inp.pos_seq.shape
     ws = sim._workspace(n, T, pos.device)
     if not one_launch:
-        ws = engine.StepWorkspace(n, T, d, 64, sim._max_num_neighbors, True, pos.device, nlayers=0)
+        ws = engine.StepWorkspace(n, T, d, 64, sim._max_num_neighbors, True, pos.device, one_launch=False)
     pk = engine.ParamPack.get(sim._encode_process_decode)
     sin = engine.step_in(inp, ws, sim._connectivity_radius, sim._particle_type_embedding.weight, use_emb)
     path = engine.step_path(pk.epd, sin, ws)
@@ -122,3 +122,33 @@ def test_headline_rollout_20_steps_against_oracle():
     _close(pos.cpu().numpy(), ref_pos.numpy(), atol=2 * nsteps * ATOL * scale, rtol=1e-6,
            what="C1 r=15 20-step rollout positions")
     _close(strain.cpu().numpy(), ref_str.numpy(), atol=2 * nsteps * ATOL, what="C1 r=15 20-step rollout strain")
+
+
+def test_step_timeout_raises_and_recovers():
+    """A one-launch step whose tiles give up waiting must not return as a success
+    (VERDICT r03 item 1): the test hook step_poll_limit < 0 makes every tile
+    record a timeout at its first wait; predict_positions and the rollout runner
+    then raise SgnnError.  The next call (default limit) zeroes the error word
+    and is valid again: same positions as before the forced failure."""
+    from sgnn_amd import _hip
+    z = golden("c1_r15")
+    hp = hparams(z)
+    sim = product_sim(z)
+    pos = torch.from_numpy(z["positions"][:, :hp["T"]]).cuda()
+    n = pos.shape[0]
+    types_ = torch.zeros(n, dtype=torch.long, device="cuda")
+    nxt0, _ = sim.predict_positions(pos, [n], types_)
+    ws = sim._workspace(n, hp["T"], pos.device)
+    assert ws.step_flags is not None, "C1 shape should take the one-launch step"
+    ws.c.step_poll_limit = -1
+    try:
+        with pytest.raises(_hip.SgnnError, match="timed out"):
+            sim.predict_positions(pos, [n], types_)
+        runner = sim.rollout_runner(pos, [n], types_, 3)
+        with pytest.raises(_hip.SgnnError, match="timed out"):
+            runner.run()
+    finally:
+        ws.c.step_poll_limit = 0
+    nxt1, _ = sim.predict_positions(pos, [n], types_)
+    assert not ws.step_timeout()
+    assert torch.equal(nxt0, nxt1)
