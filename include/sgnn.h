@@ -106,30 +106,10 @@ int sgnn_encode_edge_features(const float* e, int32_t fe, const int32_t* perm,
                               const sgnn_mlp* enc, float* e0t, void* stream);
 
 /* ---------------------------------------------------------------------------
- * Width-generic blocks (generic.hip): any latent / hidden / edge widths and
- * nmlp_layers, plain fp32 FMA -- the reference's build_mlp(...) (+ LayerNorm)
- * (graph_network.py:7-45, :86-96, :139-148, :321-322; multi_scale_gnn.py:26-64)
- * on rows assembled from up to three sources, the MessagePassing receiver sum
- * (aggr='add', graph_network.py:136 / multi_scale_gnn.py:67) and the feature
- * construction of _encoder_preprocessor (learned_simulator.py:231-316).  They
- * back the reference's per-module forwards (Encoder / InteractionNetwork /
- * Processor / Decoder, G2M / M2M / M2G blocks) and the shapes the MFMA kernels
- * are not built for; the hidden-64 / 128 kernels above are the fast path.
+ * Feature construction on explicit tensors (generic.hip): the node and edge
+ * features of _encoder_preprocessor (learned_simulator.py:231-316) for the
+ * width-generic path (the fused encoders compute them on the fly).
  * ------------------------------------------------------------------------- */
-typedef struct sgnn_rows_src {
-  const float* data;    /* row r of this source: data[(index ? index[r] : r) * ld + c], c < dim */
-  const int32_t* index; /* optional gather (e.g. receivers / senders of every edge) */
-  int64_t ld;
-  int32_t dim;
-  float scale;          /* multiplies every value read (1 = none) */
-} sgnn_rows_src;
-/* out[r] = MLP(cat(src_0[r], .., src_{nsrc-1}[r])) (+ LayerNorm when mlp->ln_g) (+ residual[r]);
- * out / residual: [n][mlp->out_dim].  1 <= nsrc <= 3; the widths must sum to mlp->in_dim. */
-int sgnn_rows_mlp(const sgnn_rows_src* srcs, int32_t nsrc, int64_t n, const sgnn_mlp* mlp,
-                  const float* residual, float* out, void* stream);
-/* agg[i] = sum of m[perm ? perm[p] : p] over p in [rowptr[i], rowptr[i+1]) (receiver CSR, in order). */
-int sgnn_segment_sum(const float* m, const int32_t* rowptr, const int32_t* perm, int64_t n, int32_t width,
-                     float* agg, void* stream);
 /* Node features [n][(T-1)*dim + 1 (+ emb_dim)] (learned_simulator.py:256-290; wall as sgnn_encode_nodes). */
 int sgnn_node_features(const float* pos_seq, int64_t n, int32_t T, int32_t dim, const int64_t* types,
                        const float* emb_w, int32_t emb_dim, int32_t use_emb, const float* vel_mean,
@@ -469,6 +449,54 @@ int sgnn_random_walk_noise(const float* pos_seq, int64_t n, int32_t T, int32_t d
  * (amsgrad=False, weight_decay=0) used by train.py:199,271-273. step >= 1. */
 int sgnn_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float lr, float beta1, float beta2, float eps, int64_t step, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Width-generic differentiable building blocks (autograd.hip).  The
+ * reference's modules are differentiable at any widths and depths
+ * (build_mlp, graph_network.py:7-45; Encoder / InteractionNetwork / Processor /
+ * Decoder forwards :98, :150, :276, :324; G2M / M2M / M2G blocks,
+ * multi_scale_gnn.py:84, :132, :179): these are the forward and backward
+ * pieces the Python autograd Functions (sgnn_amd/autograd.py) compose for
+ * every shape the fused MFMA kernels are not built for.  Everything is
+ * deterministic: no float atomics, fixed summation orders.
+ * ------------------------------------------------------------------------- */
+/* C[M][N] (ldc) = op(A) op(B) (+ C when accumulate) (+ bias[n]) (then ReLU when relu), fp32 on the
+ * MFMA cores (v_mfma_f32_32x32x2_f32, exact fp32 products).  op(A) = A stored [M][K] (lda), or A^T with
+ * A stored [K][M] (trans_a); op(B) = B stored [K][N] (ldb), or B^T with B stored [N][K] (trans_b).
+ * Long K is split over workgroups whose partial tiles are summed in split order in `workspace`
+ * (sgnn_gemm_workspace_bytes(M, N, K) bytes; the split depends on the shape only). */
+size_t sgnn_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int sgnn_gemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+              const float* B, int64_t ldb, const float* bias, int32_t relu, float* C, int64_t ldc,
+              int32_t accumulate, void* workspace, size_t workspace_bytes, void* stream);
+/* LayerNorm over rows of `width` (torch: biased variance, eps 1e-5, affine), out = LN(x) (+ residual);
+ * yhat [n][width] / rstd [n] receive the normalised rows and 1/std when not NULL. */
+int sgnn_layernorm(const float* x, int64_t n, int32_t width, const float* gamma, const float* beta,
+                   const float* residual, float* out, float* yhat, float* rstd, void* stream);
+/* dx = rstd (g - mean(g) - yhat mean(g yhat)), g = dout * gamma (per row). */
+int sgnn_layernorm_bwd(const float* dout, const float* yhat, const float* rstd, const float* gamma, int64_t n,
+                       int32_t width, float* dx, void* stream);
+/* out[c] (+)= sum_r x[r][c] (* mul[r][c]) over the n rows, in row order per 256-row block, blocks in order
+ * (workspace: sgnn_colsum_workspace_bytes(n, width)). */
+size_t sgnn_colsum_workspace_bytes(int64_t n, int32_t width);
+int sgnn_colsum(const float* x, int64_t ldx, const float* mul, int64_t ldm, int64_t n, int32_t width, float* out,
+                int32_t accumulate, void* workspace, size_t workspace_bytes, void* stream);
+/* dy[r][c] = y[r][c] > 0 ? dy[r][c] : 0 (ReLU backward on the saved post-activation rows). */
+int sgnn_relu_bwd(float* dy, int64_t ldd, const float* y, int64_t ldy, int64_t n, int32_t width, void* stream);
+/* out[r][0:width] (ld_out) = scale * src[index ? index[r] : r][0:width] (ld_src): one column block of a
+ * concatenation of gathered rows (cat([x_i, x_j, e]), graph_network.py:197). */
+int sgnn_gather_rows(const float* src, int64_t ld_src, int32_t width, const int32_t* index, int64_t nrows,
+                     float scale, float* out, int64_t ld_out, void* stream);
+/* out[i][0:width] (+)= scale * sum over p in [rowptr[i], rowptr[i+1]) of src[perm ? perm[p] : p][0:width], in
+ * CSR order: the receiver sums of aggr='add' (graph_network.py:136) and the backward of a row gather. */
+int sgnn_segment_sum_cols(const float* src, int64_t ld_src, int32_t width, const int32_t* rowptr,
+                          const int32_t* perm, int64_t n, float scale, float* out, int64_t ld_out,
+                          int32_t accumulate, void* stream);
+/* Explicit edge latent rows e [E][width] (COO order; ld) -> the tiled e0t layout sgnn_edge_layer reads
+ * (width a multiple of 32; CSR position p reads row perm[p] of sgnn_coo_to_csr; tiles padded with zeros up
+ * to edge_cap).  InteractionNetwork.forward(x, edge_index, e) on the fused kernels (graph_network.py:150). */
+int sgnn_edge_rows_to_tiles(const float* e, int64_t ld, int32_t width, const int32_t* perm, const int32_t* rowptr,
+                            int64_t n, int64_t edge_cap, float* e0t, void* stream);
 
 #ifdef __cplusplus
 }

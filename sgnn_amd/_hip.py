@@ -67,11 +67,6 @@ class SgnnReduceDesc(ctypes.Structure):
                 ("scale", c_float)]
 
 
-class SgnnRowsSrc(ctypes.Structure):
-    """struct sgnn_rows_src (include/sgnn.h)."""
-    _fields_ = [("data", c_void_p), ("index", c_void_p), ("ld", c_int64), ("dim", c_int32), ("scale", c_float)]
-
-
 P_SAVES = ctypes.POINTER(SgnnSaves)
 SLAB_EDGE, SLAB_NODE, SLAB_UV, SLAB_DECODER, SLAB_ENC_NODE, SLAB_ENC_EDGE = range(6)
 
@@ -156,9 +151,6 @@ SIGNATURES = {
                                              P_MLP, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
     "sgnn_predict_positions": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p, c_void_p]),
-    "sgnn_rows_mlp": (ctypes.c_int, [ctypes.POINTER(SgnnRowsSrc), c_int32, c_int64, P_MLP, c_void_p, c_void_p,
-                                     c_void_p]),
-    "sgnn_segment_sum": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     "sgnn_node_features": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                           c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p]),
     "sgnn_edge_features": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_int64,
@@ -171,6 +163,23 @@ SIGNATURES = {
                                               ctypes.c_uint64, c_void_p, c_void_p, c_void_p]),
     "sgnn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,
                                       c_float, c_float, c_float, c_int64, c_void_p]),
+    "sgnn_gemm_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int64, c_int64]),
+    "sgnn_gemm": (ctypes.c_int, [c_int32, c_int32, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                 c_void_p, c_int32, c_void_p, c_int64, c_int32, c_void_p, ctypes.c_size_t, c_void_p]),
+    "sgnn_layernorm": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p]),
+    "sgnn_layernorm_bwd": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p,
+                                          c_void_p]),
+    "sgnn_colsum_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int32]),
+    "sgnn_colsum": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int32,
+                                   c_void_p, ctypes.c_size_t, c_void_p]),
+    "sgnn_relu_bwd": (ctypes.c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
+    "sgnn_gather_rows": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_float, c_void_p, c_int64,
+                                        c_void_p]),
+    "sgnn_segment_sum_cols": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int64, c_float,
+                                             c_void_p, c_int64, c_int32, c_void_p]),
+    "sgnn_edge_rows_to_tiles": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int64, c_int64,
+                                               c_void_p, c_void_p]),
 }
 
 _LIB: Optional[ctypes.CDLL] = None

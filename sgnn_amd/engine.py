@@ -501,6 +501,49 @@ def epd_forward(epd, x, edge_index, edge_features):
                      [2.0 ** k for k in range(nl)], x, {"e": g}, {"e": ef}, pk.dec.out_dim)
 
 
+def interaction_forward(block: nn.Module, x: torch.Tensor, edge_index: torch.Tensor, edge_features: torch.Tensor,
+                        graph: Optional[CsrGraph] = None):
+    """One InteractionNetwork / G2M / M2M / M2G block forward in inference
+    (graph_network.py:150-222) on the fused kernels: u = W1_i x + b1 and v = W1_j x
+    (the node halves of the first edge Linear, sgnn_gemm), the given edge latent
+    rows in the tiled layout (sgnn_edge_rows_to_tiles), then sgnn_edge_layer
+    (k_edge_layer: gather, edge MLP, LayerNorm, receiver sums) and sgnn_node_layer
+    (k_node_layer: node MLP, LayerNorm, residual).  Returns (x', 2e)."""
+    from . import autograd
+    x = _feature_rows(x, "x")
+    e = _feature_rows(edge_features, "edge_features")
+    n = x.shape[0]
+    g = graph if graph is not None else coo_to_csr(edge_index, n, with_perm=True)
+    if e.shape[0] != g.num_edges:
+        raise ValueError(f"{e.shape[0]} edge feature rows for {g.num_edges} edges")
+    L = lib()
+    dev = x.device
+    s = stream_ptr(dev)
+    edge_fn, node_fn = mlp_struct(block.edge_fn, True), mlp_struct(block.node_fn, True)
+    H = edge_fn.hidden
+    w1 = _linears(block.edge_fn[0])[0]
+    u = autograd.gemm(x, w1.weight[:, :H], tb=True, bias=w1.bias)
+    v = autograd.gemm(x, w1.weight[:, H:2 * H], tb=True)
+    f32 = dict(dtype=torch.float32, device=dev)
+    e0t = torch.empty(int(L.sgnn_edge_latent_floats(g.edge_cap, H)), **f32)
+    check(L.sgnn_edge_rows_to_tiles(e.data_ptr() if g.num_edges else None, max(e.stride(0), H), H, g.perm.data_ptr(),
+                                    g.rowptr.data_ptr(), n, g.edge_cap, e0t.data_ptr(), s), "sgnn_edge_rows_to_tiles")
+    agg = torch.empty(n, H, **f32)
+    cin, cout = torch.empty(g.ntiles, H, **f32), torch.empty(g.ntiles, H, **f32)
+    check(L.sgnn_edge_layer(u.data_ptr(), v.data_ptr(), e0t.data_ptr(), 1.0, g.rowptr.data_ptr(), g.send.data_ptr(),
+                            g.recv.data_ptr(), n, g.edge_cap, ctypes.byref(edge_fn), agg.data_ptr(), cin.data_ptr(),
+                            cout.data_ptr(), None, s), "sgnn_edge_layer")
+    x_out = torch.empty(n, H, **f32)
+    # sgnn_node_layer also forms the next block's u / v: given this block's edge_fn, into scratch
+    check(L.sgnn_node_layer(x.data_ptr(), agg.data_ptr(), cin.data_ptr(), cout.data_ptr(), g.rowptr.data_ptr(), n,
+                            ctypes.byref(node_fn), ctypes.byref(edge_fn), x_out.data_ptr(), u.data_ptr(),
+                            v.data_ptr(), None, s), "sgnn_node_layer")
+    e2 = torch.empty_like(e)
+    if g.num_edges:
+        autograd.gather_into(e2, 0, e, None, 2.0)   # update returns the input edge features: e + e
+    return x_out, e2
+
+
 class DeviceRollout:
     """Autoregressive rollout issued as ONE sgnn_rollout call (evaluate.py:
     117-145): the C driver ping-pongs two window buffers (the shift is fused

@@ -6,8 +6,11 @@ EncodeProcessDecode :336-406) so that `state_dict()` keys, shapes and the
 default-initialisation RNG order are identical to the reference's — reference
 checkpoints load unchanged.  The arithmetic runs in libsgnn_hip.so: a
 whole EncodeProcessDecode (and LearnedSimulator's steps) through the fused
-MFMA kernels (`sgnn_amd.engine`), each module's own forward on explicit
-tensors through the width-generic kernels (`sgnn_amd.generic`).
+MFMA kernels (`sgnn_amd.engine`); each module's own forward on explicit
+tensors through the fused edge / node kernels in inference at the fast widths,
+and otherwise -- any widths, any depth, and whenever autograd needs a graph --
+through the differentiable width-generic path (`sgnn_amd.autograd`, dispatch in
+`sgnn_amd.generic`).
 """
 from __future__ import annotations
 
@@ -43,8 +46,8 @@ class Encoder(nn.Module):
 
     def forward(self, x, edge_features):
         """graph_network.py:98-111 -> (node latent, edge latent)."""
-        from . import generic
-        return generic.encoder_forward(self, x, edge_features)
+        from . import autograd
+        return autograd.encoder_forward(self, x, edge_features)
 
 
 class InteractionNetwork(nn.Module):
@@ -86,8 +89,8 @@ class Decoder(nn.Module):
 
     def forward(self, x):
         """graph_network.py:324-333"""
-        from . import generic
-        return generic.decoder_forward(self, x)
+        from . import autograd
+        return autograd.decoder_forward(self, x)
 
 
 class EncodeProcessDecode(nn.Module):
@@ -111,9 +114,7 @@ class EncodeProcessDecode(nn.Module):
 
     def forward(self, x, edge_index, edge_features):
         """graph_network.py:388-406 on explicit features: the fused MFMA chain
-        (engine.epd_forward) for the widths it is built for, else module by
-        module on the width-generic kernels."""
-        from . import engine, generic
-        if generic.fast_shapes(self):
-            return engine.epd_forward(self, x, edge_index, edge_features)
+        (engine.epd_forward) in inference at the widths it is built for, else
+        module by module on the differentiable path."""
+        from . import generic
         return generic.epd_forward(self, x, edge_index, edge_features)

@@ -217,7 +217,9 @@ class LearnedSimulator(nn.Module):
                               particle_types: torch.Tensor):
         """learned_simulator.py:440-491 -> (predicted_normalized_acceleration,
         target_normalized_acceleration, predicted_strain); differentiable with
-        respect to the EncodeProcessDecode parameters (HIP backward)."""
+        respect to the EncodeProcessDecode parameters and the type embedding: the
+        fused HIP backward at the widths it is built for, the width-generic
+        autograd path (sgnn_amd.autograd) at every other shape."""
         noisy = position_sequence + position_sequence_noise
         epd = self._encode_process_decode
         params = list(epd.parameters())
@@ -225,12 +227,11 @@ class LearnedSimulator(nn.Module):
             self._nparticle_types > 1 and self._particle_type_embedding.weight.requires_grad))
         inp, use_emb = self._step_inputs(noisy, nparticles_per_example, particle_types)
         n, T, d = inp.pos_seq.shape
-        if need_grad:
-            training.check_trainable(epd, self._nparticle_types)
+        if need_grad and training.fused_trainable(epd, self._nparticle_types):
             tw = self._train_workspace(n, T, inp.pos_seq.device)
             emb = self._particle_type_embedding.weight if use_emb else None
             pred = _TrainedEPD.apply(self, inp, tw, emb, *params)
-        elif not self._fast_path():
+        elif need_grad or not self._fast_path():   # differentiable width-generic path (any widths / depth)
             pred = generic.predict_step(self, inp, use_emb)
         else:
             ws = self._workspace(n, T, inp.pos_seq.device)

@@ -32,15 +32,13 @@ from .ms_engine import EDGE_TYPES
 KIND_SLOT = {"g2m": 0, "m2m": 1, "m2g": 2}
 
 
-def check_trainable(sim) -> None:
-    gnn = sim._multi_scale_gnn
-    if gnn.latent_dim not in (64, 128) or gnn.nedge_out != gnn.latent_dim:
-        raise NotImplementedError("HIP multi-scale training: latent_dim = nedge_out in {64, 128} (other widths "
-                                  "run inference only, on the width-generic kernels)")
-    if gnn.nmlp_layers not in (1, 2):
-        raise NotImplementedError("HIP multi-scale training: nmlp_layers must be 1 or 2")
-    if sim._nparticle_types > MAX_TYPES:
-        raise NotImplementedError(f"HIP multi-scale training: at most {MAX_TYPES} particle types")
+def fused_trainable(sim) -> bool:
+    """The fused multi-scale training kernels implement this model (latent =
+    nedge_out in {64, 128}, nmlp_layers 1 or 2, the encoder widths they tile,
+    <= 256 particle types); every other shape trains on the differentiable
+    width-generic path (sgnn_amd.autograd)."""
+    from .. import generic
+    return generic.ms_fast_shapes(sim._multi_scale_gnn) and sim._nparticle_types <= MAX_TYPES
 
 
 class MSTrainWorkspace:
@@ -257,7 +255,7 @@ class MultiScaleTrainer:
                  lr_decay_steps: int = 15000, noise_std: float = 0.02,
                  loss_weight_position: float = 1.0, loss_weight_strain: float = 1.0,
                  group=None, nslab: int = MS_NSLAB):
-        check_trainable(simulator)
+        self.fused = fused_trainable(simulator)
         self.sim = simulator
         self.gnn = simulator._multi_scale_gnn
         self.flat = FlatParams(simulator)
@@ -302,6 +300,12 @@ class MultiScaleTrainer:
         else:
             noise = noise.to(pos.device, torch.float32).contiguous()
             noisy = (pos + noise).contiguous()
+        if not self.fused:   # differentiable width-generic path (e.g. nedge_out != latent_dim)
+            from ..train import autograd_step
+            autograd_step(self, lambda: self.sim.predict_accelerations(
+                next_position.to(pos.device, torch.float32), noise, pos, None, particle_types),
+                next_strain.to(pos.device, torch.float32), n_global)
+            return self._finish(self.flat.loss, n_global)
         inp, _ = self.sim._step_inputs(noisy, particle_types)
         n, T, _ = noisy.shape
         tw = self.workspace(n, T, pos.device)
@@ -314,9 +318,11 @@ class MultiScaleTrainer:
                        emb_grad=self.grads.get("_particle_type_embedding.weight"))
         self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
         self.opt.step()
+        return self._finish(tw.loss_out, n_global)
+
+    def _finish(self, lo: torch.Tensor, n_global: int) -> dict:
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6
         self.step += 1
-        lo = tw.loss_out
         return {"loss": lo[0] / n_global, "loss_position": (lo[1] + lo[2] + lo[3]) / n_global,
                 "loss_strain": lo[4] / n_global, "loss_xyz": lo[1:4] / n_global,
                 "n_global": n_global, "lr": self.opt.lr}

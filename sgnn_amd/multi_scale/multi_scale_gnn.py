@@ -7,8 +7,8 @@ unchanged; under one seed both draw identical weights).  The arithmetic of
 (encoder -> G2M -> M2M x L -> M2G -> prediction head), driven by
 `MultiScaleSimulator`; `MultiScaleGNN.forward` on explicit features runs the
 same kernels, and each block's own forward (and any width the fused kernels
-are not built for, e.g. nedge_out != latent_dim) runs on the width-generic
-kernels (`sgnn_amd.generic`).
+are not built for, e.g. nedge_out != latent_dim, and every forward under
+autograd) runs on the differentiable width-generic path (`sgnn_amd.autograd`).
 
 Semantics the kernels implement (what PyG executes for these blocks):
   message  m = LN(MLP_e([x_i, x_j, e]))   (multi_scale_gnn.py:96-101)
@@ -92,12 +92,8 @@ class MultiScaleGNN(nn.Module):
     def forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index, m2m_edge_features,
                 m2g_edge_index, m2g_edge_features, graph_hierarchy=None):
         """multi_scale_gnn.py:262-326 on explicit features (HIP kernels: the fused
-        chain, or block by block on the width-generic kernels for widths it is
-        not built for); graph_hierarchy is unused, as in the reference."""
+        chain in inference at the widths it is built for, else block by block on
+        the differentiable path); graph_hierarchy is unused, as in the reference."""
         from .. import generic
-        from . import ms_engine
-        if generic.ms_fast_shapes(self):
-            return ms_engine.gnn_forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index,
-                                         m2m_edge_features, m2g_edge_index, m2g_edge_features)
         return generic.ms_gnn_forward(self, x, g2m_edge_index, g2m_edge_features, m2m_edge_index,
                                       m2m_edge_features, m2g_edge_index, m2g_edge_features)

@@ -180,12 +180,10 @@ class MultiScaleSimulator(nn.Module):
     def _run(self, position_sequence, particle_types, window_out=None):
         inp, use_emb = self._step_inputs(position_sequence, particle_types)
         n, T, d = inp.pos_seq.shape
-        if not self._fast_path():   # e.g. nedge_out != latent_dim: block by block, width-generic kernels
+        if not self._fast_path():   # e.g. nedge_out != latent_dim: block by block, width-generic path
             if window_out is not None:
                 raise NotImplementedError("window_out needs the fused chain")
-            nf, idx, ef = self._encoder_preprocessor(inp.pos_seq, None, particle_types)
-            pred = generic.ms_gnn_forward(self._multi_scale_gnn, nf, idx["g2m"], ef["g2m"], idx["m2m"], ef["m2m"],
-                                          idx["m2g"], ef["m2g"])
+            pred = self._generic_pred(inp, use_emb)
             return inp, pred, self._decoder_postprocessor(pred[:, :d], inp.pos_seq)
         dev = inp.pos_seq.device
         graphs = self._csr(n, dev)
@@ -196,6 +194,32 @@ class MultiScaleSimulator(nn.Module):
                                graphs, self._grid_radius(), self._mesh_radius(), ws, pred, nxt,
                                window_out)
         return inp, pred, nxt
+
+    def _generic_pred(self, inp: engine.StepInputs, use_emb: bool) -> torch.Tensor:
+        """MultiScaleGNN(features) on the differentiable width-generic path
+        (sgnn_amd.autograd): node features from sgnn_node_features (wall
+        clamp(x + 2, 0, R_g) / R_g, :190-193) with the type embedding as a
+        differentiable gather, edge features of the three static graphs in their
+        receiver-CSR order (sgnn_edge_features; g2m / m2g over R_g, m2m over the
+        coarsest mesh radius, :206-250), then block by block."""
+        from .. import autograd
+        pos = inp.pos_seq
+        n, T, d = pos.shape
+        dev = pos.device
+        graphs = self._csr(n, dev)
+        key = (n, str(dev), "autograd")
+        egs = self._csr_cache.get(key)
+        if egs is None:
+            egs = {k: autograd.EdgeGraph(torch.stack([g.send[:g.num_edges], g.recv[:g.num_edges]]), n)
+                   for k, g in graphs.items()}
+            self._csr_cache[key] = egs
+        rg, rm = self._grid_radius(), self._mesh_radius()
+        nf = autograd.node_features(pos, inp.types, self._particle_type_embedding.weight, use_emb, inp.vel_mean,
+                                    inp.vel_std, rg, rg, self._nparticle_types)
+        ef = {k: generic.edge_features(graphs[k], pos, (T - 1) * d, T * d, d, r)
+              for k, r in (("g2m", rg), ("m2m", rm), ("m2g", rg))}
+        return autograd.ms_gnn_forward(self._multi_scale_gnn, nf, None, ef["g2m"], None, ef["m2m"], None, ef["m2g"],
+                                       graphs=egs)
 
     def rollout_runner(self, window: torch.Tensor, particle_types, nsteps: int):
         """Device-resident rollout of `nsteps` predict_positions steps from
@@ -268,9 +292,13 @@ class MultiScaleSimulator(nn.Module):
         noisy = position_sequence + position_sequence_noise
         params = list(self._multi_scale_gnn.parameters())
         d = self._kinematic_dimensions
-        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
-            from . import ms_training
-            ms_training.check_trainable(self)
+        from . import ms_training
+        need_grad = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or (
+            self._nparticle_types > 1 and self._particle_type_embedding.weight.requires_grad))
+        if need_grad and not ms_training.fused_trainable(self):   # differentiable width-generic path
+            inp, use_emb = self._step_inputs(noisy, particle_types)
+            pred = self._generic_pred(inp, use_emb)
+        elif need_grad:
             inp, _ = self._step_inputs(noisy, particle_types)
             n, T, _ = inp.pos_seq.shape
             tw = self._train_workspace(n, T, inp.pos_seq.device)

@@ -67,6 +67,9 @@ class DataParallel:
         # gloo (CPU tests, or several ranks sharing one GPU) reduces host tensors: device buffers are
         # staged through host memory; nccl (= RCCL on ROCm) reduces them in place over xGMI
         self.host_staging = on and dist.get_backend(group) == "gloo"
+        # test hook: the overlapped bucket path on a one-rank RCCL group (tests/test_gpu_dp.py: RCCL refuses
+        # two ranks on one device, so the box's one GPU runs the collectives' stream logic at world size 1)
+        self.force_overlap = False
 
     def layout(self, n_local: int, device) -> Tuple[int, int]:
         """(N_global, offset): the particle count over all ranks (the mean
@@ -89,7 +92,7 @@ class DataParallel:
         """Per-layer gradient buckets all-reduced on the side stream while the
         layers below run their backward (device collectives only: gloo stages
         device buffers through host memory, so it keeps the one collective)."""
-        return OVERLAP_BUCKETS and self.world > 1 and not self.host_staging
+        return OVERLAP_BUCKETS and (self.world > 1 or self.force_overlap) and not self.host_staging
 
     def allreduce_async(self, t: torch.Tensor, stream: torch.cuda.Stream):
         """SUM all-reduce of `t` ordered after the work queued on `stream`; the
@@ -157,7 +160,8 @@ class Trainer:
                  group=None, nslab: Optional[int] = None):
         self.sim = simulator
         self.epd = simulator._encode_process_decode
-        training.check_trainable(self.epd, simulator._nparticle_types)
+        # the fused kernels where they are built for the widths, else the width-generic autograd path
+        self.fused = training.fused_trainable(self.epd, simulator._nparticle_types)
         self.flat = training.FlatParams(simulator)
         self.opt = training.Adam(self.flat, lr_init)
         self.grads: Dict[str, torch.Tensor] = {k: p.grad for k, p in simulator.named_parameters()}
@@ -210,6 +214,9 @@ class Trainer:
         else:
             noise = noise.to(pos.device, torch.float32).contiguous()
             noisy = (pos + noise).contiguous()                      # learned_simulator.py:467
+        if not self.fused:
+            return self._generic_step(pos, noise, next_position, next_strain, nparticles_per_example,
+                                      particle_types, n_global)
         inp, _ = self.sim._step_inputs(noisy, nparticles_per_example, particle_types)
         n, T, _ = noisy.shape
         tw = self.workspace(n, T, pos.device)
@@ -239,12 +246,46 @@ class Trainer:
             for w in works:
                 w.wait()
         self.opt.step()
+        return self._finish(n_global)
+
+    def _finish(self, n_global: int) -> dict:
         # train.py:276-278: LR for the NEXT step, computed from the pre-increment step
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6
         self.step += 1
-        lo = tw.loss_out[:5] / n_global        # one kernel; the terms are views of it
+        lo = self.flat.loss[:5] / n_global     # one kernel; the terms are views of it
         return {"loss": lo[0], "loss_position": lo[1:4].sum(), "loss_strain": lo[4],
                 "loss_xyz": lo[1:4], "n_global": n_global, "lr": self.opt.lr}
+
+    def _generic_step(self, pos, noise, next_position, next_strain, nparticles_per_example, particle_types,
+                      n_global: int) -> dict:
+        """The step at shapes the fused kernels are not built for (autograd_step)."""
+        autograd_step(self, lambda: self.sim.predict_accelerations(
+            next_position.to(pos.device, torch.float32), noise, pos, nparticles_per_example, particle_types),
+            next_strain.to(pos.device, torch.float32), n_global)
+        return self._finish(n_global)
+
+
+def autograd_step(trainer, predict, next_strain: torch.Tensor, n_global: int) -> None:
+    """One optimisation step on the differentiable width-generic path (HIP forward
+    and backward, sgnn_amd.autograd): `predict()` = predict_accelerations, the
+    reference's loss (train.py:257-268 / multi_scale_train.py:160-176) as this
+    rank's sums over N_global, backward into the flat gradient views, the loss
+    sums into the buffer's tail, one all-reduce of both, the fused Adam."""
+    flat = trainer.flat
+    flat.comm.zero_()
+    with torch.enable_grad():
+        pa, ta, ps = predict()
+        sq = (pa - ta) ** 2
+        ls = (ps - next_strain) ** 2
+        per = trainer.w_pos * sq.sum(-1) + trainer.w_strain * ls
+        (per.sum() / n_global).backward()   # AccumulateGrad adds into the flat gradient views
+    with torch.no_grad():
+        d = sq.shape[1]
+        flat.loss[0] = per.sum()
+        flat.loss[1:1 + d] = sq.sum(0)
+        flat.loss[4] = ls.sum()
+    trainer.dp.allreduce_(flat.comm)
+    trainer.opt.step()
 
 
 # ---------------------------------------------------------------------------
@@ -408,32 +449,3 @@ def train(simulator, metadata: dict, device, config: dict, group=None, log_every
         checkpoint_utils.save_train_state(str(save_dir / f"train_state-final-{trainer.step:06}.pt"),
                                           trainer.opt.state_dict(), trainer.step)
     return {"step": trainer.step, "lowest_eval_loss": lowest, "history": history, "trainer": trainer}
-
-
-def main(argv=None) -> None:
-    """train.py:494-552 without wandb: --config, --mode, --model_file."""
-    import argparse
-    import os
-    from . import data
-    ap = argparse.ArgumentParser(description="Single-scale GNN training (MI355X)")
-    ap.add_argument("--config", required=True)
-    ap.add_argument("--mode", choices=["train", "valid", "rollout"])
-    ap.add_argument("--model_file")
-    args = ap.parse_args(argv)
-    config = load_config(args.config)
-    if args.mode:
-        config["mode"] = args.mode
-    if args.model_file:
-        config["model_file"] = args.model_file
-    device = torch.device("cuda")
-    metadata = data.read_metadata(config["data_path"])
-    sim = _get_simulator(metadata, config["noise_std"], config["noise_std"], device, config).to(device)
-    if config["mode"] == "train":
-        train(sim, metadata, device, config)
-    else:
-        losses = predict(sim, metadata, device, config)
-        print(f"Mean loss: {sum(losses) / max(len(losses), 1):.6f}")
-
-
-if __name__ == "__main__":
-    main()

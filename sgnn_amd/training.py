@@ -364,14 +364,12 @@ def _saves(h=None, yhat=None, rstd=None, agg=None, hd=None, h2=None, hd2=None) -
     return SgnnSaves(h=p(h), yhat=p(yhat), rstd=p(rstd), agg=p(agg), hd=p(hd), h2=p(h2), hd2=p(hd2))
 
 
-def check_trainable(epd: nn.Module, nparticle_types: int) -> None:
-    if epd.latent_dim not in (64, 128) or getattr(epd, "mlp_hidden_dim", epd.latent_dim) != epd.latent_dim:
-        raise NotImplementedError("HIP training path: latent_dim = mlp_hidden_dim in {64, 128} (other widths "
-                                  "run inference only, on the width-generic kernels)")
-    if epd.nmlp_layers not in (1, 2):
-        raise NotImplementedError("HIP training path: nmlp_layers must be 1 or 2")
-    if nparticle_types > MAX_TYPES:
-        raise NotImplementedError(f"HIP training path: at most {MAX_TYPES} particle types")
+def fused_trainable(epd: nn.Module, nparticle_types: int) -> bool:
+    """The fused training kernels implement this model (hidden = latent in {64, 128},
+    nmlp_layers 1 or 2, the encoder widths they tile, <= 256 particle types); every
+    other shape trains on the differentiable width-generic path (sgnn_amd.autograd)."""
+    from . import generic
+    return generic.fast_shapes(epd) and nparticle_types <= MAX_TYPES
 
 
 class _Timer:

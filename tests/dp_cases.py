@@ -49,7 +49,7 @@ def _result(tr, losses):
             "param": tr.flat.param.detach().cpu().clone()}
 
 
-def run_single_scale(graph_ids, overlap=False):
+def run_single_scale(graph_ids, overlap=False, force=False):
     """STEPS Trainer steps on the concatenation of `graph_ids` (this process's
     share of the global batch); DP bookkeeping from the default process group.
     overlap: the per-layer gradient buckets go out asynchronously on the side
@@ -62,6 +62,7 @@ def run_single_scale(graph_ids, overlap=False):
     tr = Trainer(sim, lr_init=LR)
     if overlap:
         tr.dp.host_staging = False
+        tr.dp.force_overlap = force
         assert tr.dp.world == 1 or tr.dp.overlaps_buckets()
     wins = [_window(nx, ny, T_SS, 100 + g) for g, (nx, ny) in enumerate(SS_GRAPHS)]
     losses = []
@@ -102,5 +103,17 @@ def run_single_scale_overlap(graph_ids):
     return run_single_scale(graph_ids, overlap=True)
 
 
+def run_single_scale_rccl(graph_ids):
+    """The overlapped bucket path on a one-rank RCCL (nccl) group: every layer's bucket goes out
+    with dist.all_reduce(async_op=True) from the side stream during the backward, the launch stream
+    waits on the handles before Adam -- the C3 / C5 collective path on real RCCL."""
+    import torch.distributed as dist
+    if dist.is_initialized():
+        assert dist.get_backend() == "nccl"
+    return run_single_scale(graph_ids, overlap=True, force=dist.is_initialized())
+
+
 CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, MS_GRAPHS, MS_RANKS),
-         "ss_overlap": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS)}
+         "ss_overlap": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS),
+         "ss_rccl1": (run_single_scale_rccl, SS_GRAPHS, [[0, 1, 2]])}
+RCCL_CASES = {"ss_rccl1"}
