@@ -143,8 +143,9 @@ def test_multi_scale_gnn_on_explicit_features(case):
     z = golden(case)
     sim = ms_product_sim(z)
     t = lambda k: torch.from_numpy(z[k]).cuda()
-    pred = sim._multi_scale_gnn(t("node_features"), t("g2m"), t("ef_g2m"), t("m2m"), t("ef_m2m"), t("m2g"),
-                                t("ef_m2g"), None)
+    with torch.no_grad():   # inference: the fused chain (ms_engine.gnn_forward)
+        pred = sim._multi_scale_gnn(t("node_features"), t("g2m"), t("ef_g2m"), t("m2m"), t("ef_m2m"), t("m2g"),
+                                    t("ef_m2g"), None)
     torch.cuda.synchronize()
     _close(pred.cpu().numpy(), z["pred"], what=f"{case} MultiScaleGNN.forward")
 

@@ -179,7 +179,8 @@ def test_encode_process_decode_on_explicit_features(case):
     z = golden(case)
     sim = product_sim(z)
     t = lambda k: torch.from_numpy(z[k]).cuda()
-    pred = sim._encode_process_decode(t("node_features"), t("edge_index"), t("edge_features"))
+    with torch.no_grad():   # inference: the fused chain (engine.epd_forward)
+        pred = sim._encode_process_decode(t("node_features"), t("edge_index"), t("edge_features"))
     torch.cuda.synchronize()
     _close(pred.cpu().numpy(), z["pred"], what=f"{case} EPD.forward")
 
@@ -197,11 +198,13 @@ def test_encode_process_decode_edgeless_and_shuffled():
     ei = torch.from_numpy(z["edge_index"])
     ef = torch.from_numpy(z["edge_features"])
     ref = O.encode_process_decode(state, nf, ei[:, :0], ef[:0], 5)
-    got = sim._encode_process_decode(nf.cuda(), ei[:, :0].cuda(), ef[:0].cuda())
-    _close(got.cpu().numpy(), ref.numpy(), what="edgeless EPD.forward")
     perm = torch.randperm(ei.shape[1], generator=torch.Generator().manual_seed(0))
-    got = sim._encode_process_decode(nf.cuda(), ei[:, perm].cuda(), ef[perm].cuda())
-    _close(got.cpu().numpy(), z["pred"], what="shuffled EPD.forward")
+    for grad in (False, True):   # the fused chain, then the differentiable path
+        with torch.set_grad_enabled(grad):
+            got = sim._encode_process_decode(nf.cuda(), ei[:, :0].cuda(), ef[:0].cuda())
+            _close(got.detach().cpu().numpy(), ref.numpy(), what=f"edgeless EPD.forward grad={grad}")
+            got = sim._encode_process_decode(nf.cuda(), ei[:, perm].cuda(), ef[perm].cuda())
+            _close(got.detach().cpu().numpy(), z["pred"], what=f"shuffled EPD.forward grad={grad}")
 
 
 @pytest.mark.parametrize("nsteps", [8, 9])
