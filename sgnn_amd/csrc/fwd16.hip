@@ -554,7 +554,10 @@ int radius_enc16_launch(const RadiusSmallArgs& r, const EncNode16Args& a, int nl
   // one workgroup per CU: at ~186 VGPRs (the encoder's resident weights) a CU holds one 8-wave
   // workgroup, so a grid past 256 would run a second round; the radius queries (cheap next to the
   // position staging every workgroup pays) take the CUs the encoder's 32-node pairs leave
-  const int egrid = (int)std::min<int64_t>((a.nd.n + 31) / 32, 64);
+#ifndef SGNN_MERGE_EGRID
+#define SGNN_MERGE_EGRID 128
+#endif
+  const int egrid = (int)std::min<int64_t>((a.nd.n + 31) / 32, SGNN_MERGE_EGRID);
   const int rgrid = (int)std::max<int64_t>(1, std::min<int64_t>((r.n + 7) / 8, 256 - egrid));
   const size_t lds = std::max(radius_small_lds(r.n, r.dim), sizeof(float) * 2 * kBufs * 16 * LDX);
   auto go = [&](auto kern) {

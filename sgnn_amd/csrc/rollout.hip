@@ -179,7 +179,10 @@ static int predict_impl(const sgnn_epd* m, const sgnn_step_in* in, const float* 
   // particles launch its search together with the node encoder (independent work, one launch whose
   // grid fits the 256 CUs once: C1 0.1275 -> 0.1239 ms/step; measured slower at 4,800 / 8,000
   // particles, 0.156 -> 0.167 / 0.217 -> 0.268, where the radius search needs more workgroups)
-  constexpr int64_t kMergeMaxN = 2560;
+#ifndef SGNN_MERGE_MAX_N
+#define SGNN_MERGE_MAX_N 8192
+#endif
+  constexpr int64_t kMergeMaxN = SGNN_MERGE_MAX_N;
   RadiusSmallArgs ra{};
   const bool small = n <= kMergeMaxN && radius_small_plan(pos_seq + (int64_t)(T - 1) * d, (int64_t)T * d, n, d, in->ex_ptr,
                                        in->n_ex, in->radius, in->K, 1, ws->radius_ws, ws->rowptr, ws->send,
