@@ -256,12 +256,12 @@ typedef struct sgnn_step_ws { /* device buffers of one (n, T, dim, H, K) shape *
   float *e0t, *x_a, *x_b, *u, *v, *agg, *cin, *cout;
   float *u2, *v2; /* [n][H] second node-half buffers: with both set, H = 64 and n <= 8192 each
                      layer runs as ONE sgnn_interaction_layer launch (u/v ping-pong); else two */
-  /* Optional, the one-launch step (hidden 64, nmlp_layers 1, n <= 4096, 2 <= nlayers <= 10):
+  /* Optional, the one-launch step (hidden 64, nmlp_layers 1, n <= 8192, 2 <= nlayers <= 10):
    * with all three set, a whole step is ONE kernel launch (radius graph, encoders, every layer,
    * decoder, integrator; sgnn_step_path() says whether it applies).  The radius graph then stays
    * in the kernel's LDS: rowptr/send/recv are not written, step_deg receives each receiver's
    * neighbour count. */
-  float* uvl;           /* nlayers*2*n*H + (n+16)*K*(H+4) floats: every layer's node halves u_k, v_k
+  float* uvl;           /* nlayers*2*n*H + (n+32)*K*(H+4) floats: every layer's node halves u_k, v_k
                            ([nlayers][2][n][H]), then room for the edge latents of tiles too large for
                            the kernel's LDS */
   uint32_t* step_flags; /* [512] per-workgroup phase counters + error word (zeroed per call) */

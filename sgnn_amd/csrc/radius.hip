@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kQBlock) void k_radius_query_lds(
     int32_t* nbr, int32_t* deg, int64_t n) {
   __shared__ f32x4 cand[kLdsCand];
   __shared__ int32_t cstart[9][kTX + 3];  // cell starts of each neighbour row's span (+ end)
-  __shared__ int32_t seg_base[9];
+  __shared__ int32_t seg_base[9 + 1];   // + the total
   __shared__ int32_t seg_g0[9];           // global index of each span's first candidate
   const Grid G = *reinterpret_cast<const Grid*>(bbox + 8);
   const int tiles_x = (G.g[0] + kTX - 1) / kTX;

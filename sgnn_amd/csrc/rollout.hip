@@ -31,7 +31,7 @@ int device_cus() {
 }
 
 // The one-launch step's arguments when it applies to this call (step16.hip):
-// hidden 64, nmlp_layers 1 everywhere, 2..10 layers, n <= 4096 particles, a
+// hidden 64, nmlp_layers 1 everywhere, 2..10 layers, n <= 8192 particles, a
 // grid of <= one workgroup per CU, and the kernel's LDS under 160 KB.
 bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq, const sgnn_step_ws* ws,
                  float* pred, float* next_pos, float* window_out, sgnn::Step16Args* out) {
@@ -69,16 +69,16 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   a.uvl = ws->uvl; a.flags = ws->step_flags; a.deg_out = ws->step_deg; a.nbr_out = nullptr;
   a.pos_seq = pos_seq; a.pred = pred; a.next_pos = next_pos; a.window_out = window_out;
   // receivers per workgroup: 8 up to 2,048 particles (C1: 250 workgroups), then as many as keep
-  // the grid at one workgroup per CU
+  // the grid at one workgroup per CU (up to 32: the Taylor bars' 4,800 / 6,400 / 8,000 at 19 / 25 / 32)
   const int64_t cus = std::min<int64_t>(device_cus(), kStep16MaxGrid);
   if (cus < 1) return false;
   a.nt = (int)std::max<int64_t>(8, (n + cus - 1) / cus);
   if (a.nt > kStep16MaxNT || (n + a.nt - 1) / a.nt > cus) return false;
   a.ecap_t = a.nt * cap;
-  a.e0_hbm = 0;
+  a.e0_hbm = a.nt > 16 ? 1 : 0;   // two node sub-tiles: their e0 rows live in HBM
   a.poll_limit = ws->step_poll_limit;
   size_t lds = step16_lds_bytes(a);
-  if (lds > kStep16MaxLds) {  // the tile's e0 rows do not fit in LDS: keep them in HBM (ws->uvl's tail)
+  if (lds > kStep16MaxLds && !a.e0_hbm) {  // the tile's e0 rows do not fit in LDS: keep them in HBM (ws->uvl's tail)
     a.e0_hbm = 1;
     lds = step16_lds_bytes(a);
   }

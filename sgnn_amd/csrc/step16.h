@@ -7,7 +7,7 @@
 namespace sgnn {
 
 constexpr int kStep16MaxL = 10;     // interaction layers carried in the kernel arguments
-constexpr int kStep16MaxNT = 16;    // receivers per workgroup (one 16-item node tile)
+constexpr int kStep16MaxNT = 32;    // receivers per workgroup (one or two 16-item node sub-tiles)
 constexpr int kStep16MaxCap = 64;   // neighbour cap (K, +1 without self loops)
 constexpr int kStep16MaxGrid = 256; // one workgroup per CU, every workgroup resident
 constexpr int kStep16MaxEx = 64;    // examples in the batch (their offsets are staged in LDS)

@@ -1,6 +1,7 @@
 // One whole LearnedSimulator.predict_positions (learned_simulator.py:413-438)
-// in ONE launch, for graphs of up to 4,096 particles at hidden 64 and
-// nmlp_layers 1 (the C1 headline: 2,000 particles, r = 15, L = 5):
+// in ONE launch, for graphs of up to 8,192 particles at hidden 64 and
+// nmlp_layers 1 (the C1 headline: 2,000 particles, r = 15, L = 5; the Taylor
+// bars' 4,800 / 6,400 / 8,000 with two 16-item node sub-tiles per workgroup):
 //   radius graph (torch_cluster.radius via radius_graph, :116-117)
 //   -> Encoder (graph_network.py:86-96, features :231-316)
 //   -> L x InteractionNetwork (graph_network.py:150-222, edge-latent doubling)
@@ -65,29 +66,37 @@ SGNN_DEV void st4_sc1(__amdgpu_buffer_rsrc_t rs, int voff, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff, 0, 16);
 }
 
-// LDS carve (floats), shared with the host's size query.
+// LDS carve (floats), shared with the host's size query.  A tile of nt <= 16 receivers is one 16-item
+// node sub-tile, nt <= 32 two (NSUB).
+constexpr int kMaxNT = sgnn::kStep16MaxNT;
 struct Carve {
   int sw0, sw1, svec, sxw, sxv, scratch, xs, dbuf, region, ints, total;  // float offsets / count
   int region_floats;
+  int list_cap;  // radius phase: candidate slots (4 waves x Q, Q = round64(n / 4) at most)
 };
 SGNN_HOST_DEV inline Carve carve(int n, int dim, int nt, int cap, bool e0g) {
   Carve c{};
+  const int nsub = (nt + 15) / 16;
   int o = 0;
   c.sw0 = o; o += H * LDX;        // edge W1e (x 2^k), LDS image [H][LDX]
   c.sw1 = o; o += H * LDX;        // edge W2
   c.svec = o; o += 4 * H;         // edge b2, gamma, beta
   c.sxw = o; o += H * LDX;        // Encoder.edge_fn W2
   c.sxv = o; o += 4 * H;          // Encoder.edge_fn b1, b2, gamma, beta
-  c.scratch = o; o += 4 * 16 * LDX;  // per-wave receiver sums; node-phase exchange buffers
-  c.xs = o; o += 16 * LDX;        // x rows of the tile's nodes (resident for the step)
+  c.scratch = o; o += 4 * 16 * nsub * LDX;  // per-wave receiver sums; node-phase exchange buffers
+  c.xs = o; o += 16 * nsub * LDX;  // x rows of the tile's nodes (resident for the step)
   c.dbuf = o; o += 2 * KQ * 64 * 4;  // donated pre-wait products (EdgePhase::plan)
-  const int e0f = e0g ? 0 : nt * cap * LDX, posf = n * dim;
-  c.region_floats = e0f > posf ? e0f : posf;  // positions (radius phase), then e0 rows (unless in HBM)
+  // the radius phase's candidate list ([dim][list_cap] positions + [list_cap] ids) overlays everything
+  // before `ints` (nothing else there is live yet); the region after dbuf holds the e0 rows (unless in HBM)
+  c.list_cap = 4 * ((((n + 3) / 4) + 63) & ~63);
+  const int e0f = e0g ? 0 : nt * cap * LDX, listf = (dim + 1) * c.list_cap - o;
+  c.region_floats = e0f > listf ? e0f : (listf > 0 ? listf : 0);
   c.region = o; o += (c.region_floats + 3) & ~3;
-  // lsend, lrecv [round16(nt*cap)] each, nbr [nt*cap]; deg [16]; pre [20]; mask [8]; kw [4][64]; deps [256] + count;
-  // example offsets [kStep16MaxEx + 1]
+  // lsend, lrecv [round16(nt*cap)] each, nbr [nt*cap]; deg [32]; pre [36]; mask [8]; kw [4][64]; deps [256] +
+  // count; example offsets [kStep16MaxEx + 1]; receiver positions [3][32]; box [8]; segment counts [4]
   c.ints = o;
-  o += 2 * ((nt * cap + 15) & ~15) + nt * cap + 16 + 20 + 8 + 4 * 64 + sgnn::kStep16MaxGrid + 4 + sgnn::kStep16MaxEx + 4;
+  o += 2 * ((nt * cap + 15) & ~15) + nt * cap + kMaxNT + kMaxNT + 4 + 8 + 4 * 64 + sgnn::kStep16MaxGrid + 4 +
+       sgnn::kStep16MaxEx + 4 + 3 * kMaxNT + 8 + 4;
   c.total = (o + 3) & ~3;
   return c;
 }
@@ -265,10 +274,14 @@ struct EdgeVec {
 // The LayerNorm + receiver sums of one half's y in four parts: 0 means, 1 deviations + variances,
 // 2 scales + incidence + messages, 3 the 16 aggregation MFMAs.  (Interleaving them with the next
 // half's MFMAs gains nothing: f32 MFMA occupies most of the SIMD's VALU, tools/exp/mfma_valu_overlap.hip.)
+// With two node sub-tiles (NSUB 2: receivers i0 .. i0 + 31) the incidence has a block per sub-tile, and a
+// half runs the MFMAs of the blocks its receivers hit (one, or two for the half that straddles).
+template <int NSUB>
 struct LnAgg {
   f32x4 d[KQ], mu, var;
-  float sb[4];
-  SGNN_DEV void part(int p, const f32x4 (&y)[KQ], f32x4 (&agg)[KQ], const EdgeVec& ev, const int32_t* lrecv,
+  float sb[NSUB][4];
+  bool hit[NSUB];
+  SGNN_DEV void part(int p, const f32x4 (&y)[KQ], f32x4 (&agg)[NSUB][KQ], const EdgeVec& ev, const int32_t* lrecv,
                      int hs, int Et, int i0, int j, int g) {
     if (p == 0) {  // two-pass statistics per edge 4 g + c (torch: biased variance, eps 1e-5)
       mu = (y[0] + y[1]) + (y[2] + y[3]);
@@ -291,14 +304,22 @@ struct LnAgg {
       typedef int i32x4 __attribute__((ext_vector_type(4)));
       const i32x4 rv = *reinterpret_cast<const i32x4*>(lrecv + hs + 4 * g);
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) sb[s2] = (hs + 4 * g + s2 < Et && rv[s2] - i0 == j) ? 1.0f : 0.0f;
+      for (int s = 0; s < NSUB; ++s) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) sb[s][s2] = (hs + 4 * g + s2 < Et && rv[s2] - i0 - 16 * s == j) ? 1.0f : 0.0f;
+        if constexpr (NSUB > 1) hit[s] = __ballot(sb[s][0] + sb[s][1] + sb[s][2] + sb[s][3] != 0.0f) != 0ull;
+      }
 #pragma unroll
       for (int t = 0; t < KQ; ++t) d[t] = d[t] * rs * ev.ga[t] + ev.be[t];  // m (A: lane (unit j, k = g))
     } else {
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2)  // the four accumulators in turn: no dependent back-to-back MFMAs
+      for (int s = 0; s < NSUB; ++s) {
+        if (NSUB > 1 && !hit[s]) continue;
 #pragma unroll
-        for (int t = 0; t < KQ; ++t) agg[t] = mfma16(d[t][s2], sb[s2], agg[t]);
+        for (int s2 = 0; s2 < 4; ++s2)  // the four accumulators in turn: no dependent back-to-back MFMAs
+#pragma unroll
+          for (int t = 0; t < KQ; ++t) agg[s][t] = mfma16(d[t][s2], sb[s][s2], agg[s][t]);
+      }
     }
   }
 };
@@ -340,6 +361,7 @@ static_assert(kPubAt >= 1 && kPubAt <= kPre, "publish point within the pre-wait,
 // Encoder.edge_fn for every half and keeps the e0 rows), and `postwait` adds the
 // gathered u / v rows, runs the last Linear + LayerNorm and the receiver sums
 // (half_agg, on the matrix cores).
+template <int NSUB>
 struct EdgePhase {
   const Step16Args& a;
   const float *sw0, *sw1, *svec, *sxw, *sxv;
@@ -495,9 +517,11 @@ struct EdgePhase {
   // after the wait: + u[recv] + v[send], ReLU, last Linear, LayerNorm, receiver sums (half_agg);
   // the wave's receiver aggregates are stored to its rows of `sums` at the end
   SGNN_DEV void postwait(__amdgpu_buffer_rsrc_t ru, __amdgpu_buffer_rsrc_t rv, bool probe = false) {
-    f32x4 agg[KQ];
+    f32x4 agg[NSUB][KQ];
 #pragma unroll
-    for (int t = 0; t < KQ; ++t) agg[t] = zero4();
+    for (int s = 0; s < NSUB; ++s)
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) agg[s][t] = zero4();
     // the raw u / v rows of the next half stay in flight across the current half's MFMAs: summing them
     // here would put a wait for the loads just issued in front of those MFMAs
     f32x4 gu[KQ], gv[KQ];
@@ -519,7 +543,7 @@ struct EdgePhase {
       ev.ga[t] = svec[H + 16 * t + j];
       ev.be[t] = svec[2 * H + 16 * t + j];
     }
-    LnAgg la;
+    LnAgg<NSUB> la;
     auto finish = [&](const f32x4 (&acc)[KQ], int hs) {  // ReLU -> last Linear -> LayerNorm -> sums
       f32x4 x[KQ], y[KQ];
       lin2_init(acc, x, y, ev);
@@ -563,7 +587,9 @@ struct EdgePhase {
       finish(acc, hs);
     }
 #pragma unroll
-    for (int t = 0; t < KQ; ++t) st4(sums + j * LDX + 16 * t + 4 * g, agg[t]);
+    for (int s = 0; s < NSUB; ++s)
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) st4(sums + (16 * s + j) * LDX + 16 * t + 4 * g, agg[s][t]);
   }
 };
 
@@ -631,7 +657,7 @@ SGNN_DEV Node16Args node_args(const Step16Args& a, const Lay16& L, const Lay16* 
 // One interaction layer of the tile: wait for the sender tiles' u_k / v_k,
 // edge phase, receiver sums, node phase, publish u_{k+1} / v_{k+1}, stage the
 // next layer's edge weights.
-template <bool FIRST, int MODE, bool E0G>
+template <bool FIRST, int MODE, bool E0G, int NSUB>
 SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv, const float (&xw1)[KQ],
                          const int32_t* deps, int ndeps, const int32_t* lsend, const int32_t* lrecv, int Et, int i0,
                          int cnt, int b, int j, int g, int l) {
@@ -654,8 +680,8 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   mark(ps);
   NodeW<2, MODE> W;
   const Node16Args nd = node_args(a, Lk, MODE == 0 ? &Ln : nullptr);
-  float* sums = scratch + b * 16 * LDX;
-  EdgePhase ep{a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, sums, e0l, lsend, lrecv, Et, i0, b, j, g, l};
+  float* sums = scratch + b * 16 * NSUB * LDX;
+  EdgePhase<NSUB> ep{a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, sums, e0l, lsend, lrecv, Et, i0, b, j, g, l};
   mark(ps < 0 ? -1 : ps + 1);
   // Between the pre-wait products: publish phase k + 1 (u_k / v_k, stored by the previous stage; the
   // drain of those write-through stores overlaps the first product), then request this layer's node
@@ -685,38 +711,58 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   // the next layer's edge weights: requested now, staged in LDS before this layer publishes
   EdgeStage nxt;
   if (MODE == 0) nxt.load(Ln);
-  f32x4 ag[KQ];
+  // receiver sums of sub-tile s: the four waves' partial rows 16 s + j of their blocks
+  constexpr int kWaveRows = 16 * NSUB;
+  auto sum_rows = [&](f32x4 (&ag)[KQ], int s) {
 #pragma unroll
-  for (int q = 0; q < KQ; ++q) {
-    ag[q] = ld4(scratch + j * LDX + 16 * q + 4 * g);
+    for (int q = 0; q < KQ; ++q) {
+      ag[q] = ld4(scratch + (16 * s + j) * LDX + 16 * q + 4 * g);
 #pragma unroll
-    for (int w = 1; w < kWaves16; ++w) ag[q] += ld4(scratch + w * 16 * LDX + j * LDX + 16 * q + 4 * g);
-  }
-  f32x4 xr[KQ];
+      for (int w = 1; w < kWaves16; ++w) ag[q] += ld4(scratch + (w * kWaveRows + 16 * s + j) * LDX + 16 * q + 4 * g);
+    }
+  };
+  f32x4 ag[KQ], xr[KQ];
+  sum_rows(ag, 0);
 #pragma unroll
   for (int q = 0; q < KQ; ++q) xr[q] = ld4(xs + j * LDX + 16 * q + 4 * g);
-  const f32x4 xo = ld4(xs + j * LDX + 16 * b + 4 * g);
+  f32x4 xo = ld4(xs + j * LDX + 16 * b + 4 * g);
+  // sub-tile 1's sums move to rows the exchange buffers (rows 0 .. 47) leave alone: wave 3's block
+  float* ag1 = scratch + 3 * kWaveRows * LDX;
+  if constexpr (NSUB > 1) {
+    f32x4 t1[KQ];
+    sum_rows(t1, 1);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) st4(ag1 + j * LDX + 16 * q + 4 * g, t1[q]);
+  }
   __syncthreads();  // the exchange buffers alias the sums
   if (k == 1) mark(52);
-  const bool valid = j < cnt;
-  const int64_t i = i0 + j;
-  const f32x4 h = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));  // graph_network.py:220
-  if (k == 1) mark(53);
+  // u_{k+1} / v_{k+1} (mode 0); the decoder needs none
+  const __amdgpu_buffer_rsrc_t ru1 = buf_rsrc(a.uvl + (MODE == 0 ? 2 * k + 2 : 0) * nH),
+                               rv1 = buf_rsrc(a.uvl + (MODE == 0 ? 2 * k + 3 : 0) * nH);
+#pragma unroll
+  for (int s = 0; s < NSUB; ++s) {
+    if (s > 0) {  // (sub-tile 1's rows: written by no exchange of sub-tile 0)
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        ag[q] = ld4(ag1 + j * LDX + 16 * q + 4 * g);
+        xr[q] = ld4(xs + (16 * s + j) * LDX + 16 * q + 4 * g);
+      }
+      xo = ld4(xs + (16 * s + j) * LDX + 16 * b + 4 * g);
+    }
+    const f32x4 h = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));  // graph_network.py:220
+    if (k == 1 && s == 0) mark(53);
+    step_tail<MODE>(a, W, scratch, xs + 16 * s * LDX, i0 + 16 * s + j, 16 * s + j < cnt, h, xo, b, j, g, ru1, rv1);
+  }
+  mark(ps < 0 ? -1 : ps + 6);
   if constexpr (MODE == 0) {
-    const __amdgpu_buffer_rsrc_t ru1 = buf_rsrc(a.uvl + (2 * k + 2) * nH), rv1 = buf_rsrc(a.uvl + (2 * k + 3) * nH);
-    step_tail<0>(a, W, scratch, xs, i, valid, h, xo, b, j, g, ru1, rv1);
-    mark(ps < 0 ? -1 : ps + 6);
     nxt.store(sw0, sw1, svec, (float)(2 << k));  // W1e x 2^(k+1): exact
     __syncthreads();  // the next layer's pre-wait reads the staged weights; it publishes u_{k+1} / v_{k+1}
-    mark(ps < 0 ? -1 : ps + 7);
-  } else {
-    step_tail<1>(a, W, scratch, xs, i, valid, h, xo, b, j, g, ru, rv);
-    mark(ps < 0 ? -1 : ps + 6);
-    mark(ps < 0 ? -1 : ps + 7);
   }
+  mark(ps < 0 ? -1 : ps + 7);
 }
 
-template <int DIM, int KQF, bool E0G>
+template <int DIM, int KQF, bool E0G, int NSUB>
 __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) void k_step16(Step16Args a_) {
   // every access through the kernel-argument segment itself (scalar loads): binding a reference to
   // the by-value parameter would copy its 1.3 KB to scratch first
@@ -734,72 +780,93 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   int32_t* lrecv = lsend + ((nt * cap + 15) & ~15);   // 16-B aligned rows: half_agg reads int4s
   int32_t* nbr_l = lrecv + ((nt * cap + 15) & ~15);
   int32_t* ldeg = nbr_l + nt * cap;
-  int32_t* lpre = ldeg + 16;
-  uint32_t* mask = reinterpret_cast<uint32_t*>(lpre + 20);
+  int32_t* lpre = ldeg + kMaxNT;
+  uint32_t* mask = reinterpret_cast<uint32_t*>(lpre + kMaxNT + 4);
   int32_t* kw_all = reinterpret_cast<int32_t*>(mask + 8);
   int32_t* deps = kw_all + 4 * 64;       // the sender tiles of this tile's edges, compacted
   int32_t* ndeps_l = deps + kMaxGrid;
   int32_t* exs = ndeps_l + 4;            // example offsets (ex_ptr)
+  float* rp = reinterpret_cast<float*>(exs + sgnn::kStep16MaxEx + 4);  // [3][32] the tile's receivers' positions
+  float* box = rp + 3 * kMaxNT;          // the receivers' bounding box grown by the margin: lo [3], hi [3]
+  int32_t* segn = reinterpret_cast<int32_t*>(box + 8);  // kept candidates per wave segment
 
   mark(0);
   if (threadIdx.x < 8) mask[threadIdx.x] = 0u;
 
   // ---- radius graph of the tile's receivers (torch_cluster's rule: first `cap` in-range senders of
   // the receiver's example in ascending index, strict <; learned_simulator.py:116-117) --------------
-  float* sp = lds + cv.region;  // [DIM][n] SoA
   // the tile's node features (learned_simulator.py:256-290): their raw inputs are requested first and
   // combined after the radius search, so the loads complete under it
-  const int64_t ic = j < cnt ? (int64_t)(i0 + j) : (int64_t)i0;
   const int nvel = (a.T - 1) * DIM;
-  float fr0[KQF][4], fr1[KQF][4], vmean[DIM], vstd[DIM];
-  {
-    const float* p = a.pos_seq + ic * a.T * DIM;
+  float fr0[NSUB][KQF][4], fr1[NSUB][KQF][4], vmean[DIM], vstd[DIM];
+  int64_t ptype[NSUB];
 #pragma unroll
-    for (int d = 0; d < DIM; ++d) {
-      vmean[d] = a.vel_mean[d];
-      vstd[d] = a.vel_std[d];
-    }
+  for (int d = 0; d < DIM; ++d) {
+    vmean[d] = a.vel_mean[d];
+    vstd[d] = a.vel_std[d];
+  }
+#pragma unroll
+  for (int s = 0; s < NSUB; ++s) {
+    const int64_t ic = 16 * s + j < cnt ? (int64_t)(i0 + 16 * s + j) : (int64_t)i0;
+    const float* p = a.pos_seq + ic * a.T * DIM;
 #pragma unroll
     for (int q = 0; q < KQF; ++q)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int f = 16 * q + 4 * g + c, t = f / DIM, cc = f - t * DIM;
-        fr0[q][c] = f < nvel ? p[(t + 1) * DIM + cc] : f == nvel ? p[(a.T - 1) * DIM] : 0.0f;
-        fr1[q][c] = f < nvel ? p[t * DIM + cc] : 0.0f;
+        fr0[s][q][c] = f < nvel ? p[(t + 1) * DIM + cc] : f == nvel ? p[(a.T - 1) * DIM] : 0.0f;
+        fr1[s][q][c] = f < nvel ? p[t * DIM + cc] : 0.0f;
       }
+    ptype[s] = a.use_emb ? a.types[ic] : 0;
   }
-  const int64_t ptype = a.use_emb ? a.types[ic] : 0;
-  {  // the window's last frame (or the previous step's contiguous next_pos), 16 loads in flight per thread
-    // (one load path: a branch per load would put a wait in each), then the example offsets
-    const float* src = a.pos_last ? a.pos_last : a.pos_seq + (int64_t)(a.T - 1) * DIM;
-    const int stride = a.pos_last ? DIM : a.T * DIM;
-    const int n_ex = a.n_ex;
+  // the window's last frame (or the previous step's contiguous next_pos)
+  const float* src = a.pos_last ? a.pos_last : a.pos_seq + (int64_t)(a.T - 1) * DIM;
+  const int pstride = a.pos_last ? DIM : a.T * DIM;
+  const int n_ex = a.n_ex;
+  {  // example offsets; wave 0: the receivers' positions and their bounding box, grown by the margin
     const int64_t exv = (int)threadIdx.x <= n_ex ? a.ex_ptr[threadIdx.x] : 0;
-    constexpr int kPosBatch = 16;
-    for (int t0 = threadIdx.x; t0 < n * DIM; t0 += kBlock16 * kPosBatch) {
-      float v[kPosBatch];
+    if (b == 0) {
+      float lo[DIM], hi[DIM];
 #pragma unroll
-      for (int u = 0; u < kPosBatch; ++u) {
-        const int t = min(t0 + u * kBlock16, n * DIM - 1), i = t / DIM, d = t - i * DIM;
-        v[u] = src[(int64_t)i * stride + d];
+      for (int d = 0; d < DIM; ++d) {
+        const float v = src[(int64_t)(i0 + min(l, cnt - 1)) * pstride + d];
+        if (l < cnt) rp[d * kMaxNT + l] = v;
+        lo[d] = v;
+        hi[d] = v;
       }
 #pragma unroll
-      for (int u = 0; u < kPosBatch; ++u) {
-        const int t = t0 + u * kBlock16, i = t / DIM, d = t - i * DIM;
-        if (t < n * DIM) sp[d * n + i] = v[u];
-      }
+      for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) {
+          lo[d] = fminf(lo[d], __shfl_xor(lo[d], o, 64));
+          hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], o, 64));
+        }
+      // |p_j - p_i|^2 < r^2 in fp32 implies |p_j,d - p_i,d| < r (1 + 2^-22) + one ulp of the coordinates:
+      // 1e-3 r + 1e-6 |p| covers both with room (a wider box only keeps more candidates; radius_small.h)
+      float mag = 0.0f;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) mag = fmaxf(mag, fmaxf(fabsf(lo[d]), fabsf(hi[d])));
+      const float m = 1.001f * a.radius + 1e-6f * (mag + 1.0f);
+      if (l == 0)
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) {
+          box[d] = lo[d] - m;
+          box[3 + d] = hi[d] + m;
+        }
     }
     if ((int)threadIdx.x <= n_ex) exs[threadIdx.x] = (int32_t)exv;
   }
 
   if (a.use_emb) {  // :287-290 type embedding
 #pragma unroll
-    for (int q = 0; q < KQF; ++q)
+    for (int s = 0; s < NSUB; ++s)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int f = 16 * q + 4 * g + c;
-        if (f > nvel && f < nvel + 1 + a.emb_dim) fr0[q][c] = a.emb_w[ptype * a.emb_dim + (f - nvel - 1)];
-      }
+      for (int q = 0; q < KQF; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int f = 16 * q + 4 * g + c;
+          if (f > nvel && f < nvel + 1 + a.emb_dim) fr0[s][q][c] = a.emb_w[ptype[s] * a.emb_dim + (f - nvel - 1)];
+        }
   }
   // weights of layer 0's edge MLP and of Encoder.edge_fn (LDS images after the radius search), issued after
   // the positions (loads complete in order) and in flight during the radius queries; Encoder.node_fn's
@@ -829,49 +896,105 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     vb1 = ld4(a.xn_b1 + 16 * b + 4 * g);
   };
   __syncthreads();
-  mark(56);  // probe: positions staged
+  // the candidates: the examples of the tile's receivers, [jb, je), kept when inside the box.  Wave w
+  // filters the contiguous quarter [jb + w Q, jb + (w + 1) Q) into its own segment of the list, so the
+  // segments in order are ascending in index (the scan below takes them in order).
+  float* cp = lds;                                                   // [DIM][list_cap] positions
+  int32_t* cid = reinterpret_cast<int32_t*>(lds + DIM * cv.list_cap);  // [list_cap] indices
+  auto example_of = [&](int i) {  // largest e with ex_ptr[e] <= i
+    int lo = 0, hi = n_ex - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (exs[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  const int cjb = exs[example_of(i0)], cje = exs[example_of(i0 + cnt - 1) + 1];
+  const int Q = (((cje - cjb + 3) >> 2) + 63) & ~63;
+  {
+    float blo[DIM], bhi[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
+      blo[d] = box[d];
+      bhi[d] = box[3 + d];
+    }
+    const int s0 = cjb + b * Q, s1 = min(s0 + Q, cje);
+    int kept = 0;
+    constexpr int kBatch = 8;  // 64-candidate chunks whose loads are in flight together
+    for (int base = s0; base < s1; base += 64 * kBatch) {
+      float pc[kBatch][DIM];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        const int jj = min(base + 64 * u + l, s1 - 1);
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) pc[u][d] = src[(int64_t)jj * pstride + d];
+      }
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        const int jj = base + 64 * u + l;
+        bool in = jj < s1;
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) in = in && pc[u][d] >= blo[d] && pc[u][d] <= bhi[d];
+        const uint64_t bal = __ballot(in);
+        if (in) {
+          const int slot = b * Q + kept + (int)__popcll(bal & ((1ull << l) - 1ull));
+          SGNN_BOUNDS(slot, 0, cv.list_cap, "step16 candidate slot");
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) cp[d * cv.list_cap + slot] = pc[u][d];
+          cid[slot] = jj;
+        }
+        kept += (int)__popcll(bal);
+      }
+    }
+    if (l == 0) segn[b] = kept;
+  }
+  __syncthreads();
+  mark(56);  // probe: candidates staged
   {
     int32_t* kw = kw_all + b * 64;
     const float r2 = a.r2;  // a local: the LDS stores below would make the compiler re-load the argument
-    const int loop = a.loop, n_ex = a.n_ex;
+    const int loop = a.loop;
+    int sn[kWaves16];
+#pragma unroll
+    for (int w = 0; w < kWaves16; ++w) sn[w] = segn[w];
     for (int rl = b; rl < cnt; rl += kWaves16) {
       const int i = i0 + rl;
-      int lo = 0, hi = n_ex - 1;  // example of i: largest e with ex_ptr[e] <= i
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (exs[mid] <= i) lo = mid; else hi = mid - 1;
-      }
-      const int jb = exs[lo], je = exs[lo + 1];
+      const int ex = example_of(i);
+      const int jb = exs[ex], je = exs[ex + 1];
       float pi[DIM];
 #pragma unroll
-      for (int d = 0; d < DIM; ++d) pi[d] = sp[d * n + i];
+      for (int d = 0; d < DIM; ++d) pi[d] = rp[d * kMaxNT + rl];
       int c = 0;
       // four 64-candidate chunks per round: their LDS reads are in flight together, then the chunks
       // are taken in index order (the first `cap` in range are kept; a round may test up to three
       // chunks past the cap, harmlessly)
       constexpr int kRound = 4;
-      for (int base = jb; base < je && c < cap; base += 64 * kRound) {
-        float pc[kRound][DIM];
+      for (int w = 0; w < kWaves16 && c < cap; ++w) {
+        const int wn = sn[w], wb = w * Q;
+        for (int base = 0; base < wn && c < cap; base += 64 * kRound) {
+          float pc[kRound][DIM];
+          int id[kRound];
 #pragma unroll
-        for (int u = 0; u < kRound; ++u) {
-          const int jj = min(base + 64 * u + l, je - 1);
+          for (int u = 0; u < kRound; ++u) {
+            const int kk = wb + min(base + 64 * u + l, wn - 1);
 #pragma unroll
-          for (int d = 0; d < DIM; ++d) pc[u][d] = sp[d * n + jj];
-        }
-#pragma unroll
-        for (int u = 0; u < kRound; ++u) {
-          const int jj = base + 64 * u + l;
-          float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
-#pragma unroll
-          for (int d = 0; d < DIM; ++d) {
-            const float t = __fsub_rn(pc[u][d], pi[d]);
-            s = __fadd_rn(s, __fmul_rn(t, t));
+            for (int d = 0; d < DIM; ++d) pc[u][d] = cp[d * cv.list_cap + kk];
+            id[u] = cid[kk];
           }
-          const bool in = jj < je && s < r2;
-          const uint64_t bal = __ballot(in);
-          const int slot = c + (int)__popcll(bal & ((1ull << l) - 1ull));
-          if (in && slot < cap) kw[slot] = jj;
-          c += (int)__popcll(bal);
+#pragma unroll
+          for (int u = 0; u < kRound; ++u) {
+            float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
+#pragma unroll
+            for (int d = 0; d < DIM; ++d) {
+              const float t = __fsub_rn(pc[u][d], pi[d]);
+              s = __fadd_rn(s, __fmul_rn(t, t));
+            }
+            const bool in = base + 64 * u + l < wn && id[u] >= jb && id[u] < je && s < r2;
+            const uint64_t bal = __ballot(in);
+            const int slot = c + (int)__popcll(bal & ((1ull << l) - 1ull));
+            if (in && slot < cap) kw[slot] = id[u];
+            c += (int)__popcll(bal);
+          }
         }
       }
       wave_lds_sync();
@@ -891,9 +1014,10 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
       wave_lds_sync();
     }
   }
+  __syncthreads();  // the candidate list overlays the weights' LDS images
   mark(1);
   load_encoder();
-  // LDS images of the staged weights (the radius phase never touches them)
+  // LDS images of the staged weights (requested before the radius phase)
   st0.store(lds + cv.sw0, lds + cv.sw1, lds + cv.svec, 1.0f);
   stage_w64_store(lds + cv.sxw, sx, 1.0f);
   sxv.store(lds + cv.sxv, 4);
@@ -904,11 +1028,11 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     const int dg = l < cnt ? ldeg[l] : 0;
     int incl = dg;
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
+    for (int o = 1; o < kMaxNT; o <<= 1) {
       const int t = __shfl_up(incl, o, 64);
       if (l >= o) incl += t;
     }
-    if (l < 16) lpre[l + 1] = incl;
+    if (l < kMaxNT) lpre[l + 1] = incl;
     if (l == 0) lpre[0] = 0;
     if (a.deg_out && l < cnt) a.deg_out[i0 + l] = dg;
   }
@@ -951,16 +1075,15 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   float xw1[KQ] = {0.0f, 0.0f, 0.0f, 0.0f};  // Encoder.edge_fn W1 [H][dim + 1]: unit 16 t + j, k = g
 #pragma unroll
   for (int t = 0; t < KQ; ++t) xw1[t] = g <= DIM ? a.xe_w1[(16 * t + j) * (DIM + 1) + g] : 0.0f;
-  {
-    const int64_t i = i0 + j;
-    const bool valid = j < cnt;
+#pragma unroll
+  for (int s = 0; s < NSUB; ++s) {
     f32x4 xf[KQF];
 #pragma unroll
     for (int q = 0; q < KQF; ++q)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int f = 16 * q + 4 * g + c, t = f / DIM, cc = f - t * DIM;
-        float val = fr0[q][c];  // embedding, or 0 past the features
+        float val = fr0[s][q][c];  // embedding, or 0 past the features
         if (f < nvel) {  // learned_simulator.py:258,272-278 normalised velocity history
           float mn = vmean[0], sd = vstd[0];
 #pragma unroll
@@ -969,25 +1092,25 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
               mn = vmean[d];
               sd = vstd[d];
             }
-          val = __fdiv_rn(__fsub_rn(__fsub_rn(fr0[q][c], fr1[q][c]), mn), sd);
+          val = __fdiv_rn(__fsub_rn(__fsub_rn(fr0[s][q][c], fr1[s][q][c]), mn), sd);
         } else if (f == nvel) {  // :282-284 wall distance
-          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(fr0[q][c], 2.0f), 0.0f), a.wall_max), a.wall_div);
+          val = __fdiv_rn(fminf(fmaxf(__fadd_rn(fr0[s][q][c], 2.0f), 0.0f), a.wall_max), a.wall_div);
         }
         xf[q][c] = val;
       }
     const f32x4 h = relu4(mm(vb1, w1f, xf));
     const int64_t nH = (int64_t)n * H;
-    step_tail<0>(a, E, lds + cv.scratch, lds + cv.xs, i, valid, h, zero4(), b, j, g, buf_rsrc(a.uvl),
-                 buf_rsrc(a.uvl + nH));
-    mark(2);  // u_0 / v_0 are published by layer 0's pre-wait
+    step_tail<0>(a, E, lds + cv.scratch, lds + cv.xs + 16 * s * LDX, i0 + 16 * s + j, 16 * s + j < cnt, h, zero4(),
+                 b, j, g, buf_rsrc(a.uvl), buf_rsrc(a.uvl + nH));
   }
+  mark(2);  // u_0 / v_0 are published by layer 0's pre-wait
 
   // ---- the interaction layers ------------------------------------------------------------------
   const int ndeps = *ndeps_l;
-  step_layer<true, 0, E0G>(a, 0, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+  step_layer<true, 0, E0G, NSUB>(a, 0, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
   for (int k = 1; k < a.L - 1; ++k)
-    step_layer<false, 0, E0G>(a, k, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
-  step_layer<false, 1, E0G>(a, a.L - 1, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+    step_layer<false, 0, E0G, NSUB>(a, k, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+  step_layer<false, 1, E0G, NSUB>(a, a.L - 1, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
 }
 
 }  // namespace
@@ -1006,16 +1129,22 @@ using Step16Kernel = void (*)(Step16Args);
 Step16Kernel step16_kernel(const Step16Args& a) {
   const int kqf = (a.feat + 15) / 16;
   if (kqf < 1 || kqf > 3 || a.dim < 1 || a.dim > 3) return nullptr;
-#define SGNN_S16(D_, G_) \
-  return kqf == 1 ? k_step16<D_, 1, G_> : kqf == 2 ? k_step16<D_, 2, G_> : k_step16<D_, 3, G_>
-  if (a.e0_hbm) {
-    if (a.dim == 1) SGNN_S16(1, true);
-    if (a.dim == 2) SGNN_S16(2, true);
-    SGNN_S16(3, true);
+#define SGNN_S16(D_, G_, S_) \
+  return kqf == 1 ? k_step16<D_, 1, G_, S_> : kqf == 2 ? k_step16<D_, 2, G_, S_> : k_step16<D_, 3, G_, S_>
+  if (a.nt > 16) {  // two node sub-tiles: the tile's e0 rows never fit next to them
+    if (!a.e0_hbm) return nullptr;
+    if (a.dim == 1) SGNN_S16(1, true, 2);
+    if (a.dim == 2) SGNN_S16(2, true, 2);
+    SGNN_S16(3, true, 2);
   }
-  if (a.dim == 1) SGNN_S16(1, false);
-  if (a.dim == 2) SGNN_S16(2, false);
-  SGNN_S16(3, false);
+  if (a.e0_hbm) {
+    if (a.dim == 1) SGNN_S16(1, true, 1);
+    if (a.dim == 2) SGNN_S16(2, true, 1);
+    SGNN_S16(3, true, 1);
+  }
+  if (a.dim == 1) SGNN_S16(1, false, 1);
+  if (a.dim == 2) SGNN_S16(2, false, 1);
+  SGNN_S16(3, false, 1);
 #undef SGNN_S16
 }
 

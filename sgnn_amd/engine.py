@@ -143,7 +143,7 @@ class StepWorkspace:
             return False
         n, H, K = self.n, self.H, self.K
         f32 = dict(dtype=torch.float32, device=self.device)
-        self.uvl = torch.empty(epd_struct.nlayers * 2 * n * H + (n + 16) * K * (H + 4), **f32)
+        self.uvl = torch.empty(epd_struct.nlayers * 2 * n * H + (n + 32) * K * (H + 4), **f32)
         self.step_flags = torch.zeros(512, dtype=torch.int32, device=self.device)
         self.step_deg = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.c.uvl, self.c.step_flags, self.c.step_deg = (self.uvl.data_ptr(), self.step_flags.data_ptr(),

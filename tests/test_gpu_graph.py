@@ -4,7 +4,7 @@ rollout at the C1 r = 15 shape).  The step is captured as two ping-pong steps
 (window A -> B -> A, the old runner's form) with torch.cuda.graph and replayed;
 every replay must reproduce the eager steps bit for bit -- the same kernels on
 the same inputs -- on each launch path the step has: the one-launch step
-(k_step16, n <= 4,096), the per-layer fused kernels (4,096 < n <= 8,192) and the
+(k_step16, n <= 8,192), the per-layer fused kernels (its fallback, n <= 8,192) and the
 general edge/node kernels with the cell-list radius graph (larger n).  A stale
 host-side plan or an out-of-range read that eager execution happens to survive
 shows up here as a mismatch or a fault."""
@@ -22,7 +22,8 @@ def _sim(n_dims, radius, dev):
 
 @pytest.mark.parametrize("dims,radius,path", [
     ((50, 40), 15.0, "one-launch"),      # C1 r = 15: the shape round 1 faulted at
-    ((80, 60), 0.6, "fused layers"),     # 4,800 particles
+    ((80, 60), 0.6, "one-launch"),       # 4,800 particles: two node sub-tiles per workgroup
+    ((80, 60), 0.6, "fused layers"),     # the same with the one-launch step off (its fallback)
     ((120, 100), 0.6, "edge/node"),      # 12,000 particles
 ])
 def test_graph_replay_matches_eager(dims, radius, path):
@@ -36,6 +37,8 @@ def test_graph_replay_matches_eager(dims, radius, path):
     types_ = torch.zeros(n, dtype=torch.long, device=dev)
     inp, use_emb = sim._step_inputs(w0, [n], types_)
     ws = sim._workspace(n, bench.T_SEQ, dev)
+    if path == "fused layers":
+        ws = engine.StepWorkspace(n, bench.T_SEQ, len(dims), 64, sim._max_num_neighbors, True, dev, one_launch=False)
     pk = engine.ParamPack.get(sim._encode_process_decode)
     one = engine.step_path(pk.epd, engine.step_in(inp, ws, radius, sim._particle_type_embedding.weight, use_emb),
                            ws)[0]

@@ -61,6 +61,11 @@ def test_one_launch_matches_golden_and_kernel_sequence(case):
     (3, (12, 10, 8), 0.75, 1, 1, 20),  # 3D
     (2, (64, 64), 0.6, 1, 1, 20),      # 4,096 particles: 16 receivers per workgroup, 256 workgroups
     (2, (9, 7), 2.0, 2, 1, 33),        # tiny grid (16 workgroups); cap 33 = torch_cluster's default
+    # two node sub-tiles per workgroup (e0 rows in HBM): the Taylor bars' 4,800 and 8,000 particles
+    (2, (120, 40), 0.6, 1, 1, 20),     # 19 receivers per workgroup, 253 workgroups
+    (2, (200, 40), 0.6, 1, 1, 20),     # 32 receivers per workgroup, 250 workgroups
+    (3, (16, 16, 12), 0.75, 2, 3, 20),  # 3D, 2 examples, type embeddings (47 node features), 24 per workgroup
+    (2, (90, 40), 15.0, 2, 1, 20),     # 7,200 particles, cap binds, 29 per workgroup
 ])
 def test_one_launch_against_oracle(dim, dims, radius, n_ex, ntypes, K):
     from oracle import sgnn_oracle as O
@@ -94,6 +99,11 @@ def test_one_launch_against_oracle(dim, dims, radius, n_ex, ntypes, K):
     _close(pred[:, -1].cpu().numpy(), ref_strain.numpy(), what=f"n={n} dim={dim} strain")
     scale = float(np.max(st["acceleration"]["std"]))
     _close(nxt.cpu().numpy(), ref_next.numpy(), atol=ATOL * scale, rtol=1e-6, what=f"n={n} next_pos")
+    # the kernel sequence the step falls back to (k_layer16 up to 8,192 particles) on the same inputs
+    pred0, nxt0, ws0, path0 = _run(sim, pos.cuda(), counts, types_.cuda(), False)
+    assert not path0[0] and ws0.num_edges() == ref_e
+    _close(pred0[:, -1].cpu().numpy(), ref_strain.numpy(), what=f"n={n} dim={dim} strain (kernel sequence)")
+    _close(nxt0.cpu().numpy(), ref_next.numpy(), atol=ATOL * scale, rtol=1e-6, what=f"n={n} next_pos (sequence)")
 
 
 def test_headline_rollout_20_steps_against_oracle():
@@ -152,3 +162,33 @@ def test_step_timeout_raises_and_recovers():
     nxt1, _ = sim.predict_positions(pos, [n], types_)
     assert not ws.step_timeout()
     assert torch.equal(nxt0, nxt1)
+
+
+def test_two_subtile_rollout_against_oracle():
+    """A rollout at a Taylor-bar size whose workgroups own two node sub-tiles
+    (6,400 particles, 25 receivers per workgroup): 5 autoregressive steps (the
+    later steps read the previous next_pos) vs the oracle's rollout."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import engine, synthetic
+    z = golden("c1_r15")
+    hp = hparams(z)
+    T, nsteps = hp["T"], 5
+    seq = synthetic.trajectory(synthetic.lattice_2d(160, 40), T + nsteps, seed=1001)
+    n = seq.shape[0]
+    sim = product_sim(z)
+    sim._connectivity_radius = 0.6
+    types_ = torch.zeros(n, dtype=torch.long, device="cuda")
+    runner = sim.rollout_runner(torch.from_numpy(seq[:, :T]).cuda(), [n], types_, nsteps)
+    pk = engine.ParamPack.get(sim._encode_process_decode)
+    path = engine.step_path(pk.epd, runner.sin, runner.ws)
+    assert path[0] and path[1] == 25, path
+    pos, strain = runner.run()
+    torch.cuda.synchronize()
+    assert not runner.ws.step_timeout()
+    osim = oracle_sim(z)
+    osim.radius = 0.6
+    ref_pos, ref_str = O.rollout(osim, torch.from_numpy(seq), torch.zeros(n, dtype=torch.long), n, nsteps, T)
+    scale = float(np.max(z["acc_std"]))
+    _close(pos.cpu().numpy(), ref_pos.numpy(), atol=2 * nsteps * ATOL * scale, rtol=1e-6,
+           what="6,400-particle 5-step rollout positions")
+    _close(strain.cpu().numpy(), ref_str.numpy(), atol=2 * nsteps * ATOL, what="6,400-particle rollout strain")
