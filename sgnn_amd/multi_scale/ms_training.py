@@ -8,8 +8,9 @@ Backward order (reverse of ms_engine.forward_step):
   block b = B-1 .. 0 (M2G, M2M L-1 .. 0, G2M):
      node_bwd(b) -> dagg, dx' ; edge_bwd(b) -> dU, dh rows, dE0[kind] ;
      uv_bwd(b) -> g = dL/dx_b
+     slab reduction of block b on the side stream (+ its all-reduce bucket under DP)
   grid encoder backward, three edge-encoder backwards (one per edge type)
-  slab reduction -> flat gradient
+  slab reduction of the encoders / head -> flat gradient
 The edge latent of M2M block k is 2^k e0_m2m, so dE0_m2m accumulates
 2^k W1e^T dh over the M2M blocks; g2m / m2g latents feed one block each.
 Sender-sorted transposes of the three static graphs are built once.
@@ -23,7 +24,7 @@ import torch
 
 from .. import _hip, engine
 from .._hip import check, lib, stream_ptr
-from ..train import DataParallel, device_random_walk_noise
+from ..train import DataParallel, block_buckets, device_random_walk_noise
 from ..training import (MAX_TYPES, MS_NSLAB, Adam, FlatParams, SlabArena, _saves, _Timer, emb_args,
                         embedding_backward, encode_nodes_backward, nslab_table, typed_embedding)
 from . import ms_engine
@@ -121,12 +122,24 @@ class MSTrainWorkspace:
         lay.enc_node(g, "grid_node_encoder.", self.emb_g if use_emb else None)
         for k in EDGE_TYPES:
             lay.enc_edge(g, f"{k}_edge_encoder.", KIND_SLOT[k])
-        prefixes = ["g2m_block."] + [f"m2m_blocks.{k}." for k in range(self.nb - 2)] + ["m2g_block."]
-        for b, p in enumerate(prefixes):
-            lay.interaction(g, p, b, self.scales[b], slot=b)
         lay.decoder(g, "prediction_head.", self.loss_out)
-        self._descs_dev, self._block_start, self._ndesc, self._nblocks = lay.upload(self.slabs.arena.device)
+        dev = self.slabs.arena.device
+        self._descs_dev, self._block_start, self._ndesc, self._nblocks = lay.upload(dev)
+        # one table per block, reduced on the side stream as soon as that block's backward is done
+        prefixes = ["g2m_block."] + [f"m2m_blocks.{k}." for k in range(self.nb - 2)] + ["m2g_block."]
+        self._reduce_block = []
+        for b, p in enumerate(prefixes):
+            lb = self.slabs.layout(self.H, self.nlin, self.feat, self.dim)
+            lb.interaction(g, p, b, self.scales[b], slot=b)
+            self._reduce_block.append(lb.upload(dev))
         self._descs_key = key
+
+    def side(self, device: torch.device):
+        """The side stream of the per-block slab reductions (and their all-reduce buckets) + events."""
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=device)
+            self._ev = {k: torch.cuda.Event() for k in ("g", "blocks")}
+        return self._side, self._ev
 
 
 def train_forward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grid_radius: float,
@@ -185,7 +198,10 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                    next_pos: Optional[torch.Tensor] = None, noise: Optional[torch.Tensor] = None,
                    next_strain: Optional[torch.Tensor] = None, w_pos: float = 1.0, w_strain: float = 1.0,
                    inv_count: float = 1.0, timers: Optional[dict] = None,
-                   emb_weight: Optional[torch.Tensor] = None, emb_grad: Optional[torch.Tensor] = None) -> None:
+                   emb_weight: Optional[torch.Tensor] = None, emb_grad: Optional[torch.Tensor] = None,
+                   block_done=None) -> None:
+    """block_done(b, side_stream), when given, is called as soon as block b's slab reduction is queued
+    on the side stream (its gradients are final there): the trainer's all-reduce bucket for it."""
     L = lib()
     pk = ms_engine.ParamPack.get(gnn)
     use_emb = emb_weight is not None and inp.types is not None
@@ -201,6 +217,8 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                                   ctypes.byref(_saves(hd=tw.hd, hd2=tw.hd2)), tw.xs[tw.nb].data_ptr(),
                                   ctypes.byref(pk.head), tw.g.data_ptr(), tw.slab(_hip.SLAB_DECODER),
                                   ns[_hip.SLAB_DECODER], s), "sgnn_decoder_loss_bwd")
+    side, ev = tw.side(inp.pos_seq.device)
+    main = torch.cuda.current_stream(inp.pos_seq.device)
     seen = set()
     for b in range(tw.nb - 1, -1, -1):
         kind = tw.kinds[b]
@@ -226,6 +244,15 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                             tw.tperm[kind].data_ptr(), tw.xs[b].data_ptr(), n, ctypes.byref(pk.edge[b]),
                             tw.g.data_ptr(), tw.slab(_hip.SLAB_UV, b), ns[_hip.SLAB_UV],
                             tw.scratch.data_ptr(), s), "sgnn_uv_bwd")
+        # block b's slabs (NODE, EDGE, UV) are complete: sum them into its gradients on the side
+        # stream, beside the blocks below
+        ev["g"].record(main)
+        side.wait_event(ev["g"])
+        dd, bs, nd, nbk = tw._reduce_block[b]
+        check(L.sgnn_reduce_slabs(dd.data_ptr(), bs.data_ptr(), nd, nbk, side.cuda_stream), "sgnn_reduce_slabs")
+        if block_done is not None:
+            block_done(b, side)
+    ev["blocks"].record(side)
     encode_nodes_backward(tw, tw.g, inp, n, T, d, emb_weight, grid_radius, grid_radius,
                           _saves(h=tw.enc_h, yhat=tw.enc_yh, rstd=tw.enc_rstd, h2=tw.enc_h2), pk.enc,
                           tw.slab(_hip.SLAB_ENC_NODE), ns[_hip.SLAB_ENC_NODE], s)
@@ -245,6 +272,7 @@ def train_backward(gnn, inp: engine.StepInputs, tw: MSTrainWorkspace, grads: Dic
                               tw._nblocks, s), "sgnn_reduce_slabs")
     if use_emb:
         embedding_backward(tw, gnn.grid_node_encoder[0][0].weight, emb_weight, emb_grad, (T - 1) * d, s)
+    main.wait_event(ev["blocks"])   # Adam (and the next step's slabs) after the blocks' reductions
 
 
 class MultiScaleTrainer:
@@ -268,6 +296,7 @@ class MultiScaleTrainer:
         self.nslab = nslab
         self.step = 0
         self._tw: Dict[tuple, MSTrainWorkspace] = {}
+        self._buckets = None   # block_buckets(...) of the overlapped all-reduce, computed once
 
     def workspace(self, n: int, T: int, device) -> MSTrainWorkspace:
         graphs = self.sim._csr(n, device)
@@ -312,11 +341,24 @@ class MultiScaleTrainer:
         rg, rm = self.sim._grid_radius(), self.sim._mesh_radius()
         emb = self.sim._particle_type_embedding.weight if self.sim._nparticle_types > 1 else None
         train_forward(self.gnn, inp, tw, rg, rm, timers=timers, emb_weight=emb)
+        works, block_done = [], None
+        if self.dp.overlaps_buckets():   # per-block buckets, all-reduced during the backward (train.Trainer)
+            if self._buckets is None:
+                self._buckets = block_buckets(self.gnn.chain(), self.flat)
+            ranges, _ = self._buckets
+
+            def block_done(b, stream):
+                works.append(self.dp.allreduce_async(self.flat.comm[ranges[b][0]:ranges[b][1]], stream))
         train_backward(self.gnn, inp, tw, self.grads, rg, rm, next_pos=next_position.to(torch.float32).contiguous(),
                        noise=noise, next_strain=next_strain.to(torch.float32).contiguous(), w_pos=self.w_pos,
                        w_strain=self.w_strain, inv_count=1.0 / n_global, timers=timers, emb_weight=emb,
-                       emb_grad=self.grads.get("_particle_type_embedding.weight"))
-        self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
+                       emb_grad=self.grads.get("_particle_type_embedding.weight"), block_done=block_done)
+        if block_done is None:
+            self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
+        else:   # encoders, head and loss sums after the final reduction; then wait for the blocks' buckets
+            self.dp.allreduce_(*[self.flat.comm[a:b] for a, b in self._buckets[1]])
+            for w in works:
+                w.wait()
         self.opt.step()
         return self._finish(tw.loss_out, n_global)
 

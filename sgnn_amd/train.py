@@ -151,6 +151,27 @@ def layer_ranges(epd, flat: training.FlatParams) -> Tuple[List[Tuple[int, int]],
     return out, (lo, hi)
 
 
+def block_buckets(blocks, flat: training.FlatParams) -> Tuple[List[Tuple[int, int]], List[Tuple[int, int]]]:
+    """The overlapped all-reduce's buckets for a chain of message-passing blocks: [start, end) of each
+    block's parameters in the flat gradient buffer (each contiguous), and the intervals of the buffer
+    no block covers (encoders, head, loss sums) -- reduced together after the backward."""
+    out = []
+    for blk in blocks:
+        offs = sorted(flat.offsets[id(p)] for p in blk.parameters())
+        s, e = offs[0][0], offs[-1][0] + offs[-1][1]
+        if e - s != sum(n for _, n in offs):
+            raise RuntimeError("block parameters are not contiguous in the flat buffer")
+        out.append((s, e))
+    rest, at = [], 0
+    for s, e in sorted(out):
+        if s > at:
+            rest.append((at, s))
+        at = max(at, e)
+    if at < flat.comm.numel():
+        rest.append((at, flat.comm.numel()))
+    return out, rest
+
+
 class Trainer:
     """Drop-in training loop body for a sgnn_amd.LearnedSimulator."""
 

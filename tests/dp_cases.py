@@ -76,9 +76,11 @@ def run_single_scale(graph_ids, overlap=False, force=False):
     return _result(tr, losses)
 
 
-def run_multi_scale(graph_ids):
+def run_multi_scale(graph_ids, overlap=False, force=False):
     """STEPS MultiScaleTrainer steps on `graph_ids` (one static graph each,
-    merged block-diagonally when a process holds several)."""
+    merged block-diagonally when a process holds several).  overlap: the
+    per-block gradient buckets go out asynchronously from the side stream
+    during the backward (as run_single_scale)."""
     from sgnn_amd.multi_scale import MultiScaleSimulator
     from sgnn_amd.multi_scale.ms_training import MultiScaleTrainer
     from sgnn_amd.multi_scale.multi_scale_graph import build_static_multi_scale_graph
@@ -90,6 +92,10 @@ def run_multi_scale(graph_ids):
     counts = [wins[g][0][0].shape[0] for g in graph_ids]
     sim.set_static_graph(graphs[0] if len(graphs) == 1 else merge_static_graphs(graphs, counts))
     tr = MultiScaleTrainer(sim, lr_init=LR)
+    if overlap:
+        tr.dp.host_staging = False
+        tr.dp.force_overlap = force
+        assert tr.dp.world == 1 or tr.dp.overlaps_buckets()
     losses = []
     for s in range(STEPS):
         pos, nxt, strain, noise = _cat([wins[g][s] for g in graph_ids])
@@ -113,7 +119,22 @@ def run_single_scale_rccl(graph_ids):
     return run_single_scale(graph_ids, overlap=True, force=dist.is_initialized())
 
 
+def run_multi_scale_overlap(graph_ids):
+    return run_multi_scale(graph_ids, overlap=True)
+
+
+def run_multi_scale_rccl(graph_ids):
+    """The multi-scale trainer's per-block buckets on a one-rank RCCL (nccl) group (C5's collective
+    path), as run_single_scale_rccl."""
+    import torch.distributed as dist
+    if dist.is_initialized():
+        assert dist.get_backend() == "nccl"
+    return run_multi_scale(graph_ids, overlap=True, force=dist.is_initialized())
+
+
 CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, MS_GRAPHS, MS_RANKS),
          "ss_overlap": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS),
-         "ss_rccl1": (run_single_scale_rccl, SS_GRAPHS, [[0, 1, 2]])}
-RCCL_CASES = {"ss_rccl1"}
+         "ss_rccl1": (run_single_scale_rccl, SS_GRAPHS, [[0, 1, 2]]),
+         "ms_overlap": (run_multi_scale_overlap, MS_GRAPHS, MS_RANKS),
+         "ms_rccl1": (run_multi_scale_rccl, MS_GRAPHS, [[0, 1]])}
+RCCL_CASES = {"ss_rccl1", "ms_rccl1"}

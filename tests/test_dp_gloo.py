@@ -185,3 +185,30 @@ def test_layer_buckets_tile_the_flat_gradient():
             for p in layer.parameters():
                 off, n = flat.offsets[id(p)]
                 assert ranges[k][0] <= off and off + n <= ranges[k][1]
+
+
+def test_block_buckets_tile_the_flat_gradient():
+    """The multi-scale trainer's overlapped buckets (train.block_buckets): one
+    per G2M / M2M / M2G block in chain order, plus the intervals no block
+    covers (encoders, head, loss sums); together they cover the flat buffer
+    exactly once and every block parameter lies in its own block's bucket."""
+    import torch
+    from sgnn_amd import synthetic, training
+    from sgnn_amd.multi_scale import MultiScaleSimulator
+    from sgnn_amd.train import block_buckets
+    st = synthetic.normalization_stats(2, noise_std=0.02)
+    stats = {k: {kk: torch.from_numpy(vv) for kk, vv in v.items()} for k, v in st.items()}
+    sim = MultiScaleSimulator(2, 11, 3, 64, 64, 3, 2, stats, 1, 9, 2, 2, 2.0)
+    flat = training.FlatParams(sim)
+    blocks = sim._multi_scale_gnn.chain()
+    ranges, rest = block_buckets(blocks, flat)
+    assert len(ranges) == len(blocks) == 5 and rest
+    cover = torch.zeros(flat.comm.numel(), dtype=torch.int32)
+    for s, e in ranges + rest:
+        assert s < e
+        cover[s:e] += 1
+    assert bool((cover == 1).all())
+    for b, blk in enumerate(blocks):
+        for p in blk.parameters():
+            off, n = flat.offsets[id(p)]
+            assert ranges[b][0] <= off and off + n <= ranges[b][1]

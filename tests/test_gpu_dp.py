@@ -11,7 +11,8 @@ whole batch).  Tolerances: loss 1e-5 relative; gradients 2e-5 of the largest
 what that gradient error can move an Adam step (~lr x the relative gradient
 error, at most 2 lr per step).  `ss_rccl1`: the same single-scale step on a one-rank RCCL (nccl)
 group with the overlapped per-layer bucket all-reduces forced on (async collectives from the side
-stream, handles waited before Adam): the collective path C3 / C5 use, on real RCCL."""
+stream, handles waited before Adam): the collective path C3 / C5 use, on real RCCL; `ms_overlap` /
+`ms_rccl1`: the multi-scale trainer's per-block buckets the same way."""
 import os
 import socket
 import subprocess
@@ -34,7 +35,7 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("case", ["ss", "ms", "ss_overlap", "ss_rccl1"])
+@pytest.mark.parametrize("case", ["ss", "ms", "ss_overlap", "ss_rccl1", "ms_overlap", "ms_rccl1"])
 def test_two_ranks_match_one_process(case, tmp_path):
     from tests.dp_cases import CASES, LR, STEPS
     run, _, ranks = CASES[case]
