@@ -40,6 +40,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 
 #include "common.h"
 #include "fwd16.h"
@@ -351,7 +352,7 @@ constexpr int kPre = 3;   // halves per wave whose W1e e0 product runs before th
 #define SGNN_PUB_AT 1
 #endif
 constexpr int kPubAt = SGNN_PUB_AT;
-static_assert(kPubAt >= 1 && kPubAt <= kPre, "publish point within the pre-wait, after the donated product");
+static_assert(kPubAt >= 0 && kPubAt <= kPre, "publish point within the pre-wait");
 
 // The edge MLP of a layer, split around the wait for the sender tiles.  Wave b
 // takes the 16-edge halves b, b + 4, ... of the compacted tile CSR.  The first
@@ -418,14 +419,16 @@ struct EdgePhase {
   // barrier; FIRST: it also encodes that half's e0 rows), so every wave runs at most F + 1 products
   // before the wait and the owner reads the donated one after it.
   int F = 0, r = 0;
-  bool donor = false, owner_d = false;
+  bool donor = false, owner_d = false, donates = false;
+  int NH = 0;   // the tile's 16-edge halves
   int hd = -1;
   float* dbuf = nullptr;   // [2][KQ][64] f32x4 donated products
   SGNN_DEV void plan(float* dbuf_) {
-    const int NH = (Et + 15) / 16;
+    NH = (Et + 15) / 16;
     F = NH / 4;
     r = NH % 4;
     const bool don = (r == 1 || r == 2) && F + 1 <= kPre;
+    donates = don;  // (workgroup-uniform: from the tile's half count)
     owner_d = don && b < r;
     donor = don && b >= r && b - r < r;
     hd = donor ? 16 * (kWaves16 * F + (b - r)) : -1;
@@ -657,7 +660,7 @@ SGNN_DEV Node16Args node_args(const Step16Args& a, const Lay16& L, const Lay16* 
 // One interaction layer of the tile: wait for the sender tiles' u_k / v_k,
 // edge phase, receiver sums, node phase, publish u_{k+1} / v_{k+1}, stage the
 // next layer's edge weights.
-template <bool FIRST, int MODE, bool E0G, int NSUB>
+template <bool FIRST, int MODE, bool E0G, int NSUB, int PUB>
 SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv, const float (&xw1)[KQ],
                          const int32_t* deps, int ndeps, const int32_t* lsend, const int32_t* lrecv, int Et, int i0,
                          int cnt, int b, int j, int g, int l) {
@@ -688,16 +691,23 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   // weights (VGPR-resident) in three parts, so neither the drain nor the load issue stalls the MFMAs.
   const uint32_t ep_k = a.epoch0 + (uint32_t)k + 1;
   TilePoll poll;
+  // The publish point PUB: after the first product (1), so the drain of the write-through stores overlaps
+  // it -- or, in tiles of at most one half per wave, whose layer is a latency chain through the sender
+  // tiles' flags, before any product (0): the kernel picks per tile (k_step16)
+  constexpr int pub_at = PUB;
   auto hook = [&](int m) {
-    if (m == kPubAt) {
+    if (m == pub_at) {
       publish(a.flags, tile, ep_k);
       mark(ps < 0 ? -1 : ps + 2);
       W.load_first(nd, b, j, g);
     }
-    if (m == (kPubAt + 1 < kPre ? kPubAt + 1 : kPre)) W.load_mid(nd, b, j, g);
+    // publishing before the first product: the donated products (dbuf, written in the donors' slot 0)
+    // need a barrier of their own before any owner reads them after its wait
+    if (pub_at == 0 && m == 1 && ep.donates) __syncthreads();
+    if (m == (pub_at + 1 < kPre ? pub_at + 1 : kPre)) W.load_mid(nd, b, j, g);
     if (m == kPre - 1) poll.issue(deps, ndeps, a.flags, ep_k, l);
     if (m == kPre) poll.issue2(deps, ndeps, a.flags, ep_k, l);
-    if (m == (kPubAt + 2 < kPre ? kPubAt + 2 : kPre)) W.load_out(nd, b, j, g);
+    if (m == (pub_at + 2 < kPre ? pub_at + 2 : kPre)) W.load_out(nd, b, j, g);
   };
   ep.plan(lds + cv.dbuf);
   if (ep.donor) ep.template prewait<FIRST, true>(xw1, hook);
@@ -1107,10 +1117,19 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
 
   // ---- the interaction layers ------------------------------------------------------------------
   const int ndeps = *ndeps_l;
-  step_layer<true, 0, E0G, NSUB>(a, 0, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
-  for (int k = 1; k < a.L - 1; ++k)
-    step_layer<false, 0, E0G, NSUB>(a, k, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
-  step_layer<false, 1, E0G, NSUB>(a, a.L - 1, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+  // the publish point (step_layer): before the first pre-wait product where the waves hold at most one
+  // half each (a layer of such tiles is a latency chain through the sender tiles' flags: C1 r = 0.6
+  // 64.9 -> 61.6 us per step), after it otherwise (its drain then overlaps the product: publishing first
+  // there cost 0.5-1.6 %); same-box A/Bs, DESIGN.md section 5
+  auto layers = [&](auto pub) {
+    constexpr int P = decltype(pub)::value;
+    step_layer<true, 0, E0G, NSUB, P>(a, 0, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+    for (int k = 1; k < a.L - 1; ++k)
+      step_layer<false, 0, E0G, NSUB, P>(a, k, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+    step_layer<false, 1, E0G, NSUB, P>(a, a.L - 1, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+  };
+  if (Et <= 16 * kWaves16) layers(std::integral_constant<int, 0>{});
+  else layers(std::integral_constant<int, kPubAt>{});
 }
 
 }  // namespace
