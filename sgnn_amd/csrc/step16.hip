@@ -151,15 +151,19 @@ struct TilePoll {
     if (limit < 0 && lane == 0)  // test hook (sgnn_step_ws.step_poll_limit < 0): the error path
       __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ok(v, epoch) || ok(w, epoch)) return;
-    for (int it = 0;; ++it) {
+    // two polls in flight: each check waits only for the older one, so the counters are sampled twice
+    // per round trip
+    read(v, deps, ndeps, flags, epoch, lane);
+    for (int it = 0;; it += 2) {
+      read(w, deps, ndeps, flags, epoch, lane);
       if (ok(v, epoch)) break;
+      read(v, deps, ndeps, flags, epoch, lane);
+      if (ok(w, epoch)) break;
       if (it >= limit) {
         if (lane == 0)
           __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
-      read(v, deps, ndeps, flags, epoch, lane);
     }
   }
 };
