@@ -40,7 +40,7 @@ def test_every_roofline_kernel_resolves_in_this_rounds_profiles():
     template argument) would otherwise leave the line's traffic null."""
     import bench
     cases = [("c1_r15", "rollout", "k_step16"), ("c1_r06", "rollout", "k_step16"),
-             ("t4800", "rollout", "k_layer16"), ("t6400", "rollout", "k_layer16"), ("t8000", "rollout", "k_layer16"),
+             ("t4800", "rollout", "k_step16"), ("t6400", "rollout", "k_step16"), ("t8000", "rollout", "k_step16"),
              ("c2", "rollout", "k_edge_layer"), ("c4", "rollout", "k_edge_layer"),
              ("c2", "train", "k_edge_bwd64"), ("c3", "train", "k_edge_bwd64"),
              ("c5", "train", "k_edge_items<4, 3> + 3 k_wgrad_half<4, 1, 8>")]
