@@ -349,7 +349,10 @@ SGNN_DEV void lin2_init(const f32x4 (&acc)[KQ], f32x4 (&x)[KQ], f32x4 (&y)[KQ], 
   }
 }
 
-constexpr int kPre = 3;   // halves per wave whose W1e e0 product runs before the wait
+#ifndef SGNN_KPRE
+#define SGNN_KPRE 3
+#endif
+constexpr int kPre = SGNN_KPRE;   // halves per wave whose W1e e0 product runs before the wait
 // The tile publishes the node halves its previous stage stored after this many of those products: the
 // drain of the write-through stores overlaps them (SGNN_PUB_AT: experiment builds)
 #ifndef SGNN_PUB_AT
