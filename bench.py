@@ -268,8 +268,6 @@ def roofline(kernel, flops, avg_s, workload, mode, alg_bytes=None, executed_flop
     exe = flops if executed_flops is None else executed_flops
     charged = flops if whole else exe
     frac = charged / avg_s / MFMA_F32_PEAK
-    if frac > 1.0:
-        raise RuntimeError(f"roofline of {kernel}: {frac:.3f} of peak -- the FLOP count or the timing is wrong")
     r = {"bound": "mfma", "kernel": kernel, "achieved": charged / avg_s / 1e12, "peak": MFMA_F32_PEAK / 1e12,
          "unit": "TFLOP/s", "frac": frac, "flops": "8d" if whole else "executed",
          "exe_frac": exe / avg_s / MFMA_F32_PEAK, "flops_per_launch": charged,
@@ -279,6 +277,8 @@ def roofline(kernel, flops, avg_s, workload, mode, alg_bytes=None, executed_flop
         r["src"] = os.path.basename(prof["source"])
     if alg_bytes is not None:
         r["alg_bytes"] = alg_bytes
+    if frac > 1.0:   # recorded, not raised: one noisy leg must not discard the whole line
+        r["error"] = f"frac {frac:.3f} > 1: the FLOP count or the timing is wrong"
     return r
 
 
@@ -300,7 +300,7 @@ def leg(r):
     if "roofline" in r:
         rf = r["roofline"]
         out["rf"] = {k: rf[k] for k in ("kernel", "frac", "flops", "exe_frac", "traffic", "alg_bytes", "live_us",
-                                        "prof_us", "src") if k in rf}
+                                        "prof_us", "src", "error") if k in rf}
     if "cpu_baseline" in r:
         out["cpu"] = {k: r["cpu_baseline"][k] for k in ("value", "cores", "sample")}
         out["x_cpu"] = r["speedup_vs_cpu"]

@@ -293,6 +293,14 @@ int sgnn_step_check(const sgnn_step_ws* ws, void* stream);
 int sgnn_rollout(const sgnn_epd* model, const sgnn_step_in* in, float* win_a, float* win_b,
                  const sgnn_step_ws* ws, int32_t nsteps, float* out_pos, float* out_pred,
                  void* stream);
+/* Teacher-forced ("one_step") rollout, evaluate.py:136-145 with inference_mode == "one_step": step k
+ * predicts from the current window exactly as sgnn_rollout does, then the next window is
+ * cat([window[:, 1:], gt_k]) -- the ground-truth position of step k, not the prediction (:140-143).
+ * gt_k[i][c] = gt[k * gt_ld_t + i * gt_ld_n + c] (the reference's position[:, T:] is [n][steps][dim]:
+ * gt_ld_n = steps * dim, gt_ld_t = dim).  Outputs as sgnn_rollout. */
+int sgnn_rollout_one_step(const sgnn_epd* model, const sgnn_step_in* in, float* win_a, float* win_b,
+                          const sgnn_step_ws* ws, int32_t nsteps, const float* gt, int64_t gt_ld_n,
+                          int64_t gt_ld_t, float* out_pos, float* out_pred, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Training backward: reverse of predict_accelerations (learned_simulator.py:

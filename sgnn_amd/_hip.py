@@ -159,6 +159,8 @@ SIGNATURES = {
     "sgnn_step_check": (ctypes.c_int, [c_void_p, c_void_p]),
     "sgnn_rollout": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                     c_void_p, c_void_p]),
+    "sgnn_rollout_one_step": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                             c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "sgnn_random_walk_noise": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_float, ctypes.c_uint64,
                                               ctypes.c_uint64, c_void_p, c_void_p, c_void_p]),
     "sgnn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,

@@ -46,6 +46,15 @@ def _c(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
+def _dense(t: torch.Tensor) -> torch.Tensor:
+    """fp32 and fully contiguous: for the kernels that index rows as r * width
+    (sgnn_layernorm's residual, sgnn_layernorm_bwd's dout; ADVICE r04 -- torch.cat's
+    backward hands each input a row-strided narrow() view)."""
+    if t.dtype != torch.float32:
+        t = t.to(torch.float32)
+    return t.contiguous()
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False,
          bias: Optional[torch.Tensor] = None, relu: bool = False, out: Optional[torch.Tensor] = None,
          accumulate: bool = False) -> torch.Tensor:
@@ -164,7 +173,7 @@ class _MLP(torch.autograd.Function):
             out = torch.empty_like(h)
             yhat = torch.empty_like(h)
             rstd = torch.empty(n, dtype=torch.float32, device=h.device)
-            res = _c(residual) if residual is not None else None
+            res = _dense(residual) if residual is not None else None
             check(lib().sgnn_layernorm(h.data_ptr() if n else None, n, w, gamma.data_ptr(), beta.data_ptr(),
                                        res.data_ptr() if res is not None else None, out.data_ptr() if n else None,
                                        yhat.data_ptr() if n else None, rstd.data_ptr() if n else None,
@@ -184,7 +193,7 @@ class _MLP(torch.autograd.Function):
         acts = saved[:nlin + 1]
         yhat, rstd = saved[nlin + 1], saved[nlin + 2]
         params = saved[nlin + 3:]
-        dout = _c(dout)
+        dout = _dense(dout) if has_ln else _c(dout)
         n = dout.shape[0]
         grads: List[Optional[torch.Tensor]] = [None] * len(params)
         if has_ln:

@@ -80,7 +80,7 @@ SGNN_DEV float epilogue(const GemmArgs& g, float v, int64_t m, int64_t n) {
   return g.relu ? fmaxf(v, 0.0f) : v;
 }
 
-// Workgroup (bx, by, split): the 64 x 64 tile of C at (by * 64, bx * 64) over this split's K chunks.
+// Workgroup (bx, by, split): the 64 x 64 tile of C at (bx * 64, by * 64) over this split's K chunks.
 // Waves in a 2 x 2 grid, each one 32 x 32 accumulator: lane l holds column (l & 31), register r row
 // crow(r, l >> 5) (common.h).
 __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
@@ -88,7 +88,8 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
   __shared__ float Bs[kKc * kLdT];
   const int l = lane_id(), w = wave_id();
   const int wm = w >> 1, wn = w & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * kTile, n0 = (int64_t)blockIdx.x * kTile;
+  // row tiles on grid.x (2^31 - 1: edge-row GEMMs of any graph), column tiles on grid.y
+  const int64_t m0 = (int64_t)blockIdx.x * kTile, n0 = (int64_t)blockIdx.y * kTile;
   const int split = blockIdx.z, nsplit = gridDim.z;
   const int64_t c0 = g.nkc * split / nsplit, c1 = g.nkc * (split + 1) / nsplit;
   f32x16 acc;
@@ -294,7 +295,8 @@ extern "C" int sgnn_gemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
   if (M == 0 || N == 0) return SGNN_OK;
   if (K > 0 && (!A || !B || lda < (trans_a ? M : K) || ldb < (trans_b ? K : N)))
     return set_error(SGNN_ERR_INVALID, "gemm: bad operand");
-  if (M / kTile >= 65535) return set_error(SGNN_ERR_UNSUPPORTED, "gemm: more than 4M rows");
+  if ((N + kTile - 1) / kTile > 65535 || (M + kTile - 1) / kTile > INT32_MAX)
+    return set_error(SGNN_ERR_UNSUPPORTED, "gemm: more than 4M columns");
   hipStream_t s = static_cast<hipStream_t>(stream);
   GemmArgs g{A, B, bias, lda, ldb, ldc, M, N, K, C, nullptr, trans_a ? 1 : 0, trans_b ? 1 : 0, relu ? 1 : 0,
              accumulate ? 1 : 0, (K + kKc - 1) / kKc};
@@ -304,7 +306,7 @@ extern "C" int sgnn_gemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
       return set_error(SGNN_ERR_INVALID, "gemm: workspace smaller than sgnn_gemm_workspace_bytes");
     g.part = static_cast<float*>(workspace);
   }
-  const dim3 grid((unsigned)((N + kTile - 1) / kTile), (unsigned)((M + kTile - 1) / kTile), (unsigned)nsplit);
+  const dim3 grid((unsigned)((M + kTile - 1) / kTile), (unsigned)((N + kTile - 1) / kTile), (unsigned)nsplit);
   hipLaunchKernelGGL(k_gemm, grid, dim3(kGemmThreads), 0, s, g);
   if (nsplit > 1) hipLaunchKernelGGL(k_gemm_reduce, dim3(ew_grid(M * N)), dim3(kEw), 0, s, g, nsplit);
   return check_launch("gemm");

@@ -185,6 +185,7 @@ SGNN_DEV float dist2_ordered(const float* a, const float* b, int dim) {
   // fp32, dims summed in order, no contraction: matches the oracle / golden rule.
   float s = 0.0f;
   for (int d = 0; d < dim; ++d) {
+#pragma clang fp contract(off)
     const float t = __fsub_rn(a[d], b[d]);
     s = __fadd_rn(s, __fmul_rn(t, t));
   }
@@ -382,6 +383,7 @@ __global__ __launch_bounds__(kQBlock) void k_radius_query_lds(
           float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
 #pragma unroll
           for (int d = 0; d < DIM; ++d) {
+#pragma clang fp contract(off)
             const float u = __fsub_rn(c[d], me[d]);
             s = __fadd_rn(s, __fmul_rn(u, u));
           }

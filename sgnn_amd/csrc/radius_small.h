@@ -209,6 +209,7 @@ SGNN_DEV void radius_small_body(const RadiusSmallArgs& a, float* lds, int blk, i
         float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
 #pragma unroll
         for (int d = 0; d < DIM; ++d) {
+#pragma clang fp contract(off)
           const float t = __fsub_rn(cp[d * n + k], pi[d]);
           s = __fadd_rn(s, __fmul_rn(t, t));
         }

@@ -295,6 +295,48 @@ extern "C" int sgnn_rollout(const sgnn_epd* m, const sgnn_step_in* in, float* wi
   return st;
 }
 
+namespace {
+// one_step rollout (evaluate.py:140-143): the next window's last frame is the ground-truth position of
+// the step, win[i][T-1][:] = gt[i * gt_ld + c] (the predicted frame the decoder shifted in is replaced)
+__global__ void k_teacher_frame(float* win, int64_t n, int T, int d, const float* gt, int64_t gt_ld) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * d) return;
+  const int64_t i = t / d;
+  const int c = (int)(t - i * d);
+  win[(i * T + T - 1) * d + c] = gt[i * gt_ld + c];
+}
+}  // namespace
+
+extern "C" int sgnn_rollout_one_step(const sgnn_epd* m, const sgnn_step_in* in, float* win_a, float* win_b,
+                                     const sgnn_step_ws* ws, int32_t nsteps, const float* gt, int64_t gt_ld_n,
+                                     int64_t gt_ld_t, float* out_pos, float* out_pred, void* stream) {
+  using namespace sgnn;
+  if (!in || !win_a || !win_b || win_a == win_b || !out_pos || !out_pred || nsteps < 0 || (nsteps > 0 && !gt) ||
+      gt_ld_n < in->dim || gt_ld_t < 0)
+    return set_error(SGNN_ERR_INVALID, "rollout_one_step: bad arguments");
+  const int64_t n = in->n;
+  const int d = in->dim, T = in->T;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Step16Call call(s);
+  bool used16 = false;
+  int st = SGNN_OK;
+  for (int32_t k = 0; k < nsteps && st == SGNN_OK; ++k) {
+    float* cur = (k & 1) ? win_b : win_a;
+    float* nxt = (k & 1) ? win_a : win_b;
+    // the window's last frame is ground truth from step 1 on: read from the window itself (no pos_last)
+    st = predict_impl(m, in, cur, ws, out_pred + (int64_t)k * n * (d + 1), out_pos + (int64_t)k * n * d, nxt,
+                      stream, k, nullptr, call.allow() && (k == 0 || used16), &used16);
+    if (st == SGNN_OK && k + 1 < nsteps && n > 0) {
+      const int64_t tot = n * d;
+      hipLaunchKernelGGL(k_teacher_frame, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, nxt, n, T, d,
+                         gt + (int64_t)k * gt_ld_t, gt_ld_n);
+      st = check_launch("rollout_one_step: ground-truth frame");
+    }
+  }
+  if (used16) call.launched_step16();
+  return st;
+}
+
 extern "C" int sgnn_step_check(const sgnn_step_ws* ws, void* stream) {
   using namespace sgnn;
   if (!ws) return set_error(SGNN_ERR_INVALID, "step_check: bad arguments");

@@ -1003,6 +1003,7 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
             float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
 #pragma unroll
             for (int d = 0; d < DIM; ++d) {
+#pragma clang fp contract(off)
               const float t = __fsub_rn(pc[u][d], pi[d]);
               s = __fadd_rn(s, __fmul_rn(t, t));
             }

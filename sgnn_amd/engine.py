@@ -560,16 +560,36 @@ class DeviceRollout:
         self.out_pos = torch.empty(max(nsteps, 1), n, dim, dtype=torch.float32, device=dev)
         self.out_pred = torch.empty(max(nsteps, 1), n, dim + 1, dtype=torch.float32, device=dev)
 
-    def run(self, window: Optional[torch.Tensor] = None, check_step: bool = True):
+    def run(self, window: Optional[torch.Tensor] = None, check_step: bool = True,
+            ground_truth: Optional[torch.Tensor] = None):
         """Returns (positions [nsteps, n, dim], strain [nsteps, n]) on the device.  With check_step
         (default) the call ends with sgnn_step_check (a stream sync) and raises SgnnError when a
-        one-launch step timed out; a caller passing False must call ws.check_step itself."""
+        one-launch step timed out; a caller passing False must call ws.check_step itself.
+        ground_truth [n, >= nsteps, dim] switches to the teacher-forced ("one_step") rollout
+        (evaluate.py:140-143): each next window ends with the ground-truth frame of the step, not the
+        prediction -- still ONE library call (sgnn_rollout_one_step)."""
         if window is not None:
             self.win[0].copy_(window)
-        check(lib().sgnn_rollout(ctypes.byref(self.epd), ctypes.byref(self.sin), self.win[0].data_ptr(),
-                                 self.win[1].data_ptr(), ctypes.byref(self.ws.c), self.nsteps,
-                                 self.out_pos.data_ptr(), self.out_pred.data_ptr(),
-                                 stream_ptr(self.win[0].device)), "sgnn_rollout")
+        dev = self.win[0].device
+        if ground_truth is None:
+            check(lib().sgnn_rollout(ctypes.byref(self.epd), ctypes.byref(self.sin), self.win[0].data_ptr(),
+                                     self.win[1].data_ptr(), ctypes.byref(self.ws.c), self.nsteps,
+                                     self.out_pos.data_ptr(), self.out_pred.data_ptr(), stream_ptr(dev)),
+                  "sgnn_rollout")
+        else:
+            _hip.require_gpu_tensor(ground_truth, "ground_truth")
+            if (ground_truth.dim() != 3 or ground_truth.shape[0] != self.n or ground_truth.shape[2] != self.dim
+                    or ground_truth.shape[1] < self.nsteps):
+                raise ValueError(f"ground_truth must be [{self.n}, >= {self.nsteps}, {self.dim}], "
+                                 f"got {tuple(ground_truth.shape)}")
+            gt = ground_truth.to(torch.float32)
+            if gt.stride(2) != 1:
+                gt = gt.contiguous()
+            self.keep_gt = gt
+            check(lib().sgnn_rollout_one_step(ctypes.byref(self.epd), ctypes.byref(self.sin), self.win[0].data_ptr(),
+                                              self.win[1].data_ptr(), ctypes.byref(self.ws.c), self.nsteps,
+                                              gt.data_ptr(), gt.stride(0), gt.stride(1), self.out_pos.data_ptr(),
+                                              self.out_pred.data_ptr(), stream_ptr(dev)), "sgnn_rollout_one_step")
         if check_step:
             self.ws.check_step(self.win[0].device)
         return self.out_pos[:self.nsteps], self.out_pred[:self.nsteps, :, -1]

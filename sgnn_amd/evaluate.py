@@ -51,14 +51,16 @@ def rollout(simulator, position: torch.Tensor, particle_types: torch.Tensor, n_p
     erosional = erosional.bool()[:, None].expand(-1, particle_dim)
     any_erosional = bool(erosional.any())
     start = time.time()
-    fast = (inference_mode == "autoregressive" and not any_erosional and nsteps > 0
-            and hasattr(simulator, "rollout_runner") and position.is_cuda
+    fast = (not any_erosional and nsteps > 0 and hasattr(simulator, "rollout_runner") and position.is_cuda
             and getattr(simulator, "_fast_path", lambda: True)())
     if fast:
         # device-resident loop: one sgnn_rollout call (window shift fused into the
-        # decoder kernel; same kernels and arithmetic as predict_positions)
+        # decoder kernel; same kernels and arithmetic as predict_positions); one_step
+        # (:140-143) is one sgnn_rollout_one_step call: each next window ends with the
+        # step's ground-truth frame
         runner = simulator.rollout_runner(initial_positions, [n_particles_per_example], particle_types, nsteps)
-        pred_positions, pred_strains = runner.run()
+        gt = None if inference_mode == "autoregressive" else ground_truth_positions
+        pred_positions, pred_strains = runner.run(ground_truth=gt)
         nsteps = 0
     for step in range(nsteps):
         nxt, ps = simulator.predict_positions(current, nparticles_per_example=[n_particles_per_example],

@@ -138,6 +138,49 @@ def test_module_forwards_backward_match_oracle():
     _check_grads(epd._decoder.named_parameters(prefix=pre + "_decoder"), state)
 
 
+def test_row_strided_views_through_layernorm():
+    """torch.cat's backward hands each input a narrow() view (row
+    stride > width), and a column slice used as an input is row-strided too.
+    The LayerNorm kernels index rows as r * width, so those views must reach
+    them dense: Encoder outputs concatenated with another tensor, and an
+    InteractionNetwork whose x (its residual) is a column slice."""
+    from oracle import sgnn_oracle as O
+    sim, osim, state, seq, types_, _ = _setup(64, 64, 1, 2)
+    pos = torch.from_numpy(seq[:, :11])
+    n = pos.shape[0]
+    nf, ei, ef = osim.preprocess(pos, [n], types_)
+    epd = sim._encode_process_decode
+    pre = "_encode_process_decode."
+    rng = np.random.default_rng(5)
+    # Encoder outputs inside a cat: the node / edge latents' gradients arrive as narrow() views
+    ex, ee = epd._encoder(nf.cuda(), ef.cuda())
+    ox = torch.from_numpy(rng.normal(0, 1, (n, 7)).astype(np.float32)).cuda()
+    oe = torch.from_numpy(rng.normal(0, 1, (ef.shape[0], 5)).astype(np.float32)).cuda()
+    wx = torch.from_numpy(rng.normal(0, 1, (n, 64 + 7)).astype(np.float32))
+    we = torch.from_numpy(rng.normal(0, 1, (ef.shape[0], 64 + 5)).astype(np.float32))
+    ((torch.cat([ex, ox], 1) * wx.cuda()).sum() + (torch.cat([ee, oe], 1) * we.cuda()).sum()).backward()
+    ((O.mlp_ln(nf, state, pre + "_encoder.node_fn.", 2) * wx[:, :64]).sum()
+     + (O.mlp_ln(ef, state, pre + "_encoder.edge_fn.", 2) * we[:, :64]).sum()).backward()
+    _check_grads(epd._encoder.named_parameters(prefix=pre + "_encoder"), state)
+    # InteractionNetwork on a column slice of a wider tensor (row-strided x and residual)
+    for v in state.values():
+        v.grad = None
+    sim.zero_grad(set_to_none=True)
+    x0 = O.mlp_ln(nf, state, pre + "_encoder.node_fn.", 2).detach()
+    e0 = O.mlp_ln(ef, state, pre + "_encoder.edge_fn.", 2).detach()
+    xr = x0.clone().requires_grad_(True)
+    rx, _ = O.interaction_network(xr, ei, e0, state, pre + "_processor.gnn_stacks.0.", 2)
+    w2 = torch.from_numpy(rng.normal(0, 1, x0.shape).astype(np.float32))
+    (rx * w2).sum().backward()
+    wide = torch.cat([x0, torch.zeros(n, 3)], 1).cuda().requires_grad_(True)
+    gx, _ = epd._processor.gnn_stacks[0](wide[:, :64], ei.cuda(), e0.cuda())
+    _close(gx.detach().cpu().numpy(), rx.detach().numpy(), what="InteractionNetwork on a column slice")
+    (gx * w2.cuda()).sum().backward()
+    _check_grads(epd._processor.gnn_stacks[0].named_parameters(prefix=pre + "_processor.gnn_stacks.0"), state)
+    _grad_close(wide.grad[:, :64].cpu().numpy(), xr.grad.numpy(), "column-slice dx", rel=5e-4)
+    assert float(wide.grad[:, 64:].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("H", [64, 128])
 def test_interaction_network_inference_runs_fused_kernels(H, monkeypatch):
     """InteractionNetwork.forward in inference at the fast widths goes through

@@ -192,3 +192,42 @@ def test_two_subtile_rollout_against_oracle():
     _close(pos.cpu().numpy(), ref_pos.numpy(), atol=2 * nsteps * ATOL * scale, rtol=1e-6,
            what="6,400-particle 5-step rollout positions")
     _close(strain.cpu().numpy(), ref_str.numpy(), atol=2 * nsteps * ATOL, what="6,400-particle rollout strain")
+
+
+@pytest.mark.parametrize("dims,radius", [((50, 40), 15.0), ((160, 40), 0.6)])
+def test_one_step_rollout_is_one_device_call(dims, radius, monkeypatch):
+    """evaluate.rollout(..., inference_mode='one_step') (evaluate.py:140-143:
+    each next window ends with the ground-truth frame) runs as ONE
+    sgnn_rollout_one_step call -- no predict_positions per step -- and matches
+    the oracle's teacher-forced rollout (C1 r = 15; 6,400 particles with two
+    node sub-tiles)."""
+    from oracle import sgnn_oracle as O
+    from sgnn_amd import engine, evaluate, synthetic
+    z = golden("c1_r15")
+    hp = hparams(z)
+    T, nsteps = hp["T"], 6
+    seq = synthetic.trajectory(synthetic.lattice_2d(*dims), T + nsteps, seed=1002)
+    n = seq.shape[0]
+    sim = product_sim(z)
+    sim._connectivity_radius = radius
+    calls = []
+    real_run = engine.DeviceRollout.run
+    monkeypatch.setattr(engine.DeviceRollout, "run",
+                        lambda self, *a, **k: calls.append(k.get("ground_truth") is not None) or real_run(self, *a, **k))
+    monkeypatch.setattr(type(sim), "predict_positions",
+                        lambda *a, **k: (_ for _ in ()).throw(AssertionError("per-step predict_positions")))
+    strains = torch.zeros(T + nsteps, n, device="cuda")
+    out = evaluate.rollout(sim, torch.from_numpy(seq).cuda(), torch.zeros(n, dtype=torch.long, device="cuda"), n,
+                           strains, nsteps, 2, torch.device("cuda"), T, inference_mode="one_step")
+    assert calls == [True]
+    osim = oracle_sim(z)
+    osim.radius = radius
+    ref_pos, ref_str = O.rollout_one_step(osim, torch.from_numpy(seq), torch.zeros(n, dtype=torch.long), n, nsteps, T)
+    scale = float(np.max(z["acc_std"]))
+    # teacher forcing: every step's error is one step's (no accumulation)
+    _close(out["predicted_rollout"], ref_pos.numpy(), atol=2 * ATOL * scale, rtol=1e-6, what="one_step positions")
+    _close(out["predicted_strain"], ref_str.numpy(), atol=2 * ATOL, what="one_step strain")
+    # and the autoregressive rollout of the same start differs (the mode switch took effect)
+    auto = evaluate.rollout(sim, torch.from_numpy(seq).cuda(), torch.zeros(n, dtype=torch.long, device="cuda"), n,
+                            strains, nsteps, 2, torch.device("cuda"), T, inference_mode="autoregressive")
+    assert not np.array_equal(auto["predicted_rollout"][-1], out["predicted_rollout"][-1])
