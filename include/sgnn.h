@@ -268,6 +268,9 @@ typedef struct sgnn_step_ws { /* device buffers of one (n, T, dim, H, K) shape *
   int32_t* step_deg;    /* [n] neighbours kept per receiver */
   int32_t step_poll_limit; /* 0: default (~1 s of polling per wait before the error word is set);
                               < 0: test hook, every tile records a timeout at its first wait */
+  int32_t step_skew;       /* test knob, 0 = off: before each phase publish, workgroup t sleeps a
+                              tile- and phase-dependent 0..7 x step_skew rounds of ~0.4 us, so tiles
+                              hand off under uneven load (results must not change) */
 } sgnn_step_ws;
 
 int sgnn_predict_positions(const sgnn_epd* model, const sgnn_step_in* in, const float* pos_seq,
@@ -505,6 +508,11 @@ int sgnn_segment_sum_cols(const float* src, int64_t ld_src, int32_t width, const
  * to edge_cap).  InteractionNetwork.forward(x, edge_index, e) on the fused kernels (graph_network.py:150). */
 int sgnn_edge_rows_to_tiles(const float* e, int64_t ld, int32_t width, const int32_t* perm, const int32_t* rowptr,
                             int64_t n, int64_t edge_cap, float* e0t, void* stream);
+/* The inverse, for the module-level block backward (InteractionNetwork.forward under autograd,
+ * graph_network.py:150): out[perm[p]][0:width] (+ when accumulate) = scale * tile position p of e0t for
+ * p < num_edges (= rowptr[n]; the edge-latent gradient dE0 back in the caller's COO row order). */
+int sgnn_edge_tiles_to_rows(const float* e0t, int32_t width, const int32_t* perm, const int32_t* rowptr, int64_t n,
+                            int64_t num_edges, float scale, float* out, int64_t ld, int32_t accumulate, void* stream);
 
 #ifdef __cplusplus
 }

@@ -56,7 +56,7 @@ class SgnnStepWs(ctypes.Structure):
                 ("edge_cap", c_int64), ("e0t", c_void_p), ("x_a", c_void_p), ("x_b", c_void_p),
                 ("u", c_void_p), ("v", c_void_p), ("agg", c_void_p), ("cin", c_void_p), ("cout", c_void_p),
                 ("u2", c_void_p), ("v2", c_void_p), ("uvl", c_void_p), ("step_flags", c_void_p),
-                ("step_deg", c_void_p), ("step_poll_limit", c_int32)]
+                ("step_deg", c_void_p), ("step_poll_limit", c_int32), ("step_skew", c_int32)]
 
 
 class SgnnReduceDesc(ctypes.Structure):
@@ -159,6 +159,8 @@ SIGNATURES = {
     "sgnn_step_check": (ctypes.c_int, [c_void_p, c_void_p]),
     "sgnn_rollout": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                     c_void_p, c_void_p]),
+    "sgnn_edge_tiles_to_rows": (ctypes.c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_int64, c_float,
+                                               c_void_p, c_int64, c_int32, c_void_p]),
     "sgnn_rollout_one_step": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                              c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "sgnn_random_walk_noise": (ctypes.c_int, [c_void_p, c_int64, c_int32, c_int32, c_float, ctypes.c_uint64,

@@ -149,6 +149,14 @@ class EdgeGraph:
         self.recv = ei[1].to(torch.int32).contiguous()
         self.by_recv = grouping(ei[1], n)   # also range-checks the indices (one host sync)
         self.by_send = grouping(ei[0], n)
+        self._ei, self._fused = ei, None
+
+    def fused(self):
+        """The fused kernels' CSR (+ COO permutation, sender transpose) of this graph, built once."""
+        if self._fused is None:
+            from .fused_block import FusedGraph
+            self._fused = FusedGraph(self._ei, self.n)
+        return self._fused
 
 
 # ----------------------------------------------------------------------------- Functions
@@ -313,7 +321,13 @@ class _SegmentSum(torch.autograd.Function):
 def message_passing(block: nn.Module, x: torch.Tensor, graph: EdgeGraph, e: torch.Tensor):
     """InteractionNetwork.forward (graph_network.py:150-222) / G2M / M2M / M2G block
     (multi_scale_gnn.py:84-205): (x + LN(node_fn([aggr, x])), e + e) with
-    aggr = sum over receivers of LN(edge_fn([x_i, x_j, e]))."""
+    aggr = sum over receivers of LN(edge_fn([x_i, x_j, e])).  At the widths the
+    fused kernels are built for (latents = MLP hidden = 64 / 128, nmlp_layers 1 / 2)
+    forward and backward run the training step's fused layer kernels
+    (sgnn_amd/fused_block.py); the GEMM chain below serves every other shape."""
+    from . import fused_block
+    if fused_block.applies(block, x, e, graph.E):
+        return fused_block.message_passing(block, x, graph.fused(), e)
     x, e = _c(x), _c(e)
     if e.shape[0] != graph.E:
         raise ValueError(f"{e.shape[0]} edge feature rows for {graph.E} edges")

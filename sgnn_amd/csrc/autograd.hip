@@ -268,7 +268,38 @@ __global__ __launch_bounds__(kEw) void k_rows_to_tiles(const float* e, int64_t l
   }
 }
 
+// The inverse: tile position p (< E) -> row perm[p] of out (+)= scale * its units (the edge-latent
+// gradient of a module-level block backward back in the caller's COO order).
+__global__ __launch_bounds__(kEw) void k_tiles_to_rows(const float* e0t, int width, const int32_t* perm,
+                                                       const int32_t* rowptr, int64_t n, float scale, float* out,
+                                                       int64_t ld, int accumulate) {
+  const int64_t E = rowptr[n];
+  const int64_t total = E * width;
+  for (int64_t t = (int64_t)blockIdx.x * kEw + threadIdx.x; t < total; t += (int64_t)gridDim.x * kEw) {
+    const int64_t p = t / width;
+    const int u = (int)(t - p * width), uu = u & 31;
+    const int64_t tile = p >> 5;
+    const int grp = 4 * (u >> 5) + (uu >> 3), lane = (int)(p & 31) + 32 * ((uu >> 2) & 1);
+    const float v = scale * e0t[tile * 32 * width + grp * 256 + lane * 4 + (uu & 3)];
+    float* o = out + (int64_t)(perm ? perm[p] : p) * ld + u;
+    *o = accumulate ? *o + v : v;
+  }
+}
+
 }  // namespace
+
+extern "C" int sgnn_edge_tiles_to_rows(const float* e0t, int32_t width, const int32_t* perm, const int32_t* rowptr,
+                                       int64_t n, int64_t num_edges, float scale, float* out, int64_t ld,
+                                       int32_t accumulate, void* stream) {
+  using namespace sgnn;
+  if (!rowptr || !e0t || width < 32 || width % 32 != 0 || ld < width || n < 0 || num_edges < 0 ||
+      (num_edges > 0 && !out))
+    return set_error(SGNN_ERR_INVALID, "edge_tiles_to_rows: bad arguments");
+  if (num_edges == 0) return SGNN_OK;
+  hipLaunchKernelGGL(k_tiles_to_rows, dim3(ew_grid(num_edges * width)), dim3(kEw), 0, static_cast<hipStream_t>(stream),
+                     e0t, width, perm, rowptr, n, scale, out, ld, accumulate ? 1 : 0);
+  return check_launch("edge_tiles_to_rows");
+}
 
 extern "C" int sgnn_edge_rows_to_tiles(const float* e, int64_t ld, int32_t width, const int32_t* perm,
                                        const int32_t* rowptr, int64_t n, int64_t edge_cap, float* e0t, void* stream) {

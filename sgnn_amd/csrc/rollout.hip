@@ -77,6 +77,7 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   a.ecap_t = a.nt * cap;
   a.e0_hbm = a.nt > 16 ? 1 : 0;   // two node sub-tiles: their e0 rows live in HBM
   a.poll_limit = ws->step_poll_limit;
+  a.skew = ws->step_skew;
   size_t lds = step16_lds_bytes(a);
   if (lds > kStep16MaxLds && !a.e0_hbm) {  // the tile's e0 rows do not fit in LDS: keep them in HBM (ws->uvl's tail)
     a.e0_hbm = 1;

@@ -51,6 +51,7 @@ struct Step16Args {
   int ecap_t;          // edge rows per workgroup (nt * cap)
   int32_t *deg_out, *nbr_out;  // optional: the radius graph as padded lists [n], [n][cap]
   int poll_limit;      // polls per wait before the error word is set (< 0: test hook, set it at the first wait)
+  int skew;            // test knob (sgnn_step_ws.step_skew): tile-dependent sleep before each publish, 0 = off
   // outputs
   float *pred, *next_pos, *window_out;
 };

@@ -119,6 +119,28 @@ SGNN_DEV void mark(int slot) {
 SGNN_DEV void mark(int) {}
 #endif
 
+// Hand-off check build (-DSGNN_HANDOFF_CHECK, tools/exp_handoff.py).  Buffer g_hc
+// (sgnn_set_handoff_check): [0] hash mismatches, [1] tag mismatches, [2] printed lines, [3] final checks
+// run, [4..15] spare; then tags [L][n][4]: for every node-half row it stores, the producing wave b
+// writes the phase its rows are published with (epoch0 + buffer + 1, sc1, drained with the rows);
+// then hashes [grid][L][kHcHalves][64][2]: per gathered half and lane, a hash of the u and of the v
+// row words as the consumer used them.  Consumers compare the tags of every row they gather (sender
+// and receiver) with the phase they polled for; at the end of the kernel every tile publishes a final
+// phase, waits for its sender tiles to reach it, re-gathers every half of every layer and compares the
+// hashes: a row read before its producer's stores had landed differs from the settled value.
+#ifdef SGNN_HANDOFF_CHECK
+__device__ uint32_t* g_hc;
+constexpr int kHcHalves = sgnn::kStep16MaxNT * sgnn::kStep16MaxCap / 16;
+SGNN_DEV uint32_t* hc_tags() { return g_hc + 16; }
+SGNN_DEV uint32_t* hc_hash(const Step16Args& a) { return g_hc + 16 + (int64_t)a.L * a.n * 4; }
+SGNN_DEV uint32_t hc_mix(uint32_t h, f32x4 v) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) h = (h ^ __builtin_bit_cast(uint32_t, v[c])) * 16777619u;
+  return h;
+}
+SGNN_DEV bool hc_print() { return atomicAdd(g_hc + 2, 1u) < 48u; }
+#endif
+
 // Per-tile counters of the sender tiles `deps` (up to 256, all requested at once).  Every wave polls for
 // itself (no workgroup barrier after the match): `issue` requests the counters early -- before the
 // wave's last pre-wait product, so their round trip overlaps it -- and `wait` checks them and polls
@@ -168,12 +190,20 @@ struct TilePoll {
   }
 };
 
-// Every storing wave drains its sc1 stores, then one lane publishes the phase.
-SGNN_DEV void publish(uint32_t* flags, int tile, uint32_t epoch) {
+// Every storing wave drains its sc1 stores, then one lane publishes the phase.  skew > 0 (test knob,
+// sgnn_step_ws.step_skew): that lane first sleeps 0..7 x skew rounds of s_sleep 16 (~0.4 us each), a
+// tile- and phase-dependent count, so tiles run the hand-off under uneven load.
+SGNN_DEV void publish(uint32_t* flags, int tile, uint32_t epoch, int skew) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
+    if (skew > 0) {
+      const uint32_t h = ((uint32_t)tile * 2654435761u) ^ (epoch * 40503u);
+      const int rounds = (int)((h >> 28) & 7u) * skew;
+      for (int r = 0; r < rounds; ++r) __builtin_amdgcn_s_sleep(16);
+    }
     __hip_atomic_store((gu32*)(flags + tile), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Sum over the lanes j, j + 16, j + 32, j + 48 (the column groups holding one item's units): two
@@ -210,7 +240,8 @@ SGNN_DEV void ln_stats_x(const f32x4 (&r)[KQ], float& mean, float& rstd) {
 template <int MODE>
 SGNN_DEV void step_tail(const Step16Args& a, const NodeW<2, MODE>& W, float* scratch, float* xs, int64_t i,
                         bool valid, f32x4 h, f32x4 xo, int b, int j, int g, __amdgpu_buffer_rsrc_t ru,
-                        __amdgpu_buffer_rsrc_t rv) {
+                        __amdgpu_buffer_rsrc_t rv, int kk) {
+  (void)kk;  // the node-half buffer written (mode 0): the check build's tags
   const int ucol = 16 * b + 4 * g;
   f32x4 hr[KQ], yr[KQ], xnr[KQ];
   xchg(scratch, j, ucol, g, h, hr);
@@ -228,6 +259,11 @@ SGNN_DEV void step_tail(const Step16Args& a, const NodeW<2, MODE>& W, float* scr
     const int off = valid ? (int)i * (H * 4) + ucol * 4 : kBufDrop;
     st4_sc1(ru, off, u);
     st4_sc1(rv, off, v);
+#ifdef SGNN_HANDOFF_CHECK
+    if (g_hc && valid && g == 0)
+      __hip_atomic_store((gu32*)(hc_tags() + ((int64_t)kk * a.n + i) * 4 + b), a.epoch0 + (uint32_t)kk + 1u,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   } else {
     f32x4 hdr[KQ];
     xchg(scratch + 2 * 16 * LDX, j, ucol, g, relu4(mm(W.vba, W.wa, xnr)), hdr);
@@ -377,6 +413,8 @@ struct EdgePhase {
   const int32_t *lsend, *lrecv;
   int Et, i0, b, j, g, l;
   f32x4 pre[kPre][KQ];
+  int hc_k = 0, hc_slot = 0;  // check build: the layer, and the workgroup's slot in the hash table
+  uint32_t hc_ep = 0;         // check build: the phase the gathered rows were polled for
 
   // Encoder.edge_fn of one half from its endpoints' positions -> x (e0), rows kept in e0l
   SGNN_DEV void encode(f32x4 (&x)[KQ], const float (&xw1)[KQ], const float (&ps)[3], const float (&pr)[3], int hs,
@@ -535,6 +573,10 @@ struct EdgePhase {
     // the raw u / v rows of the next half stay in flight across the current half's MFMAs: summing them
     // here would put a wait for the loads just issued in front of those MFMAs
     f32x4 gu[KQ], gv[KQ];
+#ifdef SGNN_HANDOFF_CHECK
+    uint32_t tg_r[4], tg_s[4];
+    int hc_r = 0, hc_s = 0;
+#endif
     auto gather = [&](int hs) {  // clamped: harmless past the end
       const int e = hs + j, ec = e < Et ? e : Et - 1;
       int r = lrecv[ec], s = lsend[ec];
@@ -545,6 +587,48 @@ struct EdgePhase {
         gu[t] = ld4_sc1(ru, r * (H * 4) + (16 * t + 4 * g) * 4);
         gv[t] = ld4_sc1(rv, s * (H * 4) + (16 * t + 4 * g) * 4);
       }
+#ifdef SGNN_HANDOFF_CHECK
+      hc_r = r;
+      hc_s = s;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        if (!g_hc) break;
+        tg_r[w] = __hip_atomic_load((const gu32*)(hc_tags() + ((int64_t)hc_k * a.n + r) * 4 + w), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+        tg_s[w] = __hip_atomic_load((const gu32*)(hc_tags() + ((int64_t)hc_k * a.n + s) * 4 + w), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+      }
+#endif
+    };
+    // check build: the rows of half hs as used (tags against the polled phase, hashes for the final check)
+    auto note = [&](int hs) {
+#ifdef SGNN_HANDOFF_CHECK
+      if (!g_hc) return;
+      uint32_t hu = 2166136261u, hv = 2166136261u;
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) {
+        hu = hc_mix(hu, gu[t]);
+        hv = hc_mix(hv, gv[t]);
+      }
+      const int64_t slot = (((int64_t)hc_slot * a.L + hc_k) * kHcHalves + hs / 16) * 64 + l;
+      hc_hash(a)[2 * slot] = hu;
+      hc_hash(a)[2 * slot + 1] = hv;
+      if (hs + j < Et) {
+        bool bad = false;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) bad = bad || tg_r[w] != hc_ep || tg_s[w] != hc_ep;
+        if (bad) {
+          atomicAdd(g_hc + 1, 1u);
+          if (hc_print())
+            printf("SGNN-HANDOFF tag: wg %d layer %d wave %d lane %d edge %d recv %d (tile %d) tags %u %u %u %u "
+                   "send %d (tile %d) tags %u %u %u %u, polled for %u\n", (int)blockIdx.x, hc_k, b, l, hs + j, hc_r,
+                   hc_r / a.nt, tg_r[0], tg_r[1], tg_r[2], tg_r[3], hc_s, hc_s / a.nt, tg_s[0], tg_s[1], tg_s[2],
+                   tg_s[3], hc_ep);
+        }
+      }
+#else
+      (void)hs;
+#endif
     };
     EdgeVec ev;
 #pragma unroll
@@ -569,6 +653,7 @@ struct EdgePhase {
     for (int m = 0; m < kPre; ++m) {
       if (hs >= Et) break;
       f32x4 acc[KQ];
+      note(hs);
       if (owner_d && m == F) {   // formed by the donor wave (published with the barrier before the wait)
 #pragma unroll
         for (int t = 0; t < KQ; ++t) acc[t] = ld4(dbuf + ((b * KQ + t) * 64 + l) * 4) + (gu[t] + gv[t]);
@@ -590,6 +675,7 @@ struct EdgePhase {
     for (; hs < Et; hs += 16 * kWaves16) {   // halves past kPre: the e0 product here
       f32x4 x[KQ], acc[KQ];
       ld_e0(x, hs);
+      note(hs);
 #pragma unroll
       for (int t = 0; t < KQ; ++t) acc[t] = gu[t] + gv[t];
       gather(hs + 16 * kWaves16);
@@ -670,8 +756,10 @@ SGNN_DEV Node16Args node_args(const Step16Args& a, const Lay16& L, const Lay16* 
 template <bool FIRST, int MODE, bool E0G, int NSUB, int PUB>
 SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv, const float (&xw1)[KQ],
                          const int32_t* deps, int ndeps, const int32_t* lsend, const int32_t* lrecv, int Et, int i0,
-                         int cnt, int b, int j, int g, int l) {
-  const int tile = blockIdx.x;
+                         int cnt, int b, int j, int g, int l, int tile) {
+#if defined(SGNN_EXP_XCD_ORDER) && SGNN_EXP_XCD_ORDER == 2
+  tile = blockIdx.x;  // experiment: the remap NOT applied here (publish / e0 block by workgroup index)
+#endif
   float* sw0 = lds + cv.sw0;
   float* sw1 = lds + cv.sw1;
   float* svec = lds + cv.svec;
@@ -692,6 +780,9 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   const Node16Args nd = node_args(a, Lk, MODE == 0 ? &Ln : nullptr);
   float* sums = scratch + b * 16 * NSUB * LDX;
   EdgePhase<NSUB> ep{a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, sums, e0l, lsend, lrecv, Et, i0, b, j, g, l};
+  ep.hc_k = k;
+  ep.hc_slot = (int)blockIdx.x;
+  ep.hc_ep = a.epoch0 + (uint32_t)k + 1;
   mark(ps < 0 ? -1 : ps + 1);
   // Between the pre-wait products: publish phase k + 1 (u_k / v_k, stored by the previous stage; the
   // drain of those write-through stores overlaps the first product), then request this layer's node
@@ -704,7 +795,7 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   constexpr int pub_at = PUB;
   auto hook = [&](int m) {
     if (m == pub_at) {
-      publish(a.flags, tile, ep_k);
+      publish(a.flags, tile, ep_k, a.skew);
       mark(ps < 0 ? -1 : ps + 2);
       W.load_first(nd, b, j, g);
     }
@@ -720,6 +811,22 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   if (ep.donor) ep.template prewait<FIRST, true>(xw1, hook);
   else ep.template prewait<FIRST, false>(xw1, hook);
   mark(ps < 0 ? -1 : ps + 3);
+#ifdef SGNN_EXP_XHALF_EARLY
+  // experiment (round-4 record): the node MLP's x half W_x x of every sub-tile before
+  // the wait, as ONE accumulator chain -- mm_cat's second chain, so the sum is bit for bit the same
+  f32x4 xh[NSUB];
+#pragma unroll
+  for (int s = 0; s < NSUB; ++s) {
+    f32x4 xq[KQ], a1 = zero4();
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) xq[q] = ld4(lds + cv.xs + (16 * s + j) * LDX + 16 * q + 4 * g);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a1 = mfma16(W.w1x[q][c], xq[q][c], a1);
+    xh[s] = a1;
+  }
+#endif
   poll.wait(deps, ndeps, a.flags, ep_k, l, a.poll_limit);
   mark(ps < 0 ? -1 : ps + 4);
   ep.postwait(ru, rv, k == 1);
@@ -767,9 +874,19 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
       }
       xo = ld4(xs + (16 * s + j) * LDX + 16 * b + 4 * g);
     }
+#ifdef SGNN_EXP_XHALF_EARLY
+    f32x4 a0 = W.vb1;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a0 = mfma16(W.w1a[q][c], ag[q][c], a0);
+    const f32x4 h = relu4(a0 + xh[s]);
+#else
     const f32x4 h = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));  // graph_network.py:220
+#endif
     if (k == 1 && s == 0) mark(53);
-    step_tail<MODE>(a, W, scratch, xs + 16 * s * LDX, i0 + 16 * s + j, 16 * s + j < cnt, h, xo, b, j, g, ru1, rv1);
+    step_tail<MODE>(a, W, scratch, xs + 16 * s * LDX, i0 + 16 * s + j, 16 * s + j < cnt, h, xo, b, j, g, ru1, rv1,
+                    k + 1);
   }
   mark(ps < 0 ? -1 : ps + 6);
   if constexpr (MODE == 0) {
@@ -778,6 +895,54 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   }
   mark(ps < 0 ? -1 : ps + 7);
 }
+
+#ifdef SGNN_HANDOFF_CHECK
+// Check build, after the last layer: every workgroup publishes a final phase (epoch0 + L + 1: no layer
+// uses it, the next step starts at epoch0 + L + 2) in its own slot and waits until EVERY slot holds it
+// (all workgroups resident; a grid barrier, once), so every node-half row of the step has settled.
+// Then each wave re-gathers every half it used in every layer (sc1 loads) and compares the hashes.
+SGNN_DEV void hc_final(const Step16Args& a, int tile, const int32_t* lsend, const int32_t* lrecv, int Et, int b,
+                       int j, int g, int l) {
+  if (a.poll_limit < 0 || !g_hc) return;  // the forced-timeout test hook / no buffer: nothing to check
+#if defined(SGNN_EXP_XCD_ORDER) && SGNN_EXP_XCD_ORDER == 2
+  tile = blockIdx.x;  // the slot the layers published in
+#endif
+  const uint32_t fin = a.epoch0 + (uint32_t)a.L + 1u;
+  publish(a.flags, tile, fin, 0);
+  const int G = (int)gridDim.x;
+  for (int it = 0; it < (1 << 22); ++it) {
+    bool ok = true;
+    for (int t = l; t < G; t += 64)
+      ok = ok && __hip_atomic_load((const gu32*)(a.flags + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= fin;
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (threadIdx.x == 0) atomicAdd(g_hc + 3, 1u);
+  const int64_t nH = (int64_t)a.n * H;
+  for (int k = 0; k < a.L; ++k) {
+    const __amdgpu_buffer_rsrc_t ru = buf_rsrc(a.uvl + (2 * k) * nH), rv = buf_rsrc(a.uvl + (2 * k + 1) * nH);
+    for (int hs = 16 * b; hs < Et; hs += 16 * kWaves16) {
+      const int e = hs + j, ec = e < Et ? e : Et - 1;
+      const int r = lrecv[ec], s = lsend[ec];
+      uint32_t hu = 2166136261u, hv = 2166136261u;
+#pragma unroll
+      for (int t = 0; t < KQ; ++t) {
+        hu = hc_mix(hu, ld4_sc1(ru, r * (H * 4) + (16 * t + 4 * g) * 4));
+        hv = hc_mix(hv, ld4_sc1(rv, s * (H * 4) + (16 * t + 4 * g) * 4));
+      }
+      const int64_t slot = (((int64_t)blockIdx.x * a.L + k) * kHcHalves + hs / 16) * 64 + l;
+      const bool bu = hu != hc_hash(a)[2 * slot], bv = hv != hc_hash(a)[2 * slot + 1];
+      if (bu || bv) {
+        atomicAdd(g_hc, 1u);
+        if (hc_print())
+          printf("SGNN-HANDOFF stale: wg %d layer %d wave %d lane %d edge %d (of %d) recv %d (tile %d)%s send %d "
+                 "(tile %d)%s\n", (int)blockIdx.x, k, b, l, e, Et, r, r / a.nt, bu ? " STALE" : "", s, s / a.nt,
+                 bv ? " STALE" : "");
+      }
+    }
+  }
+}
+#endif
 
 template <int DIM, int KQF, bool E0G, int NSUB>
 __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) void k_step16(Step16Args a_) {
@@ -788,7 +953,15 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
                              __builtin_amdgcn_kernarg_segment_ptr();
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
-  const int tile = blockIdx.x, nt = a.nt, cap = a.cap, n = a.n;
+#ifdef SGNN_EXP_XCD_ORDER
+  // experiment (round-4 record): XCD-contiguous tiles -- blocks b, b + 8, ... share an
+  // XCD and take consecutive tiles; XCD x (= b mod 8) owns G / 8 (+1 for x < G mod 8) of them: a bijection
+  const int xq = (int)gridDim.x / 8, xr = (int)gridDim.x % 8, xc = (int)blockIdx.x % 8;
+  const int tile = xc * xq + min(xc, xr) + (int)blockIdx.x / 8;
+#else
+  const int tile = blockIdx.x;
+#endif
+  const int nt = a.nt, cap = a.cap, n = a.n;
   const int i0 = tile * nt;
   const int cnt = min(nt, n - i0);
   const Carve cv = carve(n, DIM, nt, cap, E0G);
@@ -1119,7 +1292,7 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     const f32x4 h = relu4(mm(vb1, w1f, xf));
     const int64_t nH = (int64_t)n * H;
     step_tail<0>(a, E, lds + cv.scratch, lds + cv.xs + 16 * s * LDX, i0 + 16 * s + j, 16 * s + j < cnt, h, zero4(),
-                 b, j, g, buf_rsrc(a.uvl), buf_rsrc(a.uvl + nH));
+                 b, j, g, buf_rsrc(a.uvl), buf_rsrc(a.uvl + nH), 0);
   }
   mark(2);  // u_0 / v_0 are published by layer 0's pre-wait
 
@@ -1131,13 +1304,18 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   // there cost 0.5-1.6 %); same-box A/Bs, DESIGN.md section 5
   auto layers = [&](auto pub) {
     constexpr int P = decltype(pub)::value;
-    step_layer<true, 0, E0G, NSUB, P>(a, 0, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+    step_layer<true, 0, E0G, NSUB, P>(a, 0, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l, tile);
     for (int k = 1; k < a.L - 1; ++k)
-      step_layer<false, 0, E0G, NSUB, P>(a, k, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
-    step_layer<false, 1, E0G, NSUB, P>(a, a.L - 1, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l);
+      step_layer<false, 0, E0G, NSUB, P>(a, k, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l,
+                                         tile);
+    step_layer<false, 1, E0G, NSUB, P>(a, a.L - 1, lds, cv, xw1, deps, ndeps, lsend, lrecv, Et, i0, cnt, b, j, g, l,
+                                       tile);
   };
   if (Et <= 16 * kWaves16) layers(std::integral_constant<int, 0>{});
   else layers(std::integral_constant<int, kPubAt>{});
+#ifdef SGNN_HANDOFF_CHECK
+  hc_final(a, tile, lsend, lrecv, Et, b, j, g, l);
+#endif
 }
 
 }  // namespace
@@ -1219,6 +1397,12 @@ int step16_launch(const Step16Args& a_in, hipStream_t s) {
 }
 
 }  // namespace sgnn
+
+#ifdef SGNN_HANDOFF_CHECK
+extern "C" int sgnn_set_handoff_check(uint32_t* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_hc), &buf, sizeof(buf)) == hipSuccess ? 0 : 3;
+}
+#endif
 
 #ifdef SGNN_PROBE
 extern "C" int sgnn_set_probe16(uint64_t* buf) {

@@ -14,6 +14,7 @@ Data layout in HBM (per graph of n particles, hidden H, cap K):
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -125,7 +126,7 @@ class StepWorkspace:
                                  u=self.u.data_ptr(), v=self.v.data_ptr(), agg=self.agg.data_ptr(),
                                  cin=self.cin.data_ptr(), cout=self.cout.data_ptr(),
                                  u2=_ptr(self.u2), v2=_ptr(self.v2), uvl=0, step_flags=0, step_deg=0,
-                                 step_poll_limit=0)
+                                 step_poll_limit=0, step_skew=int(os.environ.get("SGNN_STEP_SKEW", "0")))
         self.device = device
         self.one_launch = one_launch   # False: never allocate them (calls take the kernel sequence)
 

@@ -57,9 +57,16 @@ def _check_grads(sim_named, state, rel=5e-4, prefix=""):
     (48, 80, 3, 2),     # latent != mlp_hidden_dim, nmlp_layers 3 (4 Linears per MLP)
     (128, 128, 2, 3),   # H = 128, 3D
 ])
-def test_epd_forward_backward_matches_oracle(latent, hidden, nmlp, dim):
-    """gnn(x, ei, e).backward() == oracle autograd (float64) per parameter and per input."""
+def test_epd_forward_backward_matches_oracle(latent, hidden, nmlp, dim, monkeypatch):
+    """gnn(x, ei, e).backward() == oracle autograd (float64) per parameter and per input.
+    At the fused widths (64/64/1, 128/128/2) every InteractionNetwork of the
+    Processor runs its forward and backward on the training step's fused layer
+    kernels (sgnn_amd/fused_block.py; counted), elsewhere the GEMM chain."""
     from oracle import sgnn_oracle as O
+    from sgnn_amd import fused_block
+    calls = []
+    real = fused_block.block_backward
+    monkeypatch.setattr(fused_block, "block_backward", lambda *a: calls.append(1) or real(*a))
     sim, osim, state, seq, types_, _ = _setup(latent, hidden, nmlp, dim)
     pos = torch.from_numpy(seq[:, :11])
     n = pos.shape[0]
@@ -77,16 +84,23 @@ def test_epd_forward_backward_matches_oracle(latent, hidden, nmlp, dim):
     assert got.grad_fn is not None
     _close(got.detach().cpu().numpy(), ref.detach().numpy(), what=f"EPD L{latent} H{hidden} nmlp{nmlp}")
     (got * w.cuda()).sum().backward()
+    assert len(calls) == (3 if latent == hidden and latent in (64, 128) else 0), calls
     worst = _check_grads(epd.named_parameters(prefix="_encode_process_decode"), state)
     _grad_close(nf_g.grad.cpu().numpy(), nf.grad.numpy(), "d node_features", rel=5e-4)
     _grad_close(ef_g.grad.cpu().numpy(), ef.grad.numpy(), "d edge_features", rel=5e-4)
     print(f"L{latent} H{hidden} nmlp{nmlp}: worst relative grad error {worst:.3e}")
 
 
-def test_module_forwards_backward_match_oracle():
+def test_module_forwards_backward_match_oracle(monkeypatch):
     """Encoder / InteractionNetwork / Processor / Decoder each on their own under
-    autograd, with the input latents' gradients (x, e) and a shuffled edge order."""
+    autograd, with the input latents' gradients (x, e) and a shuffled edge order
+    (the fused block's COO -> CSR permutation both ways)."""
     from oracle import sgnn_oracle as O
+    from sgnn_amd import fused_block
+    calls = []
+    real = fused_block.block_backward
+    monkeypatch.setattr(fused_block, "block_backward", lambda *a: calls.append(1) or real(*a))
+    fused_block_calls = lambda: len(calls)
     sim, osim, state, seq, types_, _ = _setup(64, 64, 1, 2)
     pos = torch.from_numpy(seq[:, :11])
     n = pos.shape[0]
@@ -111,6 +125,7 @@ def test_module_forwards_backward_match_oracle():
     _check_grads(epd._processor.gnn_stacks[1].named_parameters(prefix=pre + "_processor.gnn_stacks.1"), state)
     _grad_close(xg.grad.cpu().numpy(), xr.grad.numpy(), "InteractionNetwork dx", rel=5e-4)
     _grad_close(eg.grad.cpu().numpy(), er.grad.numpy(), "InteractionNetwork de", rel=5e-4)
+    assert fused_block_calls(), "the InteractionNetwork backward did not run the fused kernels"
     # Processor, Encoder, Decoder
     for v in state.values():
         v.grad = None

@@ -4,6 +4,7 @@
 #   bash tools/gpu.sh tests [pytest -k expr]     every -m gpu test (or a -k subset)   -> gpurun_out/t.log
 #   bash tools/gpu.sh smoke                      __graft_entry__.smoke()               -> gpurun_out/smoke.log
 #   bash tools/gpu.sh bench [bench.py args]      one bench line                        -> gpurun_out/bench.json
+#   bash tools/gpu.sh handoff VARIANT [SKEW]    the step's hand-off check build (base / xcd1 / xcd2 / xhalf)
 #   bash tools/gpu.sh bounds128                  H = 128 gradient tests on the bounds-checked library
 #   bash tools/gpu.sh profile TAG WORKLOAD MODE [bench.py args]
 #        rocprofv3 kernel trace (--stats, durations) + separate FETCH_SIZE / WRITE_SIZE passes of the same
@@ -30,6 +31,13 @@ case "$step" in
     timeout -k 10 900 python -u bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err \
       || { tail -20 gpurun_out/bench.err; exit 1; }
     python -c "import json; d = json.load(open('gpurun_out/bench.json')); print(len(open('gpurun_out/bench.json').read()), 'bytes;', d['metric'], d['value'], d['ms_per_step'], d.get('roofline', {}).get('frac'))" ;;
+  handoff)
+    # the one-launch step's hand-off check build (tools/exp_handoff.py): VARIANT [SKEW]
+    V=$1 S=${2:-0}
+    timeout -k 10 400 python -u tools/exp_handoff.py run "$V" "$S" > "gpurun_out/handoff_${V}_s${S}.log" 2>&1 \
+      || { tail -30 "gpurun_out/handoff_${V}_s${S}.log"; exit 1; }
+    mkdir -p gpurun_out/profiles && cp "gpurun_out/handoff_${V}_s${S}.log" gpurun_out/profiles/
+    tail -1 "gpurun_out/handoff_${V}_s${S}.log" ;;
   bounds128)
     timeout -k 10 600 python -u tools/exp_debug_bounds.py train128 > gpurun_out/bounds128.log 2>&1 \
       || { tail -30 gpurun_out/bounds128.log; exit 1; }
