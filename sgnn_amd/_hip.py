@@ -12,7 +12,9 @@ from typing import Optional
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libsgnn_hip.so")
+# SGNN_LIB: an experiment build of the same library (tools/exp_ab.py, tools/exp_handoff.py) in place of the
+# product one -- for same-box A/Bs of the test suite; unset in every product run
+LIB_PATH = os.environ.get("SGNN_LIB") or os.path.join(HERE, "_lib", "libsgnn_hip.so")
 
 SGNN_OK, SGNN_ERR_INVALID, SGNN_ERR_UNSUPPORTED, SGNN_ERR_HIP, SGNN_ERR_STEP_TIMEOUT = 0, 1, 2, 3, 4
 

@@ -52,6 +52,7 @@ struct Step16Args {
   int32_t *deg_out, *nbr_out;  // optional: the radius graph as padded lists [n], [n][cap]
   int poll_limit;      // polls per wait before the error word is set (< 0: test hook, set it at the first wait)
   int skew;            // test knob (sgnn_step_ws.step_skew): tile-dependent sleep before each publish, 0 = off
+  int tile_order;      // 0: tile = workgroup index; 1: XCD-contiguous tiles (k_step16)
   // outputs
   float *pred, *next_pos, *window_out;
 };

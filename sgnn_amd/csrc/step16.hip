@@ -138,7 +138,24 @@ SGNN_DEV uint32_t hc_mix(uint32_t h, f32x4 v) {
   for (int c = 0; c < 4; ++c) h = (h ^ __builtin_bit_cast(uint32_t, v[c])) * 16777619u;
   return h;
 }
-SGNN_DEV bool hc_print() { return atomicAdd(g_hc + 2, 1u) < 48u; }
+// the reports are out-of-line calls: printf inlined into the unrolled layer code made the check build's
+// compile take 15+ minutes
+__attribute__((noinline)) __device__ void hc_report_tag(int wg, int k, int b, int l, int e, int r, int rt, uint32_t r0,
+                                                       uint32_t r1, uint32_t r2, uint32_t r3, int s, int st, uint32_t s0,
+                                                       uint32_t s1, uint32_t s2, uint32_t s3, uint32_t ep) {
+  atomicAdd(g_hc + 1, 1u);
+  if (atomicAdd(g_hc + 2, 1u) < 48u)
+    printf("SGNN-HANDOFF tag: wg %d layer %d wave %d lane %d edge %d recv %d (tile %d) tags %u %u %u %u "
+           "send %d (tile %d) tags %u %u %u %u, polled for %u\n", wg, k, b, l, e, r, rt, r0, r1, r2, r3, s, st, s0,
+           s1, s2, s3, ep);
+}
+__attribute__((noinline)) __device__ void hc_report_stale(int wg, int k, int b, int l, int e, int Et, int r, int rt,
+                                                         int bu, int s, int st, int bv) {
+  atomicAdd(g_hc, 1u);
+  if (atomicAdd(g_hc + 2, 1u) < 48u)
+    printf("SGNN-HANDOFF stale: wg %d layer %d wave %d lane %d edge %d (of %d) recv %d (tile %d)%s send %d "
+           "(tile %d)%s\n", wg, k, b, l, e, Et, r, rt, bu ? " STALE" : "", s, st, bv ? " STALE" : "");
+}
 #endif
 
 // Per-tile counters of the sender tiles `deps` (up to 256, all requested at once).  Every wave polls for
@@ -617,14 +634,9 @@ struct EdgePhase {
         bool bad = false;
 #pragma unroll
         for (int w = 0; w < 4; ++w) bad = bad || tg_r[w] != hc_ep || tg_s[w] != hc_ep;
-        if (bad) {
-          atomicAdd(g_hc + 1, 1u);
-          if (hc_print())
-            printf("SGNN-HANDOFF tag: wg %d layer %d wave %d lane %d edge %d recv %d (tile %d) tags %u %u %u %u "
-                   "send %d (tile %d) tags %u %u %u %u, polled for %u\n", (int)blockIdx.x, hc_k, b, l, hs + j, hc_r,
-                   hc_r / a.nt, tg_r[0], tg_r[1], tg_r[2], tg_r[3], hc_s, hc_s / a.nt, tg_s[0], tg_s[1], tg_s[2],
-                   tg_s[3], hc_ep);
-        }
+        if (bad)
+          hc_report_tag((int)blockIdx.x, hc_k, b, l, hs + j, hc_r, hc_r / a.nt, tg_r[0], tg_r[1], tg_r[2], tg_r[3], hc_s,
+                        hc_s / a.nt, tg_s[0], tg_s[1], tg_s[2], tg_s[3], hc_ep);
       }
 #else
       (void)hs;
@@ -932,13 +944,7 @@ SGNN_DEV void hc_final(const Step16Args& a, int tile, const int32_t* lsend, cons
       }
       const int64_t slot = (((int64_t)blockIdx.x * a.L + k) * kHcHalves + hs / 16) * 64 + l;
       const bool bu = hu != hc_hash(a)[2 * slot], bv = hv != hc_hash(a)[2 * slot + 1];
-      if (bu || bv) {
-        atomicAdd(g_hc, 1u);
-        if (hc_print())
-          printf("SGNN-HANDOFF stale: wg %d layer %d wave %d lane %d edge %d (of %d) recv %d (tile %d)%s send %d "
-                 "(tile %d)%s\n", (int)blockIdx.x, k, b, l, e, Et, r, r / a.nt, bu ? " STALE" : "", s, s / a.nt,
-                 bv ? " STALE" : "");
-      }
+      if (bu || bv) hc_report_stale((int)blockIdx.x, k, b, l, e, Et, r, r / a.nt, bu, s, s / a.nt, bv);
     }
   }
 }
@@ -953,14 +959,18 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
                              __builtin_amdgcn_kernarg_segment_ptr();
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
+  // The tile this workgroup owns.  tile_order 1 (and the experiment builds): XCD-contiguous tiles -- blocks
+  // b, b + 8, ... share an XCD under the dispatch order and take consecutive tiles, so the sender tiles of a
+  // tile (its lattice neighbours) mostly share its L2: XCD x (= b mod 8) owns G / 8 (+1 for x < G mod 8)
+  // consecutive tiles, a bijection.  EVERY use of the tile index (publish slot, dependency list, e0 block)
+  // takes this one value (step_layer's `tile` argument); placement is a speed matter only.
 #ifdef SGNN_EXP_XCD_ORDER
-  // experiment (round-4 record): XCD-contiguous tiles -- blocks b, b + 8, ... share an
-  // XCD and take consecutive tiles; XCD x (= b mod 8) owns G / 8 (+1 for x < G mod 8) of them: a bijection
-  const int xq = (int)gridDim.x / 8, xr = (int)gridDim.x % 8, xc = (int)blockIdx.x % 8;
-  const int tile = xc * xq + min(xc, xr) + (int)blockIdx.x / 8;
+  const bool xcd_order = true;
 #else
-  const int tile = blockIdx.x;
+  const bool xcd_order = a.tile_order != 0;
 #endif
+  const int xq = (int)gridDim.x / 8, xr = (int)gridDim.x % 8, xc = (int)blockIdx.x % 8;
+  const int tile = xcd_order ? xc * xq + min(xc, xr) + (int)blockIdx.x / 8 : (int)blockIdx.x;
   const int nt = a.nt, cap = a.cap, n = a.n;
   const int i0 = tile * nt;
   const int cnt = min(nt, n - i0);
