@@ -250,62 +250,91 @@ SGNN_DEV void ln_stats_x(const f32x4 (&r)[KQ], float& mean, float& rstd) {
   rstd = __builtin_amdgcn_rsqf(xg_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / H) + 1e-5f);
 }
 
-// Node update of the tile (16 item rows, `valid` rows written) from the first
-// Linear's post-ReLU output h: last Linear, LayerNorm, + residual xo -> x
-// (LDS rows xs), then u, v of the next layer (mode 0, sc1 rows) or decoder +
-// integrator + window shift (mode 1).  Same arithmetic as fwd16.hip node_tail.
-template <int MODE>
-SGNN_DEV void step_tail(const Step16Args& a, const NodeW<2, MODE>& W, float* scratch, float* xs, int64_t i,
-                        bool valid, f32x4 h, f32x4 xo, int b, int j, int g, __amdgpu_buffer_rsrc_t ru,
+// Node update of the tile's NS 16-item sub-tiles (item rows 16 s + j; `cnt` valid rows in all) from the
+// first Linear's post-ReLU outputs h[s]: last Linear, LayerNorm, + residual xo -> x (LDS rows xs), then u, v
+// of the next layer (mode 0, sc1 rows) or decoder + integrator + window shift (mode 1).  Same arithmetic
+// as fwd16.hip node_tail.  The sub-tiles go through each exchange together (round 5): one workgroup
+// barrier per exchange for both, and two independent MFMA chains between them (sub-tile s's exchange
+// buffers: scratch rows 48 s .. 48 s + 47).
+template <int NS>
+SGNN_DEV void xchg_n(float* buf, int sstride, int j, int ucol, int g, const f32x4 (&v)[NS], f32x4 (&out)[NS][KQ]) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) st4(buf + s * sstride + j * LDX + ucol, v[s]);
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) out[s][q] = ld4(buf + s * sstride + j * LDX + 16 * q + 4 * g);
+}
+
+template <int MODE, int NS>
+SGNN_DEV void step_tail(const Step16Args& a, const NodeW<2, MODE>& W, float* scratch, float* xs, int64_t i0, int cnt,
+                        const f32x4 (&h)[NS], const f32x4 (&xo)[NS], int b, int j, int g, __amdgpu_buffer_rsrc_t ru,
                         __amdgpu_buffer_rsrc_t rv, int kk) {
   (void)kk;  // the node-half buffer written (mode 0): the check build's tags
+  constexpr int SB = 48 * LDX;
   const int ucol = 16 * b + 4 * g;
-  f32x4 hr[KQ], yr[KQ], xnr[KQ];
-  xchg(scratch, j, ucol, g, h, hr);
-  const f32x4 y = mm(W.vb2, W.w2, hr);
-  xchg(scratch + 16 * LDX, j, ucol, g, y, yr);
-  float mean, rstd;
-  ln_stats_x(yr, mean, rstd);
-  f32x4 xn;
+  f32x4 hr[NS][KQ], yr[NS][KQ], xnr[NS][KQ], y[NS], xn[NS];
+  xchg_n<NS>(scratch, SB, j, ucol, g, h, hr);
 #pragma unroll
-  for (int c = 0; c < 4; ++c) xn[c] = (y[c] - mean) * rstd * W.vg[c] + W.vbb[c] + xo[c];  // LN (+ :176 residual)
-  xchg(xs, j, ucol, g, xn, xnr);
+  for (int s = 0; s < NS; ++s) y[s] = mm(W.vb2, W.w2, hr[s]);
+  xchg_n<NS>(scratch + 16 * LDX, SB, j, ucol, g, y, yr);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    float mean, rstd;
+    ln_stats_x(yr[s], mean, rstd);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) xn[s][c] = (y[s][c] - mean) * rstd * W.vg[c] + W.vbb[c] + xo[s][c];  // LN + :176
+  }
+  xchg_n<NS>(xs, 16 * LDX, j, ucol, g, xn, xnr);
   if constexpr (MODE == 0) {
-    const f32x4 u = mm(W.vba, W.wa, xnr);
-    const f32x4 v = mm(zero4(), W.wb, xnr);
-    const int off = valid ? (int)i * (H * 4) + ucol * 4 : kBufDrop;
-    st4_sc1(ru, off, u);
-    st4_sc1(rv, off, v);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int64_t i = i0 + 16 * s + j;
+      const bool valid = 16 * s + j < cnt;
+      const f32x4 u = mm(W.vba, W.wa, xnr[s]);
+      const f32x4 v = mm(zero4(), W.wb, xnr[s]);
+      const int off = valid ? (int)i * (H * 4) + ucol * 4 : kBufDrop;
+      st4_sc1(ru, off, u);
+      st4_sc1(rv, off, v);
 #ifdef SGNN_HANDOFF_CHECK
-    if (g_hc && valid && g == 0)
-      __hip_atomic_store((gu32*)(hc_tags() + ((int64_t)kk * a.n + i) * 4 + b), a.epoch0 + (uint32_t)kk + 1u,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (g_hc && valid && g == 0)
+        __hip_atomic_store((gu32*)(hc_tags() + ((int64_t)kk * a.n + i) * 4 + b), a.epoch0 + (uint32_t)kk + 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
+    }
   } else {
-    f32x4 hdr[KQ];
-    xchg(scratch + 2 * 16 * LDX, j, ucol, g, relu4(mm(W.vba, W.wa, xnr)), hdr);
+    f32x4 hd[NS], hdr[NS][KQ];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) hd[s] = relu4(mm(W.vba, W.wa, xnr[s]));
+    xchg_n<NS>(scratch + 2 * 16 * LDX, SB, j, ucol, g, hd, hdr);
     const int D = a.dim;
-    if (b == 0) {
-      const f32x4 o = mm(W.vbo, W.wb, hdr);  // lanes g == 0 hold outputs 0..3
-      if (valid && g == 0) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (c <= D) a.pred[i * (D + 1) + c] = comp(o, c);
-        const float* p = a.pos_seq + i * a.T * D;  // learned_simulator.py:398-411
+    for (int s = 0; s < NS; ++s) {
+      const int64_t i = i0 + 16 * s + j;
+      const bool valid = 16 * s + j < cnt;
+      if (b == 0) {
+        const f32x4 o = mm(W.vbo, W.wb, hdr[s]);  // lanes g == 0 hold outputs 0..3
+        if (valid && g == 0) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          if (c >= D) break;
-          const float acc = __fadd_rn(__fmul_rn(comp(o, c), a.acc_std[c]), a.acc_mean[c]);
-          const float pT = p[(a.T - 1) * D + c], pT1 = p[(a.T - 2) * D + c];
-          const float np = __fadd_rn(pT, __fadd_rn(__fsub_rn(pT, pT1), acc));
-          a.next_pos[i * D + c] = np;
-          if (a.window_out) a.window_out[(i * a.T + a.T - 1) * D + c] = np;
+          for (int c = 0; c < 4; ++c)
+            if (c <= D) a.pred[i * (D + 1) + c] = comp(o, c);
+          const float* p = a.pos_seq + i * a.T * D;  // learned_simulator.py:398-411
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            if (c >= D) break;
+            const float acc = __fadd_rn(__fmul_rn(comp(o, c), a.acc_std[c]), a.acc_mean[c]);
+            const float pT = p[(a.T - 1) * D + c], pT1 = p[(a.T - 2) * D + c];
+            const float np = __fadd_rn(pT, __fadd_rn(__fsub_rn(pT, pT1), acc));
+            a.next_pos[i * D + c] = np;
+            if (a.window_out) a.window_out[(i * a.T + a.T - 1) * D + c] = np;
+          }
         }
+      } else if (b == 1 && g == 0 && valid && a.window_out) {  // evaluate.py:136-139
+        const float* p = a.pos_seq + i * a.T * D;
+        float* w = a.window_out + i * a.T * D;
+        for (int k = 0; k < (a.T - 1) * D; ++k) w[k] = p[k + D];
       }
-    } else if (b == 1 && g == 0 && valid && a.window_out) {  // evaluate.py:136-139
-      const float* p = a.pos_seq + i * a.T * D;
-      float* w = a.window_out + i * a.T * D;
-      for (int k = 0; k < (a.T - 1) * D; ++k) w[k] = p[k + D];
     }
   }
 }
@@ -876,6 +905,7 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   // u_{k+1} / v_{k+1} (mode 0); the decoder needs none
   const __amdgpu_buffer_rsrc_t ru1 = buf_rsrc(a.uvl + (MODE == 0 ? 2 * k + 2 : 0) * nH),
                                rv1 = buf_rsrc(a.uvl + (MODE == 0 ? 2 * k + 3 : 0) * nH);
+#ifndef SGNN_EXP_MERGE_NODE
 #pragma unroll
   for (int s = 0; s < NSUB; ++s) {
     if (s > 0) {  // (sub-tile 1's rows: written by no exchange of sub-tile 0)
@@ -892,14 +922,33 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
     for (int q = 0; q < KQ; ++q)
 #pragma unroll
       for (int c = 0; c < 4; ++c) a0 = mfma16(W.w1a[q][c], ag[q][c], a0);
-    const f32x4 h = relu4(a0 + xh[s]);
+    const f32x4 h[1] = {relu4(a0 + xh[s])};
 #else
-    const f32x4 h = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));  // graph_network.py:220
+    const f32x4 h[1] = {relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr))};  // graph_network.py:220
 #endif
     if (k == 1 && s == 0) mark(53);
-    step_tail<MODE>(a, W, scratch, xs + 16 * s * LDX, i0 + 16 * s + j, 16 * s + j < cnt, h, xo, b, j, g, ru1, rv1,
-                    k + 1);
+    const f32x4 xo1[1] = {xo};
+    step_tail<MODE, 1>(a, W, scratch, xs + 16 * s * LDX, i0 + 16 * s, cnt - 16 * s, h, xo1, b, j, g, ru1, rv1, k + 1);
   }
+#else
+  // experiment (round 5): both node sub-tiles through each exchange together (one barrier
+  // per exchange for the pair) -- failed the 3D two-example case on three boxes, not shipped
+  f32x4 hs[NSUB], xos[NSUB];
+#pragma unroll
+  for (int s = 0; s < NSUB; ++s) {
+    if (s > 0) {
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        ag[q] = ld4(ag1 + j * LDX + 16 * q + 4 * g);
+        xr[q] = ld4(xs + (16 * s + j) * LDX + 16 * q + 4 * g);
+      }
+      xo = ld4(xs + (16 * s + j) * LDX + 16 * b + 4 * g);
+    }
+    hs[s] = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));
+    xos[s] = xo;
+  }
+  step_tail<MODE, NSUB>(a, W, scratch, xs, i0, cnt, hs, xos, b, j, g, ru1, rv1, k + 1);
+#endif
   mark(ps < 0 ? -1 : ps + 6);
   if constexpr (MODE == 0) {
     nxt.store(sw0, sw1, svec, (float)(2 << k));  // W1e x 2^(k+1): exact
@@ -1276,6 +1325,7 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   float xw1[KQ] = {0.0f, 0.0f, 0.0f, 0.0f};  // Encoder.edge_fn W1 [H][dim + 1]: unit 16 t + j, k = g
 #pragma unroll
   for (int t = 0; t < KQ; ++t) xw1[t] = g <= DIM ? a.xe_w1[(16 * t + j) * (DIM + 1) + g] : 0.0f;
+  f32x4 eh[NSUB], ez[NSUB];
 #pragma unroll
   for (int s = 0; s < NSUB; ++s) {
     f32x4 xf[KQF];
@@ -1299,11 +1349,20 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
         }
         xf[q][c] = val;
       }
-    const f32x4 h = relu4(mm(vb1, w1f, xf));
-    const int64_t nH = (int64_t)n * H;
-    step_tail<0>(a, E, lds + cv.scratch, lds + cv.xs + 16 * s * LDX, i0 + 16 * s + j, 16 * s + j < cnt, h, zero4(),
-                 b, j, g, buf_rsrc(a.uvl), buf_rsrc(a.uvl + nH), 0);
+    eh[s] = relu4(mm(vb1, w1f, xf));
+    ez[s] = zero4();
   }
+#ifndef SGNN_EXP_MERGE_NODE
+#pragma unroll
+  for (int s = 0; s < NSUB; ++s) {
+    const f32x4 h1[1] = {eh[s]}, x1[1] = {ez[s]};
+    step_tail<0, 1>(a, E, lds + cv.scratch, lds + cv.xs + 16 * s * LDX, i0 + 16 * s, cnt - 16 * s, h1, x1, b, j, g,
+                    buf_rsrc(a.uvl), buf_rsrc(a.uvl + (int64_t)n * H), 0);
+  }
+#else
+  step_tail<0, NSUB>(a, E, lds + cv.scratch, lds + cv.xs, i0, cnt, eh, ez, b, j, g, buf_rsrc(a.uvl),
+                     buf_rsrc(a.uvl + (int64_t)n * H), 0);
+#endif
   mark(2);  // u_0 / v_0 are published by layer 0's pre-wait
 
   // ---- the interaction layers ------------------------------------------------------------------
