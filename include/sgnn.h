@@ -289,7 +289,10 @@ int sgnn_step_path(const sgnn_epd* model, const sgnn_step_in* in, const sgnn_ste
  * the error word is set.  sgnn_step_check reads that word once the call's work is done (it
  * synchronises `stream`, the one entry point that does) and returns SGNN_ERR_STEP_TIMEOUT when set --
  * the caller must treat that call's outputs as invalid.  The Python wrappers call it after every
- * predict_positions / rollout (learned_simulator.py:413-438, evaluate.py:117-145 sync on .cpu() too). */
+ * predict_positions / rollout (learned_simulator.py:413-438, evaluate.py:117-145 sync on .cpu() too).
+ * Processes that share one device (e.g. data-parallel ranks on one GPU) should opt out: a workspace
+ * without the one-launch buffers (uvl / step_flags / step_deg NULL; in Python StepWorkspace(one_launch=
+ * False), or SGNN_ONE_LAUNCH=0 in the environment) always runs the per-kernel sequence. */
 int sgnn_step_check(const sgnn_step_ws* ws, void* stream);
 /* Steps alternate win_a -> win_b -> win_a ...; step k writes out_pred[k][n][dim+1]
  * (normalised acceleration + strain) and out_pos[k][n][dim]. */

@@ -128,7 +128,9 @@ class StepWorkspace:
                                  u2=_ptr(self.u2), v2=_ptr(self.v2), uvl=0, step_flags=0, step_deg=0,
                                  step_poll_limit=0, step_skew=int(os.environ.get("SGNN_STEP_SKEW", "0")))
         self.device = device
-        self.one_launch = one_launch   # False: never allocate them (calls take the kernel sequence)
+        # False: never allocate them (calls take the kernel sequence).  SGNN_ONE_LAUNCH=0: the same for every
+        # workspace of the process (several processes sharing one device, include/sgnn.h "Co-residency")
+        self.one_launch = one_launch and os.environ.get("SGNN_ONE_LAUNCH", "1") != "0"
 
     def prepare_step(self, epd_struct, sin) -> bool:
         """Allocate the one-launch step's buffers when sgnn_step_path says calls with these
