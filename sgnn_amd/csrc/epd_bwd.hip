@@ -622,6 +622,78 @@ void k_edge_bwd64(EdgeBwdArgs a) {
   f32x4 s_dbl = {0.0f, 0.0f, 0.0f, 0.0f}, s_dg = s_dbl, s_db = s_dbl;   // units 4 (lane & 15) + c
   const int64_t E = a.rowptr[a.n];
   const int64_t nchunks = (E + kChunk - 1) / kChunk;
+#ifdef SGNN_EXP_EDGE_BWD_IDS
+  if constexpr (!DW1E) {
+    // Experiment (round 5, measured slower and not kept: C2 kernel 71.5 -> 76.3 us, step 1.933 -> 1.965 ms,
+    // profiles/r05_ab_edge_bwd_ids.txt): the receiver ids of chunk c + grid (and its rstd, the neighbouring
+    // receivers) requested before chunk c's dWl outer product, so the dependent gather of the dagg rows
+    // (recv[e] -> dagg[recv[e]]) is one round trip at the loop top instead of two.
+    float rs_n = 0.0f;
+    int rv_n = 0, nb_n = -1;
+    auto fetch_ids = [&](int64_t c) {
+      const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+      rs_n = 0.0f;
+      rv_n = 0;
+      nb_n = -1;
+      if (clamp_items(E - base) > 0) {
+        const int64_t ec = e < E ? e : E - 1;
+        rv_n = a.recv[ec];
+        rs_n = a.rstd[ec];
+        const int64_t q = j == 0 ? base - 1 : base + 32;
+        const bool has = j == 0 ? base > 0 : base + 32 < E;
+        nb_n = has ? a.recv[has ? q : base] : -1;
+      }
+    };
+    if ((int64_t)blockIdx.x < nchunks) fetch_ids(blockIdx.x);
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+      const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
+      const int nvalid = clamp_items(E - base);
+      const bool valid = e < E;
+      f32x16 dm[TH], yh[TH], h1[TH];
+      const float rs = rs_n;
+      const int rv = rv_n, nb = nb_n;
+      if (nvalid > 0) {  // tiles past the last valid one are not allocated
+        load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
+        load_tiled<TH>(yh, a.yh + tile * (32 * H));
+        load_tiled<TH>(h1, a.hs + tile * (32 * H));
+      } else {
+        zero<TH>(dm);
+        zero<TH>(yh);
+        zero<TH>(h1);
+      }
+      zero_if<TH>(dm, !valid);
+      zero_if<TH>(h1, !valid);
+      f32x16 dy[TH];
+      acc_layernorm_bwd<TH>(dm, yh, rs, a.gamma, dy);   // graph_network.py:148
+      zero_if<TH>(dy, !valid);
+#pragma unroll
+      for (int t = 0; t < TH; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];   // dgamma terms (dm = 0 off the edges)
+      swz_store_items(sA, j, dm);
+      swz_store_items(sB, j, yh);
+      wave_lds_sync();
+      s_db += swz_col_sums(sA);
+      s_dg += swz_col_sums(sB);
+      wave_lds_sync();
+      swz_store_items(sA, j, dy);
+      swz_store_items(sB, j, h1);
+      wave_lds_sync();
+      s_dbl += swz_col_sums(sA);
+      const int nb0 = __builtin_amdgcn_readlane(nb, 0), nb1 = __builtin_amdgcn_readlane(nb, 1);
+      if (c + gridDim.x < nchunks) fetch_ids(c + gridDim.x);   // in flight under the outer product
+      __syncthreads();
+      swz_outer(acc, bufA, 32 * tu, bufB, 32 * tv);
+      __syncthreads();
+      f32x16 dh[TH];
+      zero<TH>(dh);
+      swz_matvec_t(dh, wt, dy);
+      relu_mask<TH>(dh, h1, valid);
+      store_row_clayout_if<TH>(buf_rsrc(a.dh_rows + base * H), j * (4 * H), valid, dh);
+      segment_sum_rows<TH>(dh, rv, valid, nb0, nb1, tile, a.du, a.cin, a.cout);
+    }
+  } else
+#endif
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
     const int nvalid = clamp_items(E - base);

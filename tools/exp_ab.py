@@ -2,7 +2,8 @@
 process (the library is chosen before anything loads the default one), alternating A, B, A, B.
 
   python tools/exp_ab.py build NAME DEFINE[=V] ...   # here (CPU): _lib/libsgnn_hip_NAME.so
-  python tools/exp_ab.py run LIB_A,LIB_B WORKLOAD,... [reps]   # on the GPU box (LIB: default or NAME)"""
+  python tools/exp_ab.py run LIB_A,LIB_B WORKLOAD,... [reps]   # on the GPU box (LIB: default or NAME;
+                                                             # WORKLOAD: a rollout workload, train or train-c3)"""
 import json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -23,7 +24,10 @@ elif sys.argv[1] == "one":   # child: one bench leg on one library
     import bench
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    r = bench.bench_rollout(sys.argv[3], 20, 5, 1, 0, dev, 0, 0)
+    if sys.argv[3] in ("train", "train-c3"):   # the C2 / C3 training step (kernel = the edge backward)
+        r = bench.bench_train(sys.argv[3], 20, 5, 1, 0, dev, 0, 0)
+    else:
+        r = bench.bench_rollout(sys.argv[3], 20, 5, 1, 0, dev, 0, 0)
     print(json.dumps({"lib": sys.argv[2], "workload": sys.argv[3], "ms_per_step": r["ms_per_step"],
                       "kernel_us": r["roofline"]["live_us"]}))
 else:
