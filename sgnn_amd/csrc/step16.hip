@@ -459,6 +459,7 @@ struct EdgePhase {
   const int32_t *lsend, *lrecv;
   int Et, i0, b, j, g, l;
   f32x4 pre[kPre][KQ];
+  bool e0_hbm = false;        // e0l is the tile's HBM block (E0G), not LDS
   int hc_k = 0, hc_slot = 0;  // check build: the layer, and the workgroup's slot in the hash table
   uint32_t hc_ep = 0;         // check build: the phase the gathered rows were polled for
 
@@ -499,8 +500,14 @@ struct EdgePhase {
 
   SGNN_DEV void ld_e0(f32x4 (&x)[KQ], int hs) const {
     const int e = hs + j, ec = e < Et ? e : Et - 1;
+#ifdef SGNN_EXP_E0_SC1
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(e0l);   // experiment: L1-bypassing loads of the e0 rows
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) x[q] = ld4_sc1(r, (ec * LDX + 16 * q + 4 * g) * 4);
+#else
 #pragma unroll
     for (int q = 0; q < KQ; ++q) x[q] = ld4(e0l + ec * LDX + 16 * q + 4 * g);
+#endif
   }
 
   // before the wait: (FIRST) e0 of every half; W1e e0 of the first kPre halves
@@ -605,6 +612,12 @@ struct EdgePhase {
         f32x4 x[KQ];
         encode_item(x, hs, k);
       }
+      // Tiles whose e0 rows live in HBM (two node sub-tiles): every storing wave drains its e0 stores
+      // here, before any of those rows is loaded back.  Without it a plain load of a row this same wave
+      // stored earlier in the launch returned STALE data (round 5, DESIGN section 8.1: the merged
+      // node-phase experiment failed 4 of 10 launches; with this wait, or with L1-bypassing loads of the
+      // rows, 10 of 10 were clean) -- the hazard behind the round-4 two-sub-tile parity failures.
+      if (e0_hbm) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
 
@@ -821,6 +834,7 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   const Node16Args nd = node_args(a, Lk, MODE == 0 ? &Ln : nullptr);
   float* sums = scratch + b * 16 * NSUB * LDX;
   EdgePhase<NSUB> ep{a, sw0, sw1, svec, lds + cv.sxw, lds + cv.sxv, sums, e0l, lsend, lrecv, Et, i0, b, j, g, l};
+  ep.e0_hbm = E0G;
   ep.hc_k = k;
   ep.hc_slot = (int)blockIdx.x;
   ep.hc_ep = a.epoch0 + (uint32_t)k + 1;
