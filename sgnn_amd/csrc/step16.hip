@@ -613,10 +613,10 @@ struct EdgePhase {
         encode_item(x, hs, k);
       }
       // Tiles whose e0 rows live in HBM (two node sub-tiles): every storing wave drains its e0 stores
-      // here, before any of those rows is loaded back.  Without it a plain load of a row this same wave
-      // stored earlier in the launch returned STALE data (round 5, DESIGN section 8.1: the merged
-      // node-phase experiment failed 4 of 10 launches; with this wait, or with L1-bypassing loads of the
-      // rows, 10 of 10 were clean) -- the hazard behind the round-4 two-sub-tile parity failures.
+      // here, before any of those rows is loaded back by the same wave (plain stores, plain loads).  The
+      // merged node-phase experiment failed far less often with this wait; its cause
+      // is not established, the wait is kept: it orders this kernel's only same-launch store -> load of
+      // plain global rows, at no measurable cost.
       if (e0_hbm) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
