@@ -18,6 +18,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* Size of sgnn_step_ws.step_flags in 32-bit words, and the index of its error word. */
+#define SGNN_STEP_FLAG_WORDS 4128
+#define SGNN_STEP_FLAG_ERR 4096
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -264,7 +268,8 @@ typedef struct sgnn_step_ws { /* device buffers of one (n, T, dim, H, K) shape *
   float* uvl;           /* nlayers*2*n*H + (n+32)*K*(H+4) floats: every layer's node halves u_k, v_k
                            ([nlayers][2][n][H]), then room for the edge latents of tiles too large for
                            the kernel's LDS */
-  uint32_t* step_flags; /* [512] per-workgroup phase counters + error word (zeroed per call) */
+  uint32_t* step_flags; /* [SGNN_STEP_FLAG_WORDS] per-workgroup phase counters (64 B apart) + error word
+                           at [SGNN_STEP_FLAG_ERR] (zeroed per call) */
   int32_t* step_deg;    /* [n] neighbours kept per receiver */
   int32_t step_poll_limit; /* 0: default (~1 s of polling per wait before the error word is set);
                               < 0: test hook, every tile records a timeout at its first wait */

@@ -16,6 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # product one -- for same-box A/Bs of the test suite; unset in every product run
 LIB_PATH = os.environ.get("SGNN_LIB") or os.path.join(HERE, "_lib", "libsgnn_hip.so")
 
+STEP_FLAG_WORDS, STEP_FLAG_ERR = 4128, 4096   # include/sgnn.h SGNN_STEP_FLAG_WORDS / _ERR
 SGNN_OK, SGNN_ERR_INVALID, SGNN_ERR_UNSUPPORTED, SGNN_ERR_HIP, SGNN_ERR_STEP_TIMEOUT = 0, 1, 2, 3, 4
 
 c_void_p, c_int64, c_int32, c_float = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float

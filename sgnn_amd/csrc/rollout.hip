@@ -78,10 +78,16 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   a.e0_hbm = a.nt > 16 ? 1 : 0;   // two node sub-tiles: their e0 rows live in HBM
   a.poll_limit = ws->step_poll_limit;
   a.skew = ws->step_skew;
-  // XCD-contiguous tiles for one-sub-tile grids (<= 16 receivers per tile): a tile's sender tiles then mostly
-  // share its XCD's L2 (C1 r = 15 85.7 -> 83.9 us per step, r = 0.6 61.5 -> 60.6 in a same-box A/B); the
-  // two-sub-tile grids keep the dispatch order (t4800 101.6 -> 106.7, t8000 unchanged)
-  a.tile_order = a.nt <= 16 ? 1 : 0;
+  // XCD-contiguous tiles: a tile's sender tiles then mostly share its XCD's L2 (HBM/MALL traffic
+  // C1 r = 15 20.1 -> 16.7 MB per launch).  With the phase counters 64 B apart it is as fast as the
+  // dispatch order or faster at every size (profiles/r05_ab_flag_stride.txt, r05_ab_xcd_all_sizes.txt);
+  // with packed counters it was slower on some boxes (the counters of a tile's neighbours shared a
+  // line its producers kept writing: r05_ab_dispatch_order_packed_flags.txt)
+#if defined(SGNN_EXP_DISPATCH_ORDER)
+  a.tile_order = 0;   // experiment builds: the dispatch order (same-box A/Bs)
+#else
+  a.tile_order = 1;
+#endif
   size_t lds = step16_lds_bytes(a);
   if (lds > kStep16MaxLds && !a.e0_hbm) {  // the tile's e0 rows do not fit in LDS: keep them in HBM (ws->uvl's tail)
     a.e0_hbm = 1;
@@ -94,7 +100,7 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   return true;
 }
 
-constexpr size_t kStepFlagBytes = 512 * sizeof(uint32_t);
+constexpr size_t kStepFlagBytes = sgnn::kStepFlagWords * sizeof(uint32_t);
 constexpr int kMaxDevices = 64;
 
 // In-process co-residency guard (include/sgnn.h, "Co-residency"): per device, the stream and an event
@@ -176,7 +182,7 @@ static int predict_impl(const sgnn_epd* m, const sgnn_step_in* in, const float* 
   }
   // the per-kernel sequence: clear a previous call's error word so sgnn_step_check reads this call's
   if (step == 0 && ws->step_flags &&
-      hipMemsetAsync(ws->step_flags + kStep16MaxGrid, 0, sizeof(uint32_t), s) != hipSuccess)
+      hipMemsetAsync(ws->step_flags + kStepFlagErr, 0, sizeof(uint32_t), s) != hipSuccess)
     return check_launch("predict_positions: clearing the step error word");
   const int64_t n = in->n;
   const int T = in->T, d = in->dim;
@@ -348,7 +354,7 @@ extern "C" int sgnn_step_check(const sgnn_step_ws* ws, void* stream) {
   if (!ws->step_flags) return SGNN_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t word = 0;
-  if (hipMemcpyAsync(&word, ws->step_flags + kStep16MaxGrid, sizeof(word), hipMemcpyDeviceToHost, s) != hipSuccess ||
+  if (hipMemcpyAsync(&word, ws->step_flags + kStepFlagErr, sizeof(word), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return check_launch("step_check: reading the step error word");
   if (word != 0) {

@@ -12,6 +12,17 @@ constexpr int kStep16MaxCap = 64;   // neighbour cap (K, +1 without self loops)
 constexpr int kStep16MaxGrid = 256; // one workgroup per CU, every workgroup resident
 constexpr int kStep16MaxEx = 64;    // examples in the batch (their offsets are staged in LDS)
 constexpr size_t kStep16MaxLds = 160 * 1024;
+// Phase counters: one per workgroup, kStepFlagStride words apart (16 = 64 B: no two tiles' counters share
+// a 128-B line half, so a publish does not disturb the polls of the neighbouring tiles' consumers), and
+// the error word at the fixed index kStepFlagErr.  sgnn_step_ws.step_flags holds kStepFlagWords words.
+#ifndef SGNN_FLAG_STRIDE
+#define SGNN_FLAG_STRIDE 16
+#endif
+constexpr int kStepFlagStride = SGNN_FLAG_STRIDE;
+constexpr int kStepFlagErr = kStep16MaxGrid * 16;
+constexpr int kStepFlagWords = kStepFlagErr + 32;
+static_assert(kStepFlagStride >= 1 && kStepFlagStride <= 16, "flag stride");
+static_assert(kStepFlagWords == 4128 && kStepFlagErr == 4096, "include/sgnn.h SGNN_STEP_FLAG_WORDS / _ERR");
 
 // Weights of one InteractionNetwork (nmlp_layers 1): edge_fn = Linear(3H, H) ->
 // ReLU -> Linear(H, H) -> LayerNorm, node_fn = Linear(2H, H) -> ReLU ->

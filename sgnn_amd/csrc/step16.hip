@@ -58,6 +58,8 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 
 constexpr int kPollLimit = 1 << 21;   // ~1 s of polling: a hang becomes an error word
 constexpr int kMaxGrid = sgnn::kStep16MaxGrid;
+using sgnn::kStepFlagErr;
+using sgnn::kStepFlagStride;
 
 SGNN_DEV f32x4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, int voff) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -169,7 +171,7 @@ struct TilePoll {
 #pragma unroll
     for (int q = 0; q < kMaxGrid / 64; ++q)
       x[q] = lane + 64 * q < ndeps
-                 ? __hip_atomic_load((const gu32*)(flags + deps[lane + 64 * q]), __ATOMIC_RELAXED,
+                 ? __hip_atomic_load((const gu32*)(flags + deps[lane + 64 * q] * kStepFlagStride), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT)
                  : epoch;
   }
@@ -188,7 +190,7 @@ struct TilePoll {
   }
   SGNN_DEV void wait(const int32_t* deps, int ndeps, uint32_t* flags, uint32_t epoch, int lane, int limit) {
     if (limit < 0 && lane == 0)  // test hook (sgnn_step_ws.step_poll_limit < 0): the error path
-      __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)(flags + kStepFlagErr), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ok(v, epoch) || ok(w, epoch)) return;
     // two polls in flight: each check waits only for the older one, so the counters are sampled twice
     // per round trip
@@ -200,7 +202,7 @@ struct TilePoll {
       if (ok(w, epoch)) break;
       if (it >= limit) {
         if (lane == 0)
-          __hip_atomic_store((gu32*)(flags + kMaxGrid), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((gu32*)(flags + kStepFlagErr), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -219,7 +221,7 @@ SGNN_DEV void publish(uint32_t* flags, int tile, uint32_t epoch, int skew) {
       const int rounds = (int)((h >> 28) & 7u) * skew;
       for (int r = 0; r < rounds; ++r) __builtin_amdgcn_s_sleep(16);
     }
-    __hip_atomic_store((gu32*)(flags + tile), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(flags + tile * kStepFlagStride), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -988,7 +990,7 @@ SGNN_DEV void hc_final(const Step16Args& a, int tile, const int32_t* lsend, cons
   for (int it = 0; it < (1 << 22); ++it) {
     bool ok = true;
     for (int t = l; t < G; t += 64)
-      ok = ok && __hip_atomic_load((const gu32*)(a.flags + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= fin;
+      ok = ok && __hip_atomic_load((const gu32*)(a.flags + t * kStepFlagStride), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= fin;
     if (__all(ok)) break;
     __builtin_amdgcn_s_sleep(2);
   }

@@ -147,7 +147,7 @@ class StepWorkspace:
         n, H, K = self.n, self.H, self.K
         f32 = dict(dtype=torch.float32, device=self.device)
         self.uvl = torch.empty(epd_struct.nlayers * 2 * n * H + (n + 32) * K * (H + 4), **f32)
-        self.step_flags = torch.zeros(512, dtype=torch.int32, device=self.device)
+        self.step_flags = torch.zeros(_hip.STEP_FLAG_WORDS, dtype=torch.int32, device=self.device)
         self.step_deg = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.c.uvl, self.c.step_flags, self.c.step_deg = (self.uvl.data_ptr(), self.step_flags.data_ptr(),
                                                           self.step_deg.data_ptr())
@@ -175,7 +175,7 @@ class StepWorkspace:
 
     def step_timeout(self) -> bool:
         """True if a workgroup of the last one-launch step gave up waiting (its error word; tests)."""
-        return self.step_flags is not None and int(self.step_flags[256].item()) != 0
+        return self.step_flags is not None and int(self.step_flags[_hip.STEP_FLAG_ERR].item()) != 0
 
 
 def step_path(epd_struct, sin, ws: StepWorkspace):

@@ -31,6 +31,17 @@ def test_library_exports_every_header_symbol():
     assert lib.sgnn_version().decode().startswith("sgnn")
 
 
+def test_header_constants_match_python_mirror():
+    """The one-launch step's counter buffer size / error-word index (include/sgnn.h) as the
+    Python workspace allocates and reads them (the kernel's static_assert pins the C side)."""
+    from sgnn_amd import _hip
+    src = open(HEADER).read()
+    words = int(re.search(r"#define SGNN_STEP_FLAG_WORDS (\d+)", src).group(1))
+    err = int(re.search(r"#define SGNN_STEP_FLAG_ERR (\d+)", src).group(1))
+    assert (words, err) == (_hip.STEP_FLAG_WORDS, _hip.STEP_FLAG_ERR)
+    assert 256 * 16 <= err < words   # 256 counters 64 B apart, then the error word
+
+
 def test_host_only_size_queries():
     from sgnn_amd import _hip
     lib = _hip.load_library()
