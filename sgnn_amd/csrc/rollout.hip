@@ -72,7 +72,11 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   // the grid at one workgroup per CU (up to 32: the Taylor bars' 4,800 / 6,400 / 8,000 at 19 / 25 / 32)
   const int64_t cus = std::min<int64_t>(device_cus(), kStep16MaxGrid);
   if (cus < 1) return false;
+#ifdef SGNN_EXP_NT
+  a.nt = (int)std::max<int64_t>(SGNN_EXP_NT, (n + cus - 1) / cus);   // experiment builds: receivers per tile
+#else
   a.nt = (int)std::max<int64_t>(8, (n + cus - 1) / cus);
+#endif
   if (a.nt > kStep16MaxNT || (n + a.nt - 1) / a.nt > cus) return false;
   a.ecap_t = a.nt * cap;
   a.e0_hbm = a.nt > 16 ? 1 : 0;   // two node sub-tiles: their e0 rows live in HBM

@@ -2,7 +2,7 @@
 process (the library is chosen before anything loads the default one), alternating A, B, A, B.
 
   python tools/exp_ab.py build NAME DEFINE[=V] ...   # here (CPU): _lib/libsgnn_hip_NAME.so
-  python tools/exp_ab.py run LIB_A,LIB_B WORKLOAD,... [reps]   # on the GPU box (LIB: default or NAME;
+  python tools/exp_ab.py run LIB_A,LIB_B WORKLOAD,... [reps]   # on the GPU box (LIB: default or NAME, optionally @VAR=VALUE;
                                                              # WORKLOAD: a rollout workload, train or train-c3)"""
 import json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -20,7 +20,7 @@ if sys.argv[1] == "build":
 elif sys.argv[1] == "one":   # child: one bench leg on one library
     import torch
     from sgnn_amd import _hip
-    _hip.load_library(lib_path(sys.argv[2]))
+    _hip.load_library(lib_path(sys.argv[2].split("@")[0]))
     import bench
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -36,8 +36,11 @@ else:
     for wl in wls:
         for rep in range(reps):
             for lib in libs:
+                env = dict(os.environ)   # LIB@VAR=VALUE: the child runs with VAR=VALUE set (Python-side switches)
+                for kv in lib.split("@")[1:]:
+                    env[kv.split("=")[0]] = kv.split("=", 1)[1]
                 out = subprocess.run([sys.executable, os.path.abspath(__file__), "one", lib, wl], capture_output=True,
-                                     text=True, timeout=300, cwd=ROOT)
+                                     text=True, timeout=300, cwd=ROOT, env=env)
                 if out.returncode != 0:
                     print(out.stderr[-2000:])
                     sys.exit(out.returncode)
