@@ -1088,6 +1088,22 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   const float* src = a.pos_last ? a.pos_last : a.pos_seq + (int64_t)(a.T - 1) * DIM;
   const int pstride = a.pos_last ? DIM : a.T * DIM;
   const int n_ex = a.n_ex;
+  // one example (the rollout benches): the candidates are [0, n) without waiting for ex_ptr, so the first
+  // filter batch's positions are requested now, under the receivers' box and the weight loads (used below
+  // only if ex_ptr confirms [0, n))
+  constexpr int kBatch = 8;  // 64-candidate chunks whose loads are in flight together
+  const int Q1 = (((a.n + 3) >> 2) + 63) & ~63;
+  const bool pre_ok = n_ex == 1 && b * Q1 < a.n;
+  float pre[kBatch][DIM];
+  if (pre_ok) {
+    const int s0 = b * Q1, s1 = min(s0 + Q1, a.n);
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const int jj = min(s0 + 64 * u + l, s1 - 1);
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) pre[u][d] = src[(int64_t)jj * pstride + d];
+    }
+  }
   {  // example offsets; wave 0: the receivers' positions and their bounding box, grown by the margin
     const int64_t exv = (int)threadIdx.x <= n_ex ? a.ex_ptr[threadIdx.x] : 0;
     if (b == 0) {
@@ -1185,14 +1201,21 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     }
     const int s0 = cjb + b * Q, s1 = min(s0 + Q, cje);
     int kept = 0;
-    constexpr int kBatch = 8;  // 64-candidate chunks whose loads are in flight together
+    const bool use_pre = pre_ok && cjb == 0 && cje == a.n;   // then s0 = b Q1, s1 = min(s0 + Q1, n) as above
     for (int base = s0; base < s1; base += 64 * kBatch) {
       float pc[kBatch][DIM];
+      if (use_pre && base == s0) {
 #pragma unroll
-      for (int u = 0; u < kBatch; ++u) {
-        const int jj = min(base + 64 * u + l, s1 - 1);
+        for (int u = 0; u < kBatch; ++u)
 #pragma unroll
-        for (int d = 0; d < DIM; ++d) pc[u][d] = src[(int64_t)jj * pstride + d];
+          for (int d = 0; d < DIM; ++d) pc[u][d] = pre[u][d];
+      } else {
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+          const int jj = min(base + 64 * u + l, s1 - 1);
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) pc[u][d] = src[(int64_t)jj * pstride + d];
+        }
       }
 #pragma unroll
       for (int u = 0; u < kBatch; ++u) {
