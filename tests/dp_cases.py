@@ -11,11 +11,13 @@ import torch
 LR = 1e-3
 STEPS = 2
 # single scale: the real Taylor-bar sizes (120/160/200 x 40 lattices = 4,800 / 6,400 / 8,000 particles)
-SS_GRAPHS = [(120, 40), (160, 40), (200, 40)]
+SS_GRAPHS = [(120, 40), (160, 40), (200, 40), (100, 40)]
 SS_RANKS = [[0, 1], [2]]          # rank 0 holds two graphs (4,800 + 6,400), rank 1 one (8,000)
+SS_RANKS4 = [[0], [1], [2], [3]]  # four ranks, one graph each (4,800 / 6,400 / 8,000 / 4,000)
 # multi scale (nmlp_layers 2, two scales): one graph per rank, unequal sizes
-MS_GRAPHS = [(30, 14), (36, 12)]
+MS_GRAPHS = [(30, 14), (36, 12), (28, 15), (33, 12)]
 MS_RANKS = [[0], [1]]
+MS_RANKS4 = [[0], [1], [2], [3]]
 T_SS, T_MS = 11, 6
 
 
@@ -44,9 +46,10 @@ def _cat(items):
     return [torch.cat([it[k] for it in items], 0) for k in range(4)]
 
 
-def _result(tr, losses):
+def _result(tr, losses, sim):
     return {"loss": torch.tensor(losses, dtype=torch.float64), "grad": tr.flat.grad.detach().cpu().clone(),
-            "param": tr.flat.param.detach().cpu().clone()}
+            "param": tr.flat.param.detach().cpu().clone(),
+            "names": [(name, p.numel()) for name, p in sim.named_parameters()]}   # the flat layout
 
 
 def run_single_scale(graph_ids, overlap=False, force=False):
@@ -73,7 +76,7 @@ def run_single_scale(graph_ids, overlap=False, force=False):
         out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), counts, noise=noise.cuda())
         losses.append(float(out["loss"]))
     torch.cuda.synchronize()
-    return _result(tr, losses)
+    return _result(tr, losses, sim)
 
 
 def run_multi_scale(graph_ids, overlap=False, force=False):
@@ -102,7 +105,7 @@ def run_multi_scale(graph_ids, overlap=False, force=False):
         out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), noise=noise.cuda())
         losses.append(float(out["loss"]))
     torch.cuda.synchronize()
-    return _result(tr, losses)
+    return _result(tr, losses, sim)
 
 
 def run_single_scale_overlap(graph_ids):
@@ -136,5 +139,8 @@ CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, 
          "ss_overlap": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS),
          "ss_rccl1": (run_single_scale_rccl, SS_GRAPHS, [[0, 1, 2]]),
          "ms_overlap": (run_multi_scale_overlap, MS_GRAPHS, MS_RANKS),
-         "ms_rccl1": (run_multi_scale_rccl, MS_GRAPHS, [[0, 1]])}
+         "ms_rccl1": (run_multi_scale_rccl, MS_GRAPHS, [[0, 1]]),
+         # four ranks (the C3 / C5 sharding at world 4; gloo, the ranks share the one leased GPU)
+         "ss4_overlap": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS4),
+         "ms4": (run_multi_scale, MS_GRAPHS, MS_RANKS4)}
 RCCL_CASES = {"ss_rccl1", "ms_rccl1"}

@@ -1,4 +1,4 @@
-"""Whole-graph data parallelism on CPU (gloo, world_size 2): the Trainer's DP
+"""Whole-graph data parallelism on CPU (gloo, world_size 2 and 4): the Trainer's DP
 bookkeeping (sgnn_amd.train.DataParallel: N_global count, 1/N_global loss
 scaling, SUM all-reduce of one flat gradient buffer) must reproduce the
 single-process gradient of the concatenated batch (train.py:268 takes the
@@ -24,11 +24,14 @@ def _free_port():
     return port
 
 
+GRAPH_DIMS = [(10, 8), (12, 7), (9, 9), (11, 6)]   # unequal graph sizes
+
+
 def _graphs():
     from sgnn_amd import synthetic
     from oracle import sgnn_oracle as O
     out = []
-    for k, (nx, ny) in enumerate([(10, 8), (12, 7)]):   # unequal graph sizes
+    for k, (nx, ny) in enumerate(GRAPH_DIMS):
         seq = synthetic.trajectory(synthetic.lattice_2d(nx, ny), 12, seed=50 + k)
         pos, nxt = torch.from_numpy(seq[:, :11]), torch.from_numpy(seq[:, 11])
         strain = torch.from_numpy(np.random.default_rng(k).normal(0, 1, seq.shape[0]).astype(np.float32))
@@ -60,9 +63,10 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from sgnn_amd.train import DataParallel
+    from sgnn_amd.train import split_batch
     dp = DataParallel()
-    mine = [_graphs()[rank]]
-    n_local = mine[0][0].shape[0]
+    mine = [_graphs()[i] for i in split_batch(list(range(len(GRAPH_DIMS))), rank, world)]   # contiguous shares
+    n_local = sum(g[0].shape[0] for g in mine)
     n_global = dp.global_count(n_local, "cpu")
     flat, loss = _oracle_grads(mine, 1.0 / n_global)
     loss_t = torch.tensor([loss])
@@ -71,8 +75,8 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_whole_graph_dp_matches_single_process():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_whole_graph_dp_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -91,7 +95,8 @@ def test_whole_graph_dp_matches_single_process():
         np.testing.assert_allclose(flat, ref_flat.numpy(), rtol=1e-4, atol=1e-7)
         assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss)
     # every rank ends with the identical gradient -> identical Adam update
-    np.testing.assert_array_equal(res[0][2], res[1][2])
+    for r in res[1:]:
+        np.testing.assert_array_equal(res[0][2], r[2])
 
 
 def _layout_worker(rank, world, port, q):

@@ -6,13 +6,14 @@ its own ragged share of a global batch -- 4,800 + 6,400 particles on rank 0,
 scaling, the one all-reduce of gradient + loss sums, and the fused Adam after
 it.  Every rank must end with the loss, gradient and Adam-updated weights of
 ONE process running the concatenated batch (train.py:268 averages over the
-whole batch).  Tolerances: loss 1e-5 relative; gradients 2e-5 of the largest
+whole batch).  Tolerances: loss 1e-5 relative; gradients 2e-5 of the largest at 1-2 ranks, 4e-5 at 4
 (the ranks' partial sums are added in another order, fp32); weights within
 what that gradient error can move an Adam step (~lr x the relative gradient
 error, at most 2 lr per step).  `ss_rccl1`: the same single-scale step on a one-rank RCCL (nccl)
 group with the overlapped per-layer bucket all-reduces forced on (async collectives from the side
 stream, handles waited before Adam): the collective path C3 / C5 use, on real RCCL; `ms_overlap` /
-`ms_rccl1`: the multi-scale trainer's per-block buckets the same way."""
+`ms_rccl1`: the multi-scale trainer's per-block buckets the same way; `ss4_overlap` / `ms4`: four ranks
+(one graph each), the single-scale one with the overlapped bucket all-reduces."""
 import os
 import socket
 import subprocess
@@ -35,7 +36,7 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("case", ["ss", "ms", "ss_overlap", "ss_rccl1", "ms_overlap", "ms_rccl1"])
+@pytest.mark.parametrize("case", ["ss", "ms", "ss_overlap", "ss_rccl1", "ms_overlap", "ms_rccl1", "ss4_overlap", "ms4"])
 def test_two_ranks_match_one_process(case, tmp_path):
     from tests.dp_cases import CASES, LR, STEPS
     run, _, ranks = CASES[case]
@@ -53,24 +54,40 @@ def test_two_ranks_match_one_process(case, tmp_path):
     assert codes == [0] * world, codes
     ref = run(sum(ranks, []))
     gmax = float(ref["grad"].abs().max())
+    # fp32 partial sums added in another order: the error grows with the number of rank partials (world 4:
+    # the multi-scale gradient's worst element is off by 3.6e-5 of max|g| with the loss bit-equal).  These
+    # small 2D multi-scale graphs are ill-conditioned in fp32: the oracle itself in fp32 vs fp64 differs by
+    # up to 9e-3 of a parameter's max on one graph, and the GPU step equals the fp32 oracle there
+    # (tools/exp_ms_merge.py, profiles/r05_ms_merge_vs_oracle.txt)
+    gtol = 2e-5 * max(1, world // 2)
     for r, path in enumerate(outs):
         got = torch.load(path, weights_only=True)
         rel = np.abs(got["loss"].numpy() - ref["loss"].numpy()) / np.abs(ref["loss"].numpy())
         print(f"{case} rank {r}: loss {got['loss'].tolist()} vs {ref['loss'].tolist()} (rel {rel.max():.2e})")
         assert rel.max() <= 1e-5
         dg = (got["grad"] - ref["grad"]).abs()
-        print(f"{case} rank {r}: max|dgrad| {float(dg.max()):.3e} of max|g| {gmax:.3e}")
-        assert float(dg.max()) <= 2e-5 * gmax
+        at = int(dg.argmax())
+        off, pname = 0, "?"
+        for name, k in ref["names"]:
+            if at < off + k:
+                pname = f"{name}[{at - off}]"
+                break
+            off += k
+        print(f"{case} rank {r}: max|dgrad| {float(dg.max()):.3e} of max|g| {gmax:.3e} ({pname}: "
+              f"{float(ref['grad'][at]):.4e} vs {float(got['grad'][at]):.4e}, 2nd largest "
+              f"{float(dg.flatten().topk(2).values[1]):.3e})")
+        assert float(dg.max()) <= gtol * gmax
         # Adam moves a weight by ~lr (g1, g2 ratios) per step: a relative gradient error d moves it
         # by ~lr d, at most 2 lr per step -> |dw| <= 1e-6 + 2 STEPS lr min(1, 2e-5 gmax / |g|)
         dw = (got["param"] - ref["param"]).abs().numpy()
         g = ref["grad"].abs().numpy()
-        bound = 1e-6 + 2 * STEPS * LR * np.minimum(1.0, 2e-5 * gmax / np.maximum(g, 1e-30))
+        bound = 1e-6 + 2 * STEPS * LR * np.minimum(1.0, gtol * gmax / np.maximum(g, 1e-30))
         print(f"{case} rank {r}: max|dw| {dw.max():.3e}, worst |dw|/bound {(dw / bound).max():.3f}")
         assert (dw <= bound).all()
     if world > 1:
-        g0, g1 = (torch.load(p, weights_only=True) for p in outs)
-        assert torch.equal(g0["grad"], g1["grad"]) and torch.equal(g0["param"], g1["param"])
+        g0, *rest = (torch.load(p, weights_only=True) for p in outs)
+        for g1 in rest:
+            assert torch.equal(g0["grad"], g1["grad"]) and torch.equal(g0["param"], g1["param"])
     else:   # one RCCL rank: the overlapped buckets change nothing -- bit for bit the plain step
         got = torch.load(outs[0], weights_only=True)
         assert torch.equal(got["grad"], ref["grad"]) and torch.equal(got["param"], ref["param"])
