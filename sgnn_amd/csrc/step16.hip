@@ -1245,6 +1245,74 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     int sn[kWaves16];
 #pragma unroll
     for (int w = 0; w < kWaves16; ++w) sn[w] = segn[w];
+#ifdef SGNN_EXP_SCAN_SHARED
+    if (loop) {
+      // Experiment (round 5, profiles/r05_ab_radius_scan_shared.txt: t8000 -1.7 %, r = 0.6 -0.6 %, r = 15 +1 %,
+      // t4800 neutral; not shipped): every receiver of the wave (rl = b + 4 q) tests each round of candidates,
+      // so a round's LDS reads serve all of them.  Per receiver the scan order is the one of the
+      // per-receiver form below (segments in order, chunks in order, lanes in order): the same first `cap`
+      // in-range senders in index order, written straight to its CSR row.
+      constexpr int kRq = kMaxNT / kWaves16;
+      const int nr = cnt > b ? (cnt - b + kWaves16 - 1) / kWaves16 : 0;
+      int cq[kRq], jbq[kRq], jeq[kRq];
+      float pq[kRq][DIM];
+#pragma unroll
+      for (int q = 0; q < kRq; ++q) {
+        const int rl = min(b + kWaves16 * q, cnt - 1);
+        const int ex = example_of(i0 + rl);
+        jbq[q] = exs[ex];
+        jeq[q] = exs[ex + 1];
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) pq[q][d] = rp[d * kMaxNT + rl];
+        cq[q] = q < nr ? 0 : cap;   // absent receivers start full
+      }
+      auto open = [&]() {
+        bool o = false;
+#pragma unroll
+        for (int q = 0; q < kRq; ++q) o = o || cq[q] < cap;
+        return o;
+      };
+      constexpr int kRound = 2;
+      for (int w = 0; w < kWaves16 && open(); ++w) {
+        const int wn = sn[w], wb = w * Q;
+        for (int base = 0; base < wn && open(); base += 64 * kRound) {
+          float pc[kRound][DIM];
+          int id[kRound];
+#pragma unroll
+          for (int u = 0; u < kRound; ++u) {
+            const int kk = wb + min(base + 64 * u + l, wn - 1);
+#pragma unroll
+            for (int d = 0; d < DIM; ++d) pc[u][d] = cp[d * cv.list_cap + kk];
+            id[u] = cid[kk];
+          }
+#pragma unroll
+          for (int q = 0; q < kRq; ++q) {
+            if (cq[q] >= cap) continue;   // (wave-uniform)
+            const int rl = b + kWaves16 * q;
+#pragma unroll
+            for (int u = 0; u < kRound; ++u) {
+              float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
+#pragma unroll
+              for (int d = 0; d < DIM; ++d) {
+#pragma clang fp contract(off)
+                const float t = __fsub_rn(pc[u][d], pq[q][d]);
+                s = __fadd_rn(s, __fmul_rn(t, t));
+              }
+              const bool in = base + 64 * u + l < wn && id[u] >= jbq[q] && id[u] < jeq[q] && s < r2;
+              const uint64_t bal = __ballot(in);
+              const int slot = cq[q] + (int)__popcll(bal & ((1ull << l) - 1ull));
+              if (in && slot < cap) nbr_l[rl * cap + slot] = id[u];
+              cq[q] += (int)__popcll(bal);
+            }
+          }
+        }
+      }
+      if (l == 0)
+#pragma unroll
+        for (int q = 0; q < kRq; ++q)
+          if (q < nr) ldeg[b + kWaves16 * q] = min(cq[q], cap);
+    } else
+#endif
     for (int rl = b; rl < cnt; rl += kWaves16) {
       const int i = i0 + rl;
       const int ex = example_of(i);
