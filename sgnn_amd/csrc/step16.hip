@@ -1091,7 +1091,10 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   // one example (the rollout benches): the candidates are [0, n) without waiting for ex_ptr, so the first
   // filter batch's positions are requested now, under the receivers' box and the weight loads (used below
   // only if ex_ptr confirms [0, n))
-  constexpr int kBatch = 8;  // 64-candidate chunks whose loads are in flight together
+#ifndef SGNN_FILTER_BATCH
+#define SGNN_FILTER_BATCH 8
+#endif
+  constexpr int kBatch = SGNN_FILTER_BATCH;  // 64-candidate chunks whose loads are in flight together
   const int Q1 = (((a.n + 3) >> 2) + 63) & ~63;
   const bool pre_ok = n_ex == 1 && b * Q1 < a.n;
   float pre[kBatch][DIM];
