@@ -413,6 +413,29 @@ struct LnAgg {
   }
 };
 
+#ifdef SGNN_EXP_SPLIT_HALF
+// mm_full<true> restricted to the unit tiles t0, t0 + 1 (two accumulator chains): half of a Linear's
+// outputs, for the halves split over a wave pair
+SGNN_DEV void mm_half_tr(f32x4 (&acc)[2], const float* Wl, const f32x4 (&x)[KQ], int j, int g, int t0) {
+  f32x4 w[2][2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) w[0][tt] = ld4(Wl + (16 * (t0 + tt) + j) * LDX + 4 * g);
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    if (q + 1 < KQ) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) w[(q + 1) & 1][tt] = ld4(Wl + (16 * (t0 + tt) + j) * LDX + 16 * (q + 1) + 4 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) acc[tt] = mfma16(x[q][c], w[q & 1][tt][c], acc[tt]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+#endif
+
 // The last Linear of the edge MLP, its LayerNorm and the receiver sums of one
 // 16-edge half, with no transposition through LDS.  The Linear runs with its
 // operands swapped (mm_full<true>): lane (j, g) receives y[unit 16 t + j][edge
@@ -702,8 +725,23 @@ struct EdgePhase {
       for (int p = 0; p < 4; ++p) la.part(p, y, agg, ev, lrecv, hs, Et, i0, j, g);
     };
     const int npre = donor ? kPre - 1 : kPre;  // own halves whose product ran before the wait
+#ifdef SGNN_EXP_SPLIT_HALF
+    // Experiment (round 5, profiles/r05_ab_split_half.txt: C1 r = 15 85.2 -> 87.3 us, the three barriers and
+    // the donor's gather cost more than the half they save; not shipped): with 4F + 2 halves (the donated
+    // pair 4F, 4F + 1) each of those two halves is
+    // finished by its owner b and its donor b + 2 together, each wave computing two of the four unit tiles
+    // of the last Linear, LayerNorm statistics summed over the pair through LDS (three barriers): every
+    // wave runs F + 1/2 halves instead of F + 1 / F.
+    const bool split = NSUB == 1 && donates && r == 2;
+    const int hs_split = 16 * (kWaves16 * F + (b & 1));
+    f32x4 acc_s[KQ];
+#else
+    constexpr bool split = false;
+    const int hs_split = 0;
+#endif
     int hs = 16 * b;
     if (hs < Et) gather(hs);
+    else if (split && donor) gather(hs_split);   // a donor with no half of its own
     if (probe) mark(48);
 #pragma unroll
     for (int m = 0; m < kPre; ++m) {
@@ -713,6 +751,13 @@ struct EdgePhase {
       if (owner_d && m == F) {   // formed by the donor wave (published with the barrier before the wait)
 #pragma unroll
         for (int t = 0; t < KQ; ++t) acc[t] = ld4(dbuf + ((b * KQ + t) * 64 + l) * 4) + (gu[t] + gv[t]);
+#ifdef SGNN_EXP_SPLIT_HALF
+        if (split) {
+#pragma unroll
+          for (int t = 0; t < KQ; ++t) acc_s[t] = acc[t];
+          break;
+        }
+#endif
       } else if (m < npre) {
 #pragma unroll
         for (int t = 0; t < KQ; ++t) acc[t] = pre[m][t] + (gu[t] + gv[t]);
@@ -723,11 +768,67 @@ struct EdgePhase {
         for (int t = 0; t < KQ; ++t) acc[t] = gu[t] + gv[t];
         mm_full(acc, sw0, x, j, g);
       }
-      gather(hs + 16 * kWaves16);
+      // (split: a donor's last own half prefetches the rows of the half it finishes with its owner)
+      gather(split && donor && hs + 16 * kWaves16 >= Et ? hs_split : hs + 16 * kWaves16);
       finish(acc, hs);
       if (probe) mark(49 + m);
       hs += 16 * kWaves16;
     }
+#ifdef SGNN_EXP_SPLIT_HALF
+    if (split) {
+      const int pr = b & 1, role = b < 2 ? 0 : 1;
+      if (donor) {
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) acc_s[t] = pre[kPre - 1][t] + (gu[t] + gv[t]);   // the donated product
+      }
+      float* xch = dbuf + pr * (KQ * 64 * 4);   // the pair's dbuf slot, free once the owner has read it
+      __syncthreads();
+      // unit tiles T0, T0 + 1 (compile-time: the per-tile registers are indexed with constants)
+      auto run = [&](auto t0c) {
+        constexpr int T0 = decltype(t0c)::value;
+        f32x4 x[KQ], y2[2];
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) x[t] = relu4(acc_s[t]);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) y2[tt] = f32x4{ev.b2[T0 + tt], ev.b2[T0 + tt], ev.b2[T0 + tt], ev.b2[T0 + tt]};
+        mm_half_tr(y2, sw1, x, j, g, T0);
+        f32x4 pm = y2[0] + y2[1];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pm[c] = row_sum16(pm[c]);
+        if (j == 0) st4(xch + (role * 4 + g) * 4, pm);
+        __syncthreads();
+        const f32x4 mu = (ld4(xch + g * 4) + ld4(xch + (4 + g) * 4)) * (1.0f / H);
+        f32x4 d[2], pv = zero4();
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          d[tt] = y2[tt] - mu;
+          pv += d[tt] * d[tt];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pv[c] = row_sum16(pv[c]);
+        if (j == 0) st4(xch + (8 + role * 4 + g) * 4, pv);
+        __syncthreads();
+        const f32x4 var = ld4(xch + (8 + g) * 4) + ld4(xch + (12 + g) * 4);
+        f32x4 rs;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rs[c] = __builtin_amdgcn_rsqf(var[c] * (1.0f / H) + 1e-5f);
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const i32x4 rv = *reinterpret_cast<const i32x4*>(lrecv + hs_split + 4 * g);
+        float sb[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) sb[s2] = (hs_split + 4 * g + s2 < Et && rv[s2] - i0 == j) ? 1.0f : 0.0f;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) d[tt] = d[tt] * rs * ev.ga[T0 + tt] + ev.be[T0 + tt];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) agg[0][T0 + tt] = mfma16(d[tt][s2], sb[s2], agg[0][T0 + tt]);
+      };
+      if (role == 0) run(std::integral_constant<int, 0>{});
+      else run(std::integral_constant<int, 2>{});
+      hs = Et;   // every half is done (an owner left its loop at the split half)
+    }
+#endif
     for (; hs < Et; hs += 16 * kWaves16) {   // halves past kPre: the e0 product here
       f32x4 x[KQ], acc[KQ];
       ld_e0(x, hs);
