@@ -622,78 +622,6 @@ void k_edge_bwd64(EdgeBwdArgs a) {
   f32x4 s_dbl = {0.0f, 0.0f, 0.0f, 0.0f}, s_dg = s_dbl, s_db = s_dbl;   // units 4 (lane & 15) + c
   const int64_t E = a.rowptr[a.n];
   const int64_t nchunks = (E + kChunk - 1) / kChunk;
-#ifdef SGNN_EXP_EDGE_BWD_IDS
-  if constexpr (!DW1E) {
-    // Experiment (round 5, measured slower and not kept: C2 kernel 71.5 -> 76.3 us, step 1.933 -> 1.965 ms,
-    // profiles/r05_ab_edge_bwd_ids.txt): the receiver ids of chunk c + grid (and its rstd, the neighbouring
-    // receivers) requested before chunk c's dWl outer product, so the dependent gather of the dagg rows
-    // (recv[e] -> dagg[recv[e]]) is one round trip at the loop top instead of two.
-    float rs_n = 0.0f;
-    int rv_n = 0, nb_n = -1;
-    auto fetch_ids = [&](int64_t c) {
-      const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
-      rs_n = 0.0f;
-      rv_n = 0;
-      nb_n = -1;
-      if (clamp_items(E - base) > 0) {
-        const int64_t ec = e < E ? e : E - 1;
-        rv_n = a.recv[ec];
-        rs_n = a.rstd[ec];
-        const int64_t q = j == 0 ? base - 1 : base + 32;
-        const bool has = j == 0 ? base > 0 : base + 32 < E;
-        nb_n = has ? a.recv[has ? q : base] : -1;
-      }
-    };
-    if ((int64_t)blockIdx.x < nchunks) fetch_ids(blockIdx.x);
-    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-      const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
-      const int nvalid = clamp_items(E - base);
-      const bool valid = e < E;
-      f32x16 dm[TH], yh[TH], h1[TH];
-      const float rs = rs_n;
-      const int rv = rv_n, nb = nb_n;
-      if (nvalid > 0) {  // tiles past the last valid one are not allocated
-        load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
-        load_tiled<TH>(yh, a.yh + tile * (32 * H));
-        load_tiled<TH>(h1, a.hs + tile * (32 * H));
-      } else {
-        zero<TH>(dm);
-        zero<TH>(yh);
-        zero<TH>(h1);
-      }
-      zero_if<TH>(dm, !valid);
-      zero_if<TH>(h1, !valid);
-      f32x16 dy[TH];
-      acc_layernorm_bwd<TH>(dm, yh, rs, a.gamma, dy);   // graph_network.py:148
-      zero_if<TH>(dy, !valid);
-#pragma unroll
-      for (int t = 0; t < TH; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];   // dgamma terms (dm = 0 off the edges)
-      swz_store_items(sA, j, dm);
-      swz_store_items(sB, j, yh);
-      wave_lds_sync();
-      s_db += swz_col_sums(sA);
-      s_dg += swz_col_sums(sB);
-      wave_lds_sync();
-      swz_store_items(sA, j, dy);
-      swz_store_items(sB, j, h1);
-      wave_lds_sync();
-      s_dbl += swz_col_sums(sA);
-      const int nb0 = __builtin_amdgcn_readlane(nb, 0), nb1 = __builtin_amdgcn_readlane(nb, 1);
-      if (c + gridDim.x < nchunks) fetch_ids(c + gridDim.x);   // in flight under the outer product
-      __syncthreads();
-      swz_outer(acc, bufA, 32 * tu, bufB, 32 * tv);
-      __syncthreads();
-      f32x16 dh[TH];
-      zero<TH>(dh);
-      swz_matvec_t(dh, wt, dy);
-      relu_mask<TH>(dh, h1, valid);
-      store_row_clayout_if<TH>(buf_rsrc(a.dh_rows + base * H), j * (4 * H), valid, dh);
-      segment_sum_rows<TH>(dh, rv, valid, nb0, nb1, tile, a.du, a.cin, a.cout);
-    }
-  } else
-#endif
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
     const int nvalid = clamp_items(E - base);
@@ -772,116 +700,6 @@ void k_edge_bwd64(EdgeBwdArgs a) {
   }
 }
 
-#ifdef SGNN_EXP_EDGE_BWD_PIPE
-// Experiment (round 5): k_edge_bwd64<false> with the next chunk's operands in flight under this chunk's
-// MFMAs -- its receiver ids, rstd and the neighbouring receivers at the loop top, its gathered dagg rows
-// and its yh / h1 tiles after the dWl outer product -- at ONE wave per SIMD (the prefetch buffers do not
-// fit the 256 registers of two), so latency hides behind the wave's own MFMAs instead of a second wave's.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void k_edge_bwd64_pipe(EdgeBwdArgs a) {
-  constexpr int TH = 2, H = 64;
-  extern __shared__ float lds[];
-  float* wt = lds;
-  float* bufA = wt + H * H;
-  float* bufB = bufA + kChunk * H;
-  swz_stage_wt(wt, a.wl, H, 1.0f);
-  __syncthreads();
-  const int w = wave_id(), l = lane_id(), j = l & 31;
-  float* sA = bufA + w * 32 * H;
-  float* sB = bufB + w * 32 * H;
-  const int tu = w >> 1, tv = w & 1;
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  f32x4 s_dbl = {0.0f, 0.0f, 0.0f, 0.0f}, s_dg = s_dbl, s_db = s_dbl;
-  const int64_t E = a.rowptr[a.n];
-  const int64_t nchunks = (E + kChunk - 1) / kChunk;
-  const int64_t G = gridDim.x;
-  struct Ids {
-    int rv, nb;
-    float rs;
-  };
-  auto fetch_ids = [&](int64_t c, Ids& d) {
-    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
-    d.rv = 0;
-    d.nb = -1;
-    d.rs = 0.0f;
-    if (c < nchunks && clamp_items(E - base) > 0) {
-      const int64_t ec = e < E ? e : E - 1;
-      d.rv = a.recv[ec];
-      d.rs = a.rstd[ec];
-      const int64_t q = j == 0 ? base - 1 : base + 32;
-      const bool has = j == 0 ? base > 0 : base + 32 < E;
-      d.nb = has ? a.recv[has ? q : base] : -1;
-    }
-  };
-  auto fetch_rows = [&](int64_t c, const Ids& d, f32x16 (&dm)[TH], f32x16 (&yh)[TH], f32x16 (&h1)[TH]) {
-    const int64_t tile = c * kWaves + w, base = tile * 32;
-    if (c < nchunks && clamp_items(E - base) > 0) {
-      load_row_clayout<TH>(dm, a.dagg + (int64_t)d.rv * H);
-      load_tiled<TH>(yh, a.yh + tile * (32 * H));
-      load_tiled<TH>(h1, a.hs + tile * (32 * H));
-    } else {
-      zero<TH>(dm);
-      zero<TH>(yh);
-      zero<TH>(h1);
-    }
-  };
-  Ids cur, nxt;
-  f32x16 dm[TH], yh[TH], h1[TH];
-  const int64_t c0 = blockIdx.x;
-  fetch_ids(c0, cur);
-  fetch_rows(c0, cur, dm, yh, h1);
-  for (int64_t c = c0; c < nchunks; c += G) {
-    const int64_t tile = c * kWaves + w, base = tile * 32, e = base + j;
-    const bool valid = e < E;
-    fetch_ids(c + G, nxt);   // in flight under this chunk's LayerNorm and outer product
-    zero_if<TH>(dm, !valid);
-    zero_if<TH>(h1, !valid);
-    f32x16 dy[TH];
-    acc_layernorm_bwd<TH>(dm, yh, cur.rs, a.gamma, dy);   // graph_network.py:148
-    zero_if<TH>(dy, !valid);
-#pragma unroll
-    for (int t = 0; t < TH; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) yh[t][r] *= dm[t][r];
-    swz_store_items(sA, j, dm);
-    swz_store_items(sB, j, yh);
-    wave_lds_sync();
-    s_db += swz_col_sums(sA);
-    s_dg += swz_col_sums(sB);
-    wave_lds_sync();
-    swz_store_items(sA, j, dy);
-    swz_store_items(sB, j, h1);
-    wave_lds_sync();
-    s_dbl += swz_col_sums(sA);
-    __syncthreads();
-    swz_outer(acc, bufA, 32 * tu, bufB, 32 * tv);
-    __syncthreads();
-    // the next chunk's rows: dm / yh are dead after the images, h1 is needed for the ReLU mask below
-    f32x16 h1c[TH];
-#pragma unroll
-    for (int t = 0; t < TH; ++t) h1c[t] = h1[t];
-    fetch_rows(c + G, nxt, dm, yh, h1);
-    f32x16 dh[TH];
-    zero<TH>(dh);
-    swz_matvec_t(dh, wt, dy);
-    relu_mask<TH>(dh, h1c, valid);
-    store_row_clayout_if<TH>(buf_rsrc(a.dh_rows + base * H), j * (4 * H), valid, dh);
-    segment_sum_rows<TH>(dh, cur.rv, valid, __builtin_amdgcn_readlane(cur.nb, 0), __builtin_amdgcn_readlane(cur.nb, 1),
-                         tile, a.du, a.cin, a.cout);
-    cur = nxt;
-  }
-  float* slab = a.slab + blockIdx.x * a.slab_stride;
-  store_tile_rowmajor(slab + (32 * tu) * H + 32 * tv, H, acc);
-  float* v = slab + slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, 2);
-  if (l < 16) {
-    st4(v + w * H + 4 * l, s_dbl);
-    st4(v + kWaves * H + w * H + 4 * l, s_dg);
-    st4(v + 2 * kWaves * H + w * H + 4 * l, s_db);
-  }
-}
-#endif
 
 // ===========================================================================
 // Node layer backward (graph_network.py:201-222 + residual :176)
@@ -2534,11 +2352,7 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
   }
   if (H == 64 && edge_fn->nlin == 2 && !de0t) {  // single-scale training: two workgroups per CU
     if (de0_accumulate & 2) launch_bwd(k_edge_bwd64<true>, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
-#ifdef SGNN_EXP_EDGE_BWD_PIPE
-    else launch_bwd(k_edge_bwd64_pipe, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
-#else
     else launch_bwd(k_edge_bwd64<false>, nslab, 4 * (size_t)(H * H + 2 * kChunk * H), stream, a);
-#endif
     return check_launch("edge_layer_bwd");
   }
   const size_t lds = bwd_lds(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin) - (de0t ? 0 : 4 * (size_t)H * (H + 4));

@@ -72,11 +72,7 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   // the grid at one workgroup per CU (up to 32: the Taylor bars' 4,800 / 6,400 / 8,000 at 19 / 25 / 32)
   const int64_t cus = std::min<int64_t>(device_cus(), kStep16MaxGrid);
   if (cus < 1) return false;
-#ifdef SGNN_EXP_NT
-  a.nt = (int)std::max<int64_t>(SGNN_EXP_NT, (n + cus - 1) / cus);   // experiment builds: receivers per tile
-#else
   a.nt = (int)std::max<int64_t>(8, (n + cus - 1) / cus);
-#endif
   if (a.nt > kStep16MaxNT || (n + a.nt - 1) / a.nt > cus) return false;
   a.ecap_t = a.nt * cap;
   a.e0_hbm = a.nt > 16 ? 1 : 0;   // two node sub-tiles: their e0 rows live in HBM
@@ -87,11 +83,7 @@ bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq
   // dispatch order or faster at every size (profiles/r05_ab_flag_stride.txt, r05_ab_xcd_all_sizes.txt);
   // with packed counters it was slower on some boxes (the counters of a tile's neighbours shared a
   // line its producers kept writing: r05_ab_dispatch_order_packed_flags.txt)
-#if defined(SGNN_EXP_DISPATCH_ORDER)
-  a.tile_order = 0;   // experiment builds: the dispatch order (same-box A/Bs)
-#else
   a.tile_order = 1;
-#endif
   size_t lds = step16_lds_bytes(a);
   if (lds > kStep16MaxLds && !a.e0_hbm) {  // the tile's e0 rows do not fit in LDS: keep them in HBM (ws->uvl's tail)
     a.e0_hbm = 1;

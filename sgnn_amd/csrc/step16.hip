@@ -255,9 +255,9 @@ SGNN_DEV void ln_stats_x(const f32x4 (&r)[KQ], float& mean, float& rstd) {
 // Node update of the tile's NS 16-item sub-tiles (item rows 16 s + j; `cnt` valid rows in all) from the
 // first Linear's post-ReLU outputs h[s]: last Linear, LayerNorm, + residual xo -> x (LDS rows xs), then u, v
 // of the next layer (mode 0, sc1 rows) or decoder + integrator + window shift (mode 1).  Same arithmetic
-// as fwd16.hip node_tail.  The sub-tiles go through each exchange together (round 5): one workgroup
-// barrier per exchange for both, and two independent MFMA chains between them (sub-tile s's exchange
-// buffers: scratch rows 48 s .. 48 s + 47).
+// as fwd16.hip node_tail.  The kernel runs it once per 16-item sub-tile (NS = 1); NS > 1 would take the
+// sub-tiles through each exchange together (sub-tile s's exchange buffers: scratch rows 48 s .. 48 s + 47),
+// the round-5 experiment DESIGN.md section 8.1 records and that is not shipped.
 template <int NS>
 SGNN_DEV void xchg_n(float* buf, int sstride, int j, int ucol, int g, const f32x4 (&v)[NS], f32x4 (&out)[NS][KQ]) {
 #pragma unroll
@@ -413,29 +413,6 @@ struct LnAgg {
   }
 };
 
-#ifdef SGNN_EXP_SPLIT_HALF
-// mm_full<true> restricted to the unit tiles t0, t0 + 1 (two accumulator chains): half of a Linear's
-// outputs, for the halves split over a wave pair
-SGNN_DEV void mm_half_tr(f32x4 (&acc)[2], const float* Wl, const f32x4 (&x)[KQ], int j, int g, int t0) {
-  f32x4 w[2][2];
-#pragma unroll
-  for (int tt = 0; tt < 2; ++tt) w[0][tt] = ld4(Wl + (16 * (t0 + tt) + j) * LDX + 4 * g);
-#pragma unroll
-  for (int q = 0; q < KQ; ++q) {
-    if (q + 1 < KQ) {
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) w[(q + 1) & 1][tt] = ld4(Wl + (16 * (t0 + tt) + j) * LDX + 16 * (q + 1) + 4 * g);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) acc[tt] = mfma16(x[q][c], w[q & 1][tt][c], acc[tt]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-#endif
-
 // The last Linear of the edge MLP, its LayerNorm and the receiver sums of one
 // 16-edge half, with no transposition through LDS.  The Linear runs with its
 // operands swapped (mm_full<true>): lane (j, g) receives y[unit 16 t + j][edge
@@ -456,16 +433,12 @@ SGNN_DEV void lin2_init(const f32x4 (&acc)[KQ], f32x4 (&x)[KQ], f32x4 (&y)[KQ], 
   }
 }
 
-#ifndef SGNN_KPRE
-#define SGNN_KPRE 3
-#endif
-constexpr int kPre = SGNN_KPRE;   // halves per wave whose W1e e0 product runs before the wait
+// halves per wave whose W1e e0 product runs before the wait (2 / 4 measured: C1 r = 15 +13 % / -1 %,
+// t8000 +4 % / 0)
+constexpr int kPre = 3;
 // The tile publishes the node halves its previous stage stored after this many of those products: the
-// drain of the write-through stores overlaps them (SGNN_PUB_AT: experiment builds)
-#ifndef SGNN_PUB_AT
-#define SGNN_PUB_AT 1
-#endif
-constexpr int kPubAt = SGNN_PUB_AT;
+// drain of the write-through stores overlaps them (after the second / third product: C1 r = 15 +11 / +13 us)
+constexpr int kPubAt = 1;
 static_assert(kPubAt >= 0 && kPubAt <= kPre, "publish point within the pre-wait");
 
 // The edge MLP of a layer, split around the wait for the sender tiles.  Wave b
@@ -525,14 +498,8 @@ struct EdgePhase {
 
   SGNN_DEV void ld_e0(f32x4 (&x)[KQ], int hs) const {
     const int e = hs + j, ec = e < Et ? e : Et - 1;
-#ifdef SGNN_EXP_E0_SC1
-    const __amdgpu_buffer_rsrc_t r = buf_rsrc(e0l);   // experiment: L1-bypassing loads of the e0 rows
-#pragma unroll
-    for (int q = 0; q < KQ; ++q) x[q] = ld4_sc1(r, (ec * LDX + 16 * q + 4 * g) * 4);
-#else
 #pragma unroll
     for (int q = 0; q < KQ; ++q) x[q] = ld4(e0l + ec * LDX + 16 * q + 4 * g);
-#endif
   }
 
   // before the wait: (FIRST) e0 of every half; W1e e0 of the first kPre halves
@@ -637,11 +604,12 @@ struct EdgePhase {
         f32x4 x[KQ];
         encode_item(x, hs, k);
       }
-      // Tiles whose e0 rows live in HBM (two node sub-tiles): every storing wave drains its e0 stores
-      // here, before any of those rows is loaded back by the same wave (plain stores, plain loads).  The
-      // merged node-phase experiment failed far less often with this wait; its cause
-      // is not established, the wait is kept: it orders this kernel's only same-launch store -> load of
-      // plain global rows, at no measurable cost.
+      // Tiles whose e0 rows live in HBM (two node sub-tiles): the rows are no hand-off.  Every e0 row is
+      // stored and later loaded by the same lane of the same wave (a padding lane reloads row Et - 1, stored
+      // by its own wave in the same instruction), and a half's 16 rows are 16 x 272 B = 34 whole 128-B
+      // lines at a 128-B aligned offset, so no line is written by two waves.  This drain is therefore not
+      // an ordering requirement: it is a leftover mitigation from the round-5 merged node-phase experiment
+      // (where the e0 path was ruled out as that failure's cause), measured neutral.
       if (e0_hbm) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
@@ -725,23 +693,8 @@ struct EdgePhase {
       for (int p = 0; p < 4; ++p) la.part(p, y, agg, ev, lrecv, hs, Et, i0, j, g);
     };
     const int npre = donor ? kPre - 1 : kPre;  // own halves whose product ran before the wait
-#ifdef SGNN_EXP_SPLIT_HALF
-    // Experiment (round 5, profiles/r05_ab_split_half.txt: C1 r = 15 85.2 -> 87.3 us, the three barriers and
-    // the donor's gather cost more than the half they save; not shipped): with 4F + 2 halves (the donated
-    // pair 4F, 4F + 1) each of those two halves is
-    // finished by its owner b and its donor b + 2 together, each wave computing two of the four unit tiles
-    // of the last Linear, LayerNorm statistics summed over the pair through LDS (three barriers): every
-    // wave runs F + 1/2 halves instead of F + 1 / F.
-    const bool split = NSUB == 1 && donates && r == 2;
-    const int hs_split = 16 * (kWaves16 * F + (b & 1));
-    f32x4 acc_s[KQ];
-#else
-    constexpr bool split = false;
-    const int hs_split = 0;
-#endif
     int hs = 16 * b;
     if (hs < Et) gather(hs);
-    else if (split && donor) gather(hs_split);   // a donor with no half of its own
     if (probe) mark(48);
 #pragma unroll
     for (int m = 0; m < kPre; ++m) {
@@ -751,13 +704,6 @@ struct EdgePhase {
       if (owner_d && m == F) {   // formed by the donor wave (published with the barrier before the wait)
 #pragma unroll
         for (int t = 0; t < KQ; ++t) acc[t] = ld4(dbuf + ((b * KQ + t) * 64 + l) * 4) + (gu[t] + gv[t]);
-#ifdef SGNN_EXP_SPLIT_HALF
-        if (split) {
-#pragma unroll
-          for (int t = 0; t < KQ; ++t) acc_s[t] = acc[t];
-          break;
-        }
-#endif
       } else if (m < npre) {
 #pragma unroll
         for (int t = 0; t < KQ; ++t) acc[t] = pre[m][t] + (gu[t] + gv[t]);
@@ -768,67 +714,11 @@ struct EdgePhase {
         for (int t = 0; t < KQ; ++t) acc[t] = gu[t] + gv[t];
         mm_full(acc, sw0, x, j, g);
       }
-      // (split: a donor's last own half prefetches the rows of the half it finishes with its owner)
-      gather(split && donor && hs + 16 * kWaves16 >= Et ? hs_split : hs + 16 * kWaves16);
+      gather(hs + 16 * kWaves16);
       finish(acc, hs);
       if (probe) mark(49 + m);
       hs += 16 * kWaves16;
     }
-#ifdef SGNN_EXP_SPLIT_HALF
-    if (split) {
-      const int pr = b & 1, role = b < 2 ? 0 : 1;
-      if (donor) {
-#pragma unroll
-        for (int t = 0; t < KQ; ++t) acc_s[t] = pre[kPre - 1][t] + (gu[t] + gv[t]);   // the donated product
-      }
-      float* xch = dbuf + pr * (KQ * 64 * 4);   // the pair's dbuf slot, free once the owner has read it
-      __syncthreads();
-      // unit tiles T0, T0 + 1 (compile-time: the per-tile registers are indexed with constants)
-      auto run = [&](auto t0c) {
-        constexpr int T0 = decltype(t0c)::value;
-        f32x4 x[KQ], y2[2];
-#pragma unroll
-        for (int t = 0; t < KQ; ++t) x[t] = relu4(acc_s[t]);
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) y2[tt] = f32x4{ev.b2[T0 + tt], ev.b2[T0 + tt], ev.b2[T0 + tt], ev.b2[T0 + tt]};
-        mm_half_tr(y2, sw1, x, j, g, T0);
-        f32x4 pm = y2[0] + y2[1];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) pm[c] = row_sum16(pm[c]);
-        if (j == 0) st4(xch + (role * 4 + g) * 4, pm);
-        __syncthreads();
-        const f32x4 mu = (ld4(xch + g * 4) + ld4(xch + (4 + g) * 4)) * (1.0f / H);
-        f32x4 d[2], pv = zero4();
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          d[tt] = y2[tt] - mu;
-          pv += d[tt] * d[tt];
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) pv[c] = row_sum16(pv[c]);
-        if (j == 0) st4(xch + (8 + role * 4 + g) * 4, pv);
-        __syncthreads();
-        const f32x4 var = ld4(xch + (8 + g) * 4) + ld4(xch + (12 + g) * 4);
-        f32x4 rs;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) rs[c] = __builtin_amdgcn_rsqf(var[c] * (1.0f / H) + 1e-5f);
-        typedef int i32x4 __attribute__((ext_vector_type(4)));
-        const i32x4 rv = *reinterpret_cast<const i32x4*>(lrecv + hs_split + 4 * g);
-        float sb[4];
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) sb[s2] = (hs_split + 4 * g + s2 < Et && rv[s2] - i0 == j) ? 1.0f : 0.0f;
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) d[tt] = d[tt] * rs * ev.ga[T0 + tt] + ev.be[T0 + tt];
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2)
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) agg[0][T0 + tt] = mfma16(d[tt][s2], sb[s2], agg[0][T0 + tt]);
-      };
-      if (role == 0) run(std::integral_constant<int, 0>{});
-      else run(std::integral_constant<int, 2>{});
-      hs = Et;   // every half is done (an owner left its loop at the split half)
-    }
-#endif
     for (; hs < Et; hs += 16 * kWaves16) {   // halves past kPre: the e0 product here
       f32x4 x[KQ], acc[KQ];
       ld_e0(x, hs);
@@ -914,9 +804,6 @@ template <bool FIRST, int MODE, bool E0G, int NSUB, int PUB>
 SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv, const float (&xw1)[KQ],
                          const int32_t* deps, int ndeps, const int32_t* lsend, const int32_t* lrecv, int Et, int i0,
                          int cnt, int b, int j, int g, int l, int tile) {
-#if defined(SGNN_EXP_XCD_ORDER) && SGNN_EXP_XCD_ORDER == 2
-  tile = blockIdx.x;  // experiment: the remap NOT applied here (publish / e0 block by workgroup index)
-#endif
   float* sw0 = lds + cv.sw0;
   float* sw1 = lds + cv.sw1;
   float* svec = lds + cv.svec;
@@ -969,23 +856,10 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   if (ep.donor) ep.template prewait<FIRST, true>(xw1, hook);
   else ep.template prewait<FIRST, false>(xw1, hook);
   mark(ps < 0 ? -1 : ps + 3);
-#ifdef SGNN_EXP_XHALF_EARLY
-  // experiment (round-4 record): the node MLP's x half W_x x of every sub-tile before
-  // the wait, as ONE accumulator chain -- mm_cat's second chain, so the sum is bit for bit the same
-  f32x4 xh[NSUB];
-#pragma unroll
-  for (int s = 0; s < NSUB; ++s) {
-    f32x4 xq[KQ], a1 = zero4();
-#pragma unroll
-    for (int q = 0; q < KQ; ++q) xq[q] = ld4(lds + cv.xs + (16 * s + j) * LDX + 16 * q + 4 * g);
-#pragma unroll
-    for (int q = 0; q < KQ; ++q)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) a1 = mfma16(W.w1x[q][c], xq[q][c], a1);
-    xh[s] = a1;
-  }
-#endif
   poll.wait(deps, ndeps, a.flags, ep_k, l, a.poll_limit);
+  // Guideline 16 (every load of the handed-off rows is an sc1 buffer load): no acquire instruction, but
+  // this wave-scope fence keeps the compiler from moving those loads above the poll
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   mark(ps < 0 ? -1 : ps + 4);
   ep.postwait(ru, rv, k == 1);
   mark(ps < 0 ? -1 : ps + 5);
@@ -1022,7 +896,6 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
   // u_{k+1} / v_{k+1} (mode 0); the decoder needs none
   const __amdgpu_buffer_rsrc_t ru1 = buf_rsrc(a.uvl + (MODE == 0 ? 2 * k + 2 : 0) * nH),
                                rv1 = buf_rsrc(a.uvl + (MODE == 0 ? 2 * k + 3 : 0) * nH);
-#ifndef SGNN_EXP_MERGE_NODE
 #pragma unroll
   for (int s = 0; s < NSUB; ++s) {
     if (s > 0) {  // (sub-tile 1's rows: written by no exchange of sub-tile 0)
@@ -1033,39 +906,11 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
       }
       xo = ld4(xs + (16 * s + j) * LDX + 16 * b + 4 * g);
     }
-#ifdef SGNN_EXP_XHALF_EARLY
-    f32x4 a0 = W.vb1;
-#pragma unroll
-    for (int q = 0; q < KQ; ++q)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) a0 = mfma16(W.w1a[q][c], ag[q][c], a0);
-    const f32x4 h[1] = {relu4(a0 + xh[s])};
-#else
     const f32x4 h[1] = {relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr))};  // graph_network.py:220
-#endif
     if (k == 1 && s == 0) mark(53);
     const f32x4 xo1[1] = {xo};
     step_tail<MODE, 1>(a, W, scratch, xs + 16 * s * LDX, i0 + 16 * s, cnt - 16 * s, h, xo1, b, j, g, ru1, rv1, k + 1);
   }
-#else
-  // experiment (round 5): both node sub-tiles through each exchange together (one barrier
-  // per exchange for the pair) -- failed the 3D two-example case on three boxes, not shipped
-  f32x4 hs[NSUB], xos[NSUB];
-#pragma unroll
-  for (int s = 0; s < NSUB; ++s) {
-    if (s > 0) {
-#pragma unroll
-      for (int q = 0; q < KQ; ++q) {
-        ag[q] = ld4(ag1 + j * LDX + 16 * q + 4 * g);
-        xr[q] = ld4(xs + (16 * s + j) * LDX + 16 * q + 4 * g);
-      }
-      xo = ld4(xs + (16 * s + j) * LDX + 16 * b + 4 * g);
-    }
-    hs[s] = relu4(mm_cat(W.vb1, W.w1a, ag, W.w1x, xr));
-    xos[s] = xo;
-  }
-  step_tail<MODE, NSUB>(a, W, scratch, xs, i0, cnt, hs, xos, b, j, g, ru1, rv1, k + 1);
-#endif
   mark(ps < 0 ? -1 : ps + 6);
   if constexpr (MODE == 0) {
     nxt.store(sw0, sw1, svec, (float)(2 << k));  // W1e x 2^(k+1): exact
@@ -1082,9 +927,6 @@ SGNN_DEV void step_layer(const Step16Args& a, int k, float* lds, const Carve& cv
 SGNN_DEV void hc_final(const Step16Args& a, int tile, const int32_t* lsend, const int32_t* lrecv, int Et, int b,
                        int j, int g, int l) {
   if (a.poll_limit < 0 || !g_hc) return;  // the forced-timeout test hook / no buffer: nothing to check
-#if defined(SGNN_EXP_XCD_ORDER) && SGNN_EXP_XCD_ORDER == 2
-  tile = blockIdx.x;  // the slot the layers published in
-#endif
   const uint32_t fin = a.epoch0 + (uint32_t)a.L + 1u;
   publish(a.flags, tile, fin, 0);
   const int G = (int)gridDim.x;
@@ -1125,16 +967,12 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
                              __builtin_amdgcn_kernarg_segment_ptr();
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int l = lane_id(), j = l & 15, g = l >> 4, b = wave_id();
-  // The tile this workgroup owns.  tile_order 1 (and the experiment builds): XCD-contiguous tiles -- blocks
+  // The tile this workgroup owns.  tile_order 1: XCD-contiguous tiles -- blocks
   // b, b + 8, ... share an XCD under the dispatch order and take consecutive tiles, so the sender tiles of a
   // tile (its lattice neighbours) mostly share its L2: XCD x (= b mod 8) owns G / 8 (+1 for x < G mod 8)
   // consecutive tiles, a bijection.  EVERY use of the tile index (publish slot, dependency list, e0 block)
   // takes this one value (step_layer's `tile` argument); placement is a speed matter only.
-#ifdef SGNN_EXP_XCD_ORDER
-  const bool xcd_order = true;
-#else
   const bool xcd_order = a.tile_order != 0;
-#endif
   const int xq = (int)gridDim.x / 8, xr = (int)gridDim.x % 8, xc = (int)blockIdx.x % 8;
   const int tile = xcd_order ? xc * xq + min(xc, xr) + (int)blockIdx.x / 8 : (int)blockIdx.x;
   const int nt = a.nt, cap = a.cap, n = a.n;
@@ -1192,10 +1030,7 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
   // one example (the rollout benches): the candidates are [0, n) without waiting for ex_ptr, so the first
   // filter batch's positions are requested now, under the receivers' box and the weight loads (used below
   // only if ex_ptr confirms [0, n))
-#ifndef SGNN_FILTER_BATCH
-#define SGNN_FILTER_BATCH 8
-#endif
-  constexpr int kBatch = SGNN_FILTER_BATCH;  // 64-candidate chunks whose loads are in flight together
+  constexpr int kBatch = 8;  // 64-candidate chunks whose loads are in flight together (16: neutral to +1 %)
   const int Q1 = (((a.n + 3) >> 2) + 63) & ~63;
   const bool pre_ok = n_ex == 1 && b * Q1 < a.n;
   float pre[kBatch][DIM];
@@ -1349,74 +1184,6 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     int sn[kWaves16];
 #pragma unroll
     for (int w = 0; w < kWaves16; ++w) sn[w] = segn[w];
-#ifdef SGNN_EXP_SCAN_SHARED
-    if (loop) {
-      // Experiment (round 5, profiles/r05_ab_radius_scan_shared.txt: t8000 -1.7 %, r = 0.6 -0.6 %, r = 15 +1 %,
-      // t4800 neutral; not shipped): every receiver of the wave (rl = b + 4 q) tests each round of candidates,
-      // so a round's LDS reads serve all of them.  Per receiver the scan order is the one of the
-      // per-receiver form below (segments in order, chunks in order, lanes in order): the same first `cap`
-      // in-range senders in index order, written straight to its CSR row.
-      constexpr int kRq = kMaxNT / kWaves16;
-      const int nr = cnt > b ? (cnt - b + kWaves16 - 1) / kWaves16 : 0;
-      int cq[kRq], jbq[kRq], jeq[kRq];
-      float pq[kRq][DIM];
-#pragma unroll
-      for (int q = 0; q < kRq; ++q) {
-        const int rl = min(b + kWaves16 * q, cnt - 1);
-        const int ex = example_of(i0 + rl);
-        jbq[q] = exs[ex];
-        jeq[q] = exs[ex + 1];
-#pragma unroll
-        for (int d = 0; d < DIM; ++d) pq[q][d] = rp[d * kMaxNT + rl];
-        cq[q] = q < nr ? 0 : cap;   // absent receivers start full
-      }
-      auto open = [&]() {
-        bool o = false;
-#pragma unroll
-        for (int q = 0; q < kRq; ++q) o = o || cq[q] < cap;
-        return o;
-      };
-      constexpr int kRound = 2;
-      for (int w = 0; w < kWaves16 && open(); ++w) {
-        const int wn = sn[w], wb = w * Q;
-        for (int base = 0; base < wn && open(); base += 64 * kRound) {
-          float pc[kRound][DIM];
-          int id[kRound];
-#pragma unroll
-          for (int u = 0; u < kRound; ++u) {
-            const int kk = wb + min(base + 64 * u + l, wn - 1);
-#pragma unroll
-            for (int d = 0; d < DIM; ++d) pc[u][d] = cp[d * cv.list_cap + kk];
-            id[u] = cid[kk];
-          }
-#pragma unroll
-          for (int q = 0; q < kRq; ++q) {
-            if (cq[q] >= cap) continue;   // (wave-uniform)
-            const int rl = b + kWaves16 * q;
-#pragma unroll
-            for (int u = 0; u < kRound; ++u) {
-              float s = 0.0f;  // fp32, dims summed in order, no contraction (oracle rule)
-#pragma unroll
-              for (int d = 0; d < DIM; ++d) {
-#pragma clang fp contract(off)
-                const float t = __fsub_rn(pc[u][d], pq[q][d]);
-                s = __fadd_rn(s, __fmul_rn(t, t));
-              }
-              const bool in = base + 64 * u + l < wn && id[u] >= jbq[q] && id[u] < jeq[q] && s < r2;
-              const uint64_t bal = __ballot(in);
-              const int slot = cq[q] + (int)__popcll(bal & ((1ull << l) - 1ull));
-              if (in && slot < cap) nbr_l[rl * cap + slot] = id[u];
-              cq[q] += (int)__popcll(bal);
-            }
-          }
-        }
-      }
-      if (l == 0)
-#pragma unroll
-        for (int q = 0; q < kRq; ++q)
-          if (q < nr) ldeg[b + kWaves16 * q] = min(cq[q], cap);
-    } else
-#endif
     for (int rl = b; rl < cnt; rl += kWaves16) {
       const int i = i0 + rl;
       const int ex = example_of(i);
@@ -1563,17 +1330,12 @@ __global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(1))) v
     eh[s] = relu4(mm(vb1, w1f, xf));
     ez[s] = zero4();
   }
-#ifndef SGNN_EXP_MERGE_NODE
 #pragma unroll
   for (int s = 0; s < NSUB; ++s) {
     const f32x4 h1[1] = {eh[s]}, x1[1] = {ez[s]};
     step_tail<0, 1>(a, E, lds + cv.scratch, lds + cv.xs + 16 * s * LDX, i0 + 16 * s, cnt - 16 * s, h1, x1, b, j, g,
                     buf_rsrc(a.uvl), buf_rsrc(a.uvl + (int64_t)n * H), 0);
   }
-#else
-  step_tail<0, NSUB>(a, E, lds + cv.scratch, lds + cv.xs, i0, cnt, eh, ez, b, j, g, buf_rsrc(a.uvl),
-                     buf_rsrc(a.uvl + (int64_t)n * H), 0);
-#endif
   mark(2);  // u_0 / v_0 are published by layer 0's pre-wait
 
   // ---- the interaction layers ------------------------------------------------------------------

@@ -8,12 +8,9 @@ gathers every half of every layer and compares hashes (a row read before its
 producer's stores landed differs from the settled value).  Consumers also
 compare the tags of every row they gather with the phase they polled for.
 
-Variants (experiment defines, the round-4 step experiments reconstructed):
-  base   the shipping kernel
-  xcd1   XCD-contiguous tile order, the remap applied everywhere the tile index is used
-  xcd2   the same remap applied in k_step16 only: step_layer publishes and indexes its e0 block by the
-         workgroup index (the suspected form of the round-4 experiment, step16.hip:674 vs :791 / :1068)
-  xhalf  the node MLP's x half W_x x formed before the wait for the sender tiles
+Variant: base = the shipping kernel.  (Round 5 also built the reconstructed round-4 experiments xcd1 /
+xcd2 / xhalf here; their defines were removed from step16.hip in round 6, their records are
+profiles/r05_handoff_*.log and DESIGN.md section 8.1.)
 
   python tools/exp_handoff.py build VARIANT          # here (CPU): _lib/libsgnn_hip_hc_VARIANT.so
   python tools/exp_handoff.py run VARIANT [SKEW]     # on the GPU box: every step test case, one line each
@@ -27,8 +24,7 @@ import traceback
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VARIANTS = {"base": (), "xcd1": ("SGNN_EXP_XCD_ORDER=1",), "xcd2": ("SGNN_EXP_XCD_ORDER=2",),
-            "xhalf": ("SGNN_EXP_XHALF_EARLY",)}
+VARIANTS = {"base": ()}
 
 
 def lib_path(v):

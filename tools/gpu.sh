@@ -4,7 +4,7 @@
 #   bash tools/gpu.sh tests [pytest -k expr]     every -m gpu test (or a -k subset)   -> gpurun_out/t.log
 #   bash tools/gpu.sh smoke                      __graft_entry__.smoke()               -> gpurun_out/smoke.log
 #   bash tools/gpu.sh bench [bench.py args]      one bench line                        -> gpurun_out/bench.json
-#   bash tools/gpu.sh handoff VARIANT [SKEW]    the step's hand-off check build (base / xcd1 / xcd2 / xhalf)
+#   bash tools/gpu.sh handoff VARIANT [SKEW]    the step's hand-off check build (base: the shipping kernel)
 #   bash tools/gpu.sh bounds128                  H = 128 gradient tests on the bounds-checked library
 #   bash tools/gpu.sh profile TAG WORKLOAD MODE [bench.py args]
 #        rocprofv3 kernel trace (--stats, durations) + separate FETCH_SIZE / WRITE_SIZE passes of the same
