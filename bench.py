@@ -275,11 +275,32 @@ def roofline(kernel, flops, avg_s, workload, mode, alg_bytes=None, executed_flop
     if prof:
         r["prof_us"] = prof["avg_us"]
         r["src"] = os.path.basename(prof["source"])
+        # achieved HBM bandwidth of the same launch (north_star: "achieved-HBM-fraction"): the profiled
+        # bytes over the profiled (trace-mode) duration, against the ~8 TB/s HBM3E peak
+        r["hbm_gbs"] = prof["bytes"] / (prof["avg_us"] * 1e-6) / 1e9
+        r["hbm_frac"] = r["hbm_gbs"] * 1e9 / HBM_PEAK
     if alg_bytes is not None:
         r["alg_bytes"] = alg_bytes
-    if frac > 1.0:   # recorded, not raised: one noisy leg must not discard the whole line
+    if frac > 1.0:
+        # physically impossible: the leg is marked invalid and its fraction withheld; one
+        # noisy leg does not discard the whole line, and bench_line_errors() lists it
         r["error"] = f"frac {frac:.3f} > 1: the FLOP count or the timing is wrong"
+        r["invalid_frac"], r["frac"], r["achieved"] = frac, None, None
     return r
+
+
+def bench_line_errors(line) -> list:
+    """Every leg of a bench line whose roofline carries an error (tests assert this is empty)."""
+    bad = []
+
+    def walk(d, path):
+        if isinstance(d, dict):
+            if "error" in d:
+                bad.append((path, d["error"]))
+            for k, v in d.items():
+                walk(v, f"{path}.{k}" if path else k)
+    walk(line, "")
+    return bad
 
 
 def _r(x):
@@ -300,7 +321,7 @@ def leg(r):
     if "roofline" in r:
         rf = r["roofline"]
         out["rf"] = {k: rf[k] for k in ("kernel", "frac", "flops", "exe_frac", "traffic", "alg_bytes", "live_us",
-                                        "prof_us", "src", "error") if k in rf}
+                                        "prof_us", "hbm_frac", "src", "error", "invalid_frac") if k in rf}
     if "cpu_baseline" in r:
         out["cpu"] = {k: r["cpu_baseline"][k] for k in ("value", "cores", "sample")}
         out["x_cpu"] = r["speedup_vs_cpu"]
@@ -818,6 +839,10 @@ def main(argv=None):
                 res["rollout_extra"][wl] = leg(bench_rollout(wl, st, 3, world, rank, device, args.seed, cs))
             res["multi_scale_c5_train"] = leg(bench_ms_train("c5", 3, 1, world, rank, device, args.seed, cs))
     if rank == 0:
+        errs = bench_line_errors(res)
+        if errs:
+            res["invalid_legs"] = [p for p, _ in errs]
+            print(f"bench: legs with an invalid roofline: {errs}", file=sys.stderr, flush=True)
         print(json.dumps(_r(res), separators=(",", ":")))
     if world > 1:
         torch.distributed.destroy_process_group()

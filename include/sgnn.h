@@ -18,7 +18,11 @@
 #include <stddef.h>
 #include <stdint.h>
 
-/* Size of sgnn_step_ws.step_flags in 32-bit words, and the index of its error word. */
+/* ABI revision of this header; sgnn_abi_version() returns the library's.  6: sgnn_step_ws starts with
+ * struct_size (checked by every entry point that takes it), step_flags is SGNN_STEP_FLAG_WORDS long. */
+#define SGNN_ABI_VERSION 6
+/* Size of sgnn_step_ws.step_flags in 32-bit words, and the index of its error word (bindings that do not
+ * include this header ask sgnn_step_flag_words()). */
 #define SGNN_STEP_FLAG_WORDS 4128
 #define SGNN_STEP_FLAG_ERR 4096
 
@@ -64,6 +68,8 @@ typedef struct sgnn_saves {
 
 const char* sgnn_version(void);
 const char* sgnn_last_error(void);
+int32_t sgnn_abi_version(void);     /* SGNN_ABI_VERSION the library was built with */
+int32_t sgnn_step_flag_words(void); /* SGNN_STEP_FLAG_WORDS the library was built with */
 
 /* ---------------------------------------------------------------------------
  * Neighbour search.  Replaces torch_geometric.nn.radius_graph(x, r, batch,
@@ -254,6 +260,8 @@ typedef struct sgnn_step_in {
 } sgnn_step_in;
 
 typedef struct sgnn_step_ws { /* device buffers of one (n, T, dim, H, K) shape */
+  int64_t struct_size; /* = sizeof(sgnn_step_ws); any other value: SGNN_ERR_INVALID (a caller built against
+                          another revision of this header) */
   void* radius_ws;
   int32_t *rowptr, *send, *recv;
   int64_t edge_cap;

@@ -12,11 +12,13 @@ from typing import Optional
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# SGNN_LIB: an experiment build of the same library (tools/exp_ab.py, tools/exp_handoff.py) in place of the
-# product one -- for same-box A/Bs of the test suite; unset in every product run
-LIB_PATH = os.environ.get("SGNN_LIB") or os.path.join(HERE, "_lib", "libsgnn_hip.so")
+PRODUCT_LIB = os.path.join(HERE, "_lib", "libsgnn_hip.so")
+# SGNN_LIB: an experiment build of the same library (tools/exp_ab.py, tools/exp_localize.py) in place of the
+# product one -- for same-box A/Bs of the test suite; load_library warns loudly whenever it is set
+LIB_PATH = os.environ.get("SGNN_LIB") or PRODUCT_LIB
 
-STEP_FLAG_WORDS, STEP_FLAG_ERR = 4128, 4096   # include/sgnn.h SGNN_STEP_FLAG_WORDS / _ERR
+ABI_VERSION = 6                               # include/sgnn.h SGNN_ABI_VERSION: checked at load
+STEP_FLAG_WORDS, STEP_FLAG_ERR = 4128, 4096   # include/sgnn.h SGNN_STEP_FLAG_WORDS / _ERR: checked at load
 SGNN_OK, SGNN_ERR_INVALID, SGNN_ERR_UNSUPPORTED, SGNN_ERR_HIP, SGNN_ERR_STEP_TIMEOUT = 0, 1, 2, 3, 4
 
 c_void_p, c_int64, c_int32, c_float = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
@@ -55,7 +57,7 @@ class SgnnStepIn(ctypes.Structure):
 
 class SgnnStepWs(ctypes.Structure):
     """struct sgnn_step_ws (include/sgnn.h)."""
-    _fields_ = [("radius_ws", c_void_p), ("rowptr", c_void_p), ("send", c_void_p), ("recv", c_void_p),
+    _fields_ = [("struct_size", c_int64), ("radius_ws", c_void_p), ("rowptr", c_void_p), ("send", c_void_p), ("recv", c_void_p),
                 ("edge_cap", c_int64), ("e0t", c_void_p), ("x_a", c_void_p), ("x_b", c_void_p),
                 ("u", c_void_p), ("v", c_void_p), ("agg", c_void_p), ("cin", c_void_p), ("cout", c_void_p),
                 ("u2", c_void_p), ("v2", c_void_p), ("uvl", c_void_p), ("step_flags", c_void_p),
@@ -77,6 +79,8 @@ SLAB_EDGE, SLAB_NODE, SLAB_UV, SLAB_DECODER, SLAB_ENC_NODE, SLAB_ENC_EDGE = rang
 SIGNATURES = {
     "sgnn_version": (ctypes.c_char_p, []),
     "sgnn_last_error": (ctypes.c_char_p, []),
+    "sgnn_abi_version": (c_int32, []),
+    "sgnn_step_flag_words": (c_int32, []),
     "sgnn_radius_workspace_bytes": (ctypes.c_size_t, [c_int64, c_int32, c_int32]),
     "sgnn_radius_graph": (ctypes.c_int, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int32,
                                          c_float, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
@@ -204,11 +208,20 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise SgnnError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                         "(the HIP library is required; there is no CPU fallback)")
+    if os.path.abspath(path) != os.path.abspath(PRODUCT_LIB):
+        import sys
+        import warnings
+        msg = f"sgnn_amd: loading a NON-PRODUCT library build {path} (SGNN_LIB / experiment tool)"
+        print("WARNING: " + msg, file=sys.stderr, flush=True)
+        warnings.warn(msg, stacklevel=2)
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.sgnn_abi_version() != ABI_VERSION or lib.sgnn_step_flag_words() != STEP_FLAG_WORDS:
+        raise SgnnError(f"{path}: ABI {lib.sgnn_abi_version()} / {lib.sgnn_step_flag_words()} flag words, this "
+                        f"binding expects {ABI_VERSION} / {STEP_FLAG_WORDS}: rebuild the library")
     _LIB = lib
     return lib
 

@@ -159,6 +159,23 @@ class EdgeGraph:
         return self._fused
 
 
+_GRAPH_CACHE: List[Tuple[torch.Tensor, int, int, "EdgeGraph"]] = []
+
+
+def cached_edge_graph(edge_index: torch.Tensor, n: int) -> EdgeGraph:
+    """The EdgeGraph of this edge_index tensor, built once while the tensor is unchanged: a block
+    called again on the same graph (each layer of a Processor / MultiScaleGNN called module by module)
+    reuses its groupings and fused CSR instead of rebuilding them (each build syncs the host).  Keyed
+    by tensor identity + its in-place version counter; the last few graphs are kept."""
+    for t, ver, nn_, g in _GRAPH_CACHE:
+        if t is edge_index and ver == edge_index._version and nn_ == n:
+            return g
+    g = EdgeGraph(edge_index, n)
+    _GRAPH_CACHE.insert(0, (edge_index, edge_index._version, n, g))
+    del _GRAPH_CACHE[4:]
+    return g
+
+
 # ----------------------------------------------------------------------------- Functions
 def _linears(seq: nn.Module) -> List[nn.Linear]:
     return [m for m in seq.modules() if isinstance(m, nn.Linear)]
@@ -353,7 +370,7 @@ def decoder_forward(dec: nn.Module, x: torch.Tensor) -> torch.Tensor:
 def processor_forward(proc: nn.Module, x, edge_index, edge_features, graph: Optional[EdgeGraph] = None):
     """Processor.forward (graph_network.py:276-293)."""
     x = _rows(x, "x")
-    g = graph if graph is not None else EdgeGraph(edge_index, x.shape[0])
+    g = graph if graph is not None else cached_edge_graph(edge_index, x.shape[0])
     e = _rows(edge_features, "edge_features")
     for gnn in proc.gnn_stacks:
         x, e = message_passing(gnn, x, g, e)
@@ -372,7 +389,8 @@ def ms_gnn_forward(gnn: nn.Module, x, g2m_ei, g2m_e, m2m_ei, m2m_e, m2g_ei, m2g_
     """MultiScaleGNN.forward (multi_scale_gnn.py:277-326), block by block."""
     x = _rows(x, "x")
     n = x.shape[0]
-    gs = graphs or {"g2m": EdgeGraph(g2m_ei, n), "m2m": EdgeGraph(m2m_ei, n), "m2g": EdgeGraph(m2g_ei, n)}
+    gs = graphs or {"g2m": cached_edge_graph(g2m_ei, n), "m2m": cached_edge_graph(m2m_ei, n),
+                    "m2g": cached_edge_graph(m2g_ei, n)}
     h = mlp(gnn.grid_node_encoder, True, x)
     eg = mlp(gnn.g2m_edge_encoder, True, _rows(g2m_e, "g2m_edge_features"))
     em = mlp(gnn.m2m_edge_encoder, True, _rows(m2m_e, "m2m_edge_features"))

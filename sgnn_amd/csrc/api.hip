@@ -26,5 +26,7 @@ int check_launch(const char* where) {
 
 }  // namespace sgnn
 
-extern "C" const char* sgnn_version(void) { return "sgnn-mi355x 0.1 (gfx950, fp32 MFMA)"; }
+extern "C" const char* sgnn_version(void) { return "sgnn-mi355x 0.6 (abi 6, gfx950, fp32 MFMA)"; }
+extern "C" int32_t sgnn_abi_version(void) { return SGNN_ABI_VERSION; }
+extern "C" int32_t sgnn_step_flag_words(void) { return SGNN_STEP_FLAG_WORDS; }
 extern "C" const char* sgnn_last_error(void) { return g_err; }

@@ -271,9 +271,10 @@ __global__ __launch_bounds__(kEw) void k_rows_to_tiles(const float* e, int64_t l
 // The inverse: tile position p (< E) -> row perm[p] of out (+)= scale * its units (the edge-latent
 // gradient of a module-level block backward back in the caller's COO order).
 __global__ __launch_bounds__(kEw) void k_tiles_to_rows(const float* e0t, int width, const int32_t* perm,
-                                                       const int32_t* rowptr, int64_t n, float scale, float* out,
-                                                       int64_t ld, int accumulate) {
-  const int64_t E = rowptr[n];
+                                                       const int32_t* rowptr, int64_t n, int64_t num_edges,
+                                                       float scale, float* out, int64_t ld, int accumulate) {
+  // the device edge count, bounded by the host's: `out` / `perm` are sized by num_edges
+  const int64_t E = min((int64_t)rowptr[n], num_edges);
   const int64_t total = E * width;
   for (int64_t t = (int64_t)blockIdx.x * kEw + threadIdx.x; t < total; t += (int64_t)gridDim.x * kEw) {
     const int64_t p = t / width;
@@ -297,7 +298,7 @@ extern "C" int sgnn_edge_tiles_to_rows(const float* e0t, int32_t width, const in
     return set_error(SGNN_ERR_INVALID, "edge_tiles_to_rows: bad arguments");
   if (num_edges == 0) return SGNN_OK;
   hipLaunchKernelGGL(k_tiles_to_rows, dim3(ew_grid(num_edges * width)), dim3(kEw), 0, static_cast<hipStream_t>(stream),
-                     e0t, width, perm, rowptr, n, scale, out, ld, accumulate ? 1 : 0);
+                     e0t, width, perm, rowptr, n, num_edges, scale, out, ld, accumulate ? 1 : 0);
   return check_launch("edge_tiles_to_rows");
 }
 

@@ -33,10 +33,13 @@ int device_cus() {
 // The one-launch step's arguments when it applies to this call (step16.hip):
 // hidden 64, nmlp_layers 1 everywhere, 2..10 layers, n <= 8192 particles, a
 // grid of <= one workgroup per CU, and the kernel's LDS under 160 KB.
+// a workspace struct from a caller built against this header revision (include/sgnn.h struct_size)
+bool ws_ok(const sgnn_step_ws* ws) { return ws && ws->struct_size == (int64_t)sizeof(sgnn_step_ws); }
+
 bool step16_plan(const sgnn_epd* m, const sgnn_step_in* in, const float* pos_seq, const sgnn_step_ws* ws,
                  float* pred, float* next_pos, float* window_out, sgnn::Step16Args* out) {
   using namespace sgnn;
-  if (!m || !in || !ws || !ws->uvl || !ws->step_flags || !ws->step_deg) return false;
+  if (!m || !in || !ws_ok(ws) || !ws->uvl || !ws->step_flags || !ws->step_deg) return false;
   const int L = m->nlayers;
   const int64_t n = in->n;
   const int d = in->dim, T = in->T;
@@ -163,6 +166,9 @@ static int predict_impl(const sgnn_epd* m, const sgnn_step_in* in, const float* 
   using namespace sgnn;
   if (!m || !in || !pos_seq || !ws || !pred || !next_pos || m->nlayers < 1 || !m->edge || !m->node)
     return set_error(SGNN_ERR_INVALID, "predict_positions: bad arguments");
+  if (!ws_ok(ws))
+    return set_error(SGNN_ERR_INVALID, "predict_positions: sgnn_step_ws.struct_size != sizeof(sgnn_step_ws) "
+                                       "(caller built against another include/sgnn.h revision)");
   if (window_out && window_out == pos_seq)
     return set_error(SGNN_ERR_INVALID, "predict_positions: window_out aliases pos_seq");
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -346,7 +352,7 @@ extern "C" int sgnn_rollout_one_step(const sgnn_epd* m, const sgnn_step_in* in, 
 
 extern "C" int sgnn_step_check(const sgnn_step_ws* ws, void* stream) {
   using namespace sgnn;
-  if (!ws) return set_error(SGNN_ERR_INVALID, "step_check: bad arguments");
+  if (!ws_ok(ws)) return set_error(SGNN_ERR_INVALID, "step_check: bad arguments (or sgnn_step_ws.struct_size)");
   if (!ws->step_flags) return SGNN_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t word = 0;

@@ -27,6 +27,17 @@ from ._hip import SgnnMlp, check, lib, stream_ptr
 MAX_NUM_NEIGHBORS = 20  # learned_simulator.py:117
 FUSED_MAX_N = 8192      # fused per-layer kernel for graphs up to this size (sgnn_predict_positions)
 
+# Test hook (include/sgnn.h sgnn_step_ws.step_skew): workspaces created after set_test_step_skew(k) make
+# the one-launch step's tiles sleep before their phase publishes.  0 in every product run; no environment
+# variable reaches it.
+_TEST_STEP_SKEW = 0
+
+
+def set_test_step_skew(k: int) -> None:
+    """Uneven-load test hook for the one-launch step's hand-off (tests / tools only)."""
+    global _TEST_STEP_SKEW
+    _TEST_STEP_SKEW = int(k)
+
 
 def _ptr(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else t.data_ptr()
@@ -120,13 +131,13 @@ class StepWorkspace:
         # one-launch step buffers: allocated by prepare_step the first time sgnn_step_path says a call
         # takes that path (every layer's node halves, the per-workgroup phase counters, the neighbour counts)
         self.uvl = self.step_flags = self.step_deg = None
-        self.c = _hip.SgnnStepWs(radius_ws=self.radius_ws_ptr(), rowptr=self.rowptr.data_ptr(),
+        self.c = _hip.SgnnStepWs(struct_size=ctypes.sizeof(_hip.SgnnStepWs), radius_ws=self.radius_ws_ptr(), rowptr=self.rowptr.data_ptr(),
                                  send=self.send.data_ptr(), recv=self.recv.data_ptr(), edge_cap=self.edge_cap,
                                  e0t=self.e0t.data_ptr(), x_a=self.x_a.data_ptr(), x_b=self.x_b.data_ptr(),
                                  u=self.u.data_ptr(), v=self.v.data_ptr(), agg=self.agg.data_ptr(),
                                  cin=self.cin.data_ptr(), cout=self.cout.data_ptr(),
                                  u2=_ptr(self.u2), v2=_ptr(self.v2), uvl=0, step_flags=0, step_deg=0,
-                                 step_poll_limit=0, step_skew=int(os.environ.get("SGNN_STEP_SKEW", "0")))
+                                 step_poll_limit=0, step_skew=_TEST_STEP_SKEW)
         self.device = device
         # False: never allocate them (calls take the kernel sequence).  SGNN_ONE_LAUNCH=0: the same for every
         # workspace of the process (several processes sharing one device, include/sgnn.h "Co-residency")

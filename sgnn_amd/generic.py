@@ -96,7 +96,7 @@ def message_passing(block: nn.Module, x: torch.Tensor, edge_index: torch.Tensor,
     widths (engine.interaction_forward), else the differentiable path."""
     if not needs_grad(block, x, edge_features) and block_fast_shapes(block):
         return engine.interaction_forward(block, x, edge_index, edge_features)
-    return autograd.message_passing(block, x, autograd.EdgeGraph(edge_index, x.shape[0]), edge_features)
+    return autograd.message_passing(block, x, autograd.cached_edge_graph(edge_index, x.shape[0]), edge_features)
 
 
 def processor_forward(proc: nn.Module, x, edge_index, edge_features):

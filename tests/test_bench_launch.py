@@ -60,3 +60,19 @@ def test_cpu_thread_counts_skip_an_oversubscribed_affinity_leg(monkeypatch):
     monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(8)))
     monkeypatch.delenv("OMP_NUM_THREADS")
     assert bench.thread_counts() == ([8], None)
+
+
+def test_impossible_roofline_marks_the_leg_invalid():
+    """A fraction above the hardware peak is recorded as an error, its frac withheld (null), and
+    bench_line_errors() lists the leg, so no physically impossible number reaches the line unmarked;
+    a valid leg carries the achieved-HBM fraction of its profiled launch."""
+    sys.path.insert(0, ROOT)
+    import bench
+    ok = bench.roofline("k_step16", 7.18e9, 85e-6, "c1_r15", "rollout")
+    assert ok["frac"] is not None and 0 < ok["frac"] < 1 and "error" not in ok
+    assert 0 < ok["hbm_frac"] < 1 and ok["hbm_gbs"] > 0
+    bad = bench.roofline("k_step16", 7.18e9, 1e-6, "c1_r15", "rollout")
+    assert bad["frac"] is None and bad["invalid_frac"] > 1 and "error" in bad
+    line = {"roofline": ok, "rollout_extra": {"x": bench.leg({"value": 1.0, "roofline": bad})}}
+    assert [p for p, _ in bench.bench_line_errors(line)] == ["rollout_extra.x.rf"]
+    assert bench.bench_line_errors({"roofline": ok}) == []

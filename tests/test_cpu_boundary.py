@@ -40,6 +40,22 @@ def test_header_constants_match_python_mirror():
     err = int(re.search(r"#define SGNN_STEP_FLAG_ERR (\d+)", src).group(1))
     assert (words, err) == (_hip.STEP_FLAG_WORDS, _hip.STEP_FLAG_ERR)
     assert 256 * 16 <= err < words   # 256 counters 64 B apart, then the error word
+    abi = int(re.search(r"#define SGNN_ABI_VERSION (\d+)", src).group(1))
+    lib = _hip.load_library()
+    assert abi == _hip.ABI_VERSION == lib.sgnn_abi_version()
+    assert lib.sgnn_step_flag_words() == words
+
+
+def test_step_workspace_struct_size_leads_the_struct():
+    """ABI guard (include/sgnn.h): sgnn_step_ws starts with struct_size, which the Python mirror fills
+    with its own size; a caller built against another header revision is refused (CPU-side: the
+    check runs before any device work, so a wrong size returns SGNN_ERR_INVALID without a GPU)."""
+    from sgnn_amd import _hip
+    assert _hip.SgnnStepWs._fields_[0] == ("struct_size", ctypes.c_int64)
+    ws = _hip.SgnnStepWs(struct_size=ctypes.sizeof(_hip.SgnnStepWs) - 8)
+    lib = _hip.load_library()
+    assert lib.sgnn_step_check(ctypes.byref(ws), None) == _hip.SGNN_ERR_INVALID
+    assert "struct_size" in lib.sgnn_last_error().decode()
 
 
 def test_host_only_size_queries():

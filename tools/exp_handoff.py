@@ -39,9 +39,9 @@ if __name__ == "__main__" and sys.argv[1] == "build":
 
 variant = sys.argv[2]
 skew = int(sys.argv[3]) if len(sys.argv) > 3 else 0
-os.environ["SGNN_STEP_SKEW"] = str(skew)
 import torch  # noqa: E402
-from sgnn_amd import _hip  # noqa: E402
+from sgnn_amd import _hip, engine  # noqa: E402
+engine.set_test_step_skew(skew)
 _hip.load_library(lib_path(variant))
 from tests import test_gpu_parity as tp, test_gpu_step as ts  # noqa: E402
 
