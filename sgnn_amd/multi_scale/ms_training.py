@@ -320,10 +320,8 @@ class MultiScaleTrainer:
         particle index, so every rank draws its own slice."""
         pos = position.to(torch.float32).contiguous()
         n = pos.shape[0]
-        if n_global is None or particle_offset is None:
-            n_g, off = self.dp.layout(n, pos.device)
-            n_global = n_g if n_global is None else n_global
-            particle_offset = off if particle_offset is None else particle_offset
+        # no collective / host sync here: train.DataParallel.plan (deferred: the count rides in the all-reduce)
+        inv_count, particle_offset, deferred = self.dp.plan(n, n_global, particle_offset)
         if noise is None:
             noise, noisy = device_random_walk_noise(pos, self.noise_std, offset=particle_offset)
         else:
@@ -331,10 +329,10 @@ class MultiScaleTrainer:
             noisy = (pos + noise).contiguous()
         if not self.fused:   # differentiable width-generic path (e.g. nedge_out != latent_dim)
             from ..train import autograd_step
-            autograd_step(self, lambda: self.sim.predict_accelerations(
+            count = autograd_step(self, lambda: self.sim.predict_accelerations(
                 next_position.to(pos.device, torch.float32), noise, pos, None, particle_types),
-                next_strain.to(pos.device, torch.float32), n_global)
-            return self._finish(self.flat.loss, n_global)
+                next_strain.to(pos.device, torch.float32), inv_count, n if deferred else None)
+            return self._finish(self.flat.loss, count)
         inp, _ = self.sim._step_inputs(noisy, particle_types)
         n, T, _ = noisy.shape
         tw = self.workspace(n, T, pos.device)
@@ -351,20 +349,26 @@ class MultiScaleTrainer:
                 works.append(self.dp.allreduce_async(self.flat.comm[ranges[b][0]:ranges[b][1]], stream))
         train_backward(self.gnn, inp, tw, self.grads, rg, rm, next_pos=next_position.to(torch.float32).contiguous(),
                        noise=noise, next_strain=next_strain.to(torch.float32).contiguous(), w_pos=self.w_pos,
-                       w_strain=self.w_strain, inv_count=1.0 / n_global, timers=timers, emb_weight=emb,
+                       w_strain=self.w_strain, inv_count=inv_count, timers=timers, emb_weight=emb,
                        emb_grad=self.grads.get("_particle_type_embedding.weight"), block_done=block_done)
+        if deferred:
+            self.dp.put_count(self.flat.loss, n)
         if block_done is None:
             self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
         else:   # encoders, head and loss sums after the final reduction; then wait for the blocks' buckets
             self.dp.allreduce_(*[self.flat.comm[a:b] for a, b in self._buckets[1]])
             for w in works:
                 w.wait()
+        count = self.dp.take_count(self.flat.grad, self.flat.loss) if deferred else 1.0 / inv_count
         self.opt.step()
-        return self._finish(tw.loss_out, n_global)
+        return self._finish(tw.loss_out, count)
 
-    def _finish(self, lo: torch.Tensor, n_global: int) -> dict:
+    def _finish(self, lo: torch.Tensor, n_global) -> dict:
+        """`n_global`: an int, or (deferred counts) the all-reduced count as a device scalar."""
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6
         self.step += 1
+        if not torch.is_tensor(n_global):
+            n_global = int(round(n_global))
         return {"loss": lo[0] / n_global, "loss_position": (lo[1] + lo[2] + lo[3]) / n_global,
                 "loss_strain": lo[4] / n_global, "loss_xyz": lo[1:4] / n_global,
                 "n_global": n_global, "lr": self.opt.lr}

@@ -88,6 +88,38 @@ class DataParallel:
     def global_count(self, n_local: int, device) -> int:
         return self.layout(n_local, device)[0]
 
+    # The counts of a step whose caller does not pass (n_global, particle_offset): no collective and no
+    # host sync before the step's work is queued.  The backward then forms the gradient of this rank's
+    # loss SUM (inv_count 1), the rank's particle count rides in the flat buffer's tail through the SAME
+    # sum all-reduce(s) as the gradient (two float slots, hi * 2^20 + lo: exact for any count up to
+    # 2^44 over up to 16 ranks), and the reduced gradient and loss sums are divided by the reduced count
+    # on the device (the gradient is linear in the loss scale, so this is the reference's mean over the
+    # concatenated batch, train.py:268, up to fp32 rounding of where the 1/N is applied).  The noise
+    # stream offset is the rank's own 2^40-particle slice (disjoint across ranks; pass particle_offset,
+    # e.g. from split_batch's host-side counts as train() does, for the single-process stream).
+    COUNT_HI, COUNT_LO = 6, 7            # slots of FlatParams.loss (the loss sums use 0..4)
+    RANK_NOISE_STRIDE = 1 << 40
+
+    def plan(self, n_local: int, n_global: Optional[int], particle_offset: Optional[int]):
+        """(inv_count for the backward kernels, particle offset, deferred) of one step."""
+        if self.world == 1:
+            return 1.0 / (n_global or n_local), particle_offset or 0, False
+        off = self.rank * self.RANK_NOISE_STRIDE if particle_offset is None else particle_offset
+        if n_global is None:
+            return 1.0, off, True
+        return 1.0 / n_global, off, False
+
+    def put_count(self, loss_tail: torch.Tensor, n_local: int) -> None:
+        """This rank's particle count into the all-reduced tail (queued after the backward's writes)."""
+        loss_tail[self.COUNT_HI] = float(n_local >> 20)
+        loss_tail[self.COUNT_LO] = float(n_local & ((1 << 20) - 1))
+
+    def take_count(self, grad: torch.Tensor, loss_tail: torch.Tensor) -> torch.Tensor:
+        """After the all-reduce: N_global as a device scalar; the gradient scaled by 1/N_global in place."""
+        cnt = loss_tail[self.COUNT_HI].double() * float(1 << 20) + loss_tail[self.COUNT_LO].double()
+        grad.mul_((1.0 / cnt).float())
+        return cnt.float()
+
     def overlaps_buckets(self) -> bool:
         """Per-layer gradient buckets all-reduced on the side stream while the
         layers below run their backward (device collectives only: gloo stages
@@ -224,10 +256,8 @@ class Trainer:
         ranks draw disjoint slices of the one-process noise."""
         pos = position.to(torch.float32).contiguous()
         n = pos.shape[0]
-        if n_global is None or particle_offset is None:
-            n_g, off = self.dp.layout(n, pos.device)
-            n_global = n_g if n_global is None else n_global
-            particle_offset = off if particle_offset is None else particle_offset
+        # no collective / host sync here: see DataParallel.plan (deferred: the count rides in the all-reduce)
+        inv_count, particle_offset, deferred = self.dp.plan(n, n_global, particle_offset)
         if noise is None:       # fused: draw + cumsum twice + noisy window in one kernel
             # the seed is a draw from torch's CPU generator: the same on every
             # rank (it also drives the shared shuffle); the offset separates them
@@ -237,7 +267,7 @@ class Trainer:
             noisy = (pos + noise).contiguous()                      # learned_simulator.py:467
         if not self.fused:
             return self._generic_step(pos, noise, next_position, next_strain, nparticles_per_example,
-                                      particle_types, n_global)
+                                      particle_types, inv_count, deferred)
         inp, _ = self.sim._step_inputs(noisy, nparticles_per_example, particle_types)
         n, T, _ = noisy.shape
         tw = self.workspace(n, T, pos.device)
@@ -255,9 +285,11 @@ class Trainer:
         training.train_backward(self.epd, radius, inp, tw, self.grads, timers=timers,
                                 next_pos=next_position.to(torch.float32).contiguous(), noise=noise,
                                 next_strain=next_strain.to(torch.float32).contiguous(),
-                                w_pos=self.w_pos, w_strain=self.w_strain, inv_count=1.0 / n_global,
+                                w_pos=self.w_pos, w_strain=self.w_strain, inv_count=inv_count,
                                 emb_weight=emb, emb_grad=self.grads.get("_particle_type_embedding.weight"),
                                 layer_done=layer_done)
+        if deferred:
+            self.dp.put_count(self.flat.loss, n)
         if layer_done is None:
             self.dp.allreduce_(self.flat.comm)   # gradient + loss sums: one collective
         else:
@@ -266,32 +298,39 @@ class Trainer:
             self.dp.allreduce_(self.flat.comm[:lo], self.flat.comm[hi:])
             for w in works:
                 w.wait()
+        count = self.dp.take_count(self.flat.grad, self.flat.loss) if deferred else 1.0 / inv_count
         self.opt.step()
-        return self._finish(n_global)
+        return self._finish(count)
 
-    def _finish(self, n_global: int) -> dict:
+    def _finish(self, n_global) -> dict:
+        """`n_global`: an int, or (deferred counts) the all-reduced count as a device scalar."""
         # train.py:276-278: LR for the NEXT step, computed from the pre-increment step
         self.opt.lr = self.lr_init * (self.lr_decay ** (self.step / self.lr_decay_steps)) + 1e-6
         self.step += 1
+        if not torch.is_tensor(n_global):
+            n_global = int(round(n_global))
         lo = self.flat.loss[:5] / n_global     # one kernel; the terms are views of it
         return {"loss": lo[0], "loss_position": lo[1:4].sum(), "loss_strain": lo[4],
                 "loss_xyz": lo[1:4], "n_global": n_global, "lr": self.opt.lr}
 
     def _generic_step(self, pos, noise, next_position, next_strain, nparticles_per_example, particle_types,
-                      n_global: int) -> dict:
+                      inv_count: float, deferred: bool) -> dict:
         """The step at shapes the fused kernels are not built for (autograd_step)."""
-        autograd_step(self, lambda: self.sim.predict_accelerations(
+        count = autograd_step(self, lambda: self.sim.predict_accelerations(
             next_position.to(pos.device, torch.float32), noise, pos, nparticles_per_example, particle_types),
-            next_strain.to(pos.device, torch.float32), n_global)
-        return self._finish(n_global)
+            next_strain.to(pos.device, torch.float32), inv_count, pos.shape[0] if deferred else None)
+        return self._finish(count)
 
 
-def autograd_step(trainer, predict, next_strain: torch.Tensor, n_global: int) -> None:
+def autograd_step(trainer, predict, next_strain: torch.Tensor, inv_count: float, deferred_n: Optional[int] = None):
     """One optimisation step on the differentiable width-generic path (HIP forward
     and backward, sgnn_amd.autograd): `predict()` = predict_accelerations, the
     reference's loss (train.py:257-268 / multi_scale_train.py:160-176) as this
-    rank's sums over N_global, backward into the flat gradient views, the loss
-    sums into the buffer's tail, one all-reduce of both, the fused Adam."""
+    rank's sums times inv_count = 1/N_global, backward into the flat gradient views,
+    the loss sums into the buffer's tail, one all-reduce of both, the fused Adam.
+    deferred_n (DataParallel.plan): inv_count is 1 and this rank's count rides in the
+    all-reduce; the gradient is scaled by the reduced count after it.  Returns N_global
+    (an int, or the reduced count as a device scalar)."""
     flat = trainer.flat
     flat.comm.zero_()
     with torch.enable_grad():
@@ -299,14 +338,18 @@ def autograd_step(trainer, predict, next_strain: torch.Tensor, n_global: int) ->
         sq = (pa - ta) ** 2
         ls = (ps - next_strain) ** 2
         per = trainer.w_pos * sq.sum(-1) + trainer.w_strain * ls
-        (per.sum() / n_global).backward()   # AccumulateGrad adds into the flat gradient views
+        (per.sum() * inv_count).backward()   # AccumulateGrad adds into the flat gradient views
     with torch.no_grad():
         d = sq.shape[1]
         flat.loss[0] = per.sum()
         flat.loss[1:1 + d] = sq.sum(0)
         flat.loss[4] = ls.sum()
+        if deferred_n is not None:
+            trainer.dp.put_count(flat.loss, deferred_n)
     trainer.dp.allreduce_(flat.comm)
+    count = trainer.dp.take_count(flat.grad, flat.loss) if deferred_n is not None else 1.0 / inv_count
     trainer.opt.step()
+    return count
 
 
 # ---------------------------------------------------------------------------

@@ -11,9 +11,12 @@ import torch
 LR = 1e-3
 STEPS = 2
 # single scale: the real Taylor-bar sizes (120/160/200 x 40 lattices = 4,800 / 6,400 / 8,000 particles)
-SS_GRAPHS = [(120, 40), (160, 40), (200, 40), (100, 40)]
+SS_GRAPHS = [(120, 40), (160, 40), (200, 40), (100, 40), (160, 40), (200, 40), (120, 40), (160, 40)]
 SS_RANKS = [[0, 1], [2]]          # rank 0 holds two graphs (4,800 + 6,400), rank 1 one (8,000)
 SS_RANKS4 = [[0], [1], [2], [3]]  # four ranks, one graph each (4,800 / 6,400 / 8,000 / 4,000)
+# C3 at its own shape (BASELINE configs[2], train.py:257-273): a global batch of 8 real-size Taylor graphs,
+# one whole graph per rank, 8 ranks -- 4,800 / 6,400 / 8,000 / 4,000 / 6,400 / 8,000 / 4,800 / 6,400
+SS_RANKS8 = [[g] for g in range(8)]
 # multi scale (nmlp_layers 2, two scales): one graph per rank, unequal sizes
 MS_GRAPHS = [(30, 14), (36, 12), (28, 15), (33, 12)]
 MS_RANKS = [[0], [1]]
@@ -67,7 +70,7 @@ def run_single_scale(graph_ids, overlap=False, force=False):
         tr.dp.host_staging = False
         tr.dp.force_overlap = force
         assert tr.dp.world == 1 or tr.dp.overlaps_buckets()
-    wins = [_window(nx, ny, T_SS, 100 + g) for g, (nx, ny) in enumerate(SS_GRAPHS)]
+    wins = {g: _window(*SS_GRAPHS[g], T_SS, 100 + g) for g in graph_ids}
     losses = []
     for s in range(STEPS):
         parts = [wins[g][s] for g in graph_ids]
@@ -142,5 +145,6 @@ CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, 
          "ms_rccl1": (run_multi_scale_rccl, MS_GRAPHS, [[0, 1]]),
          # four ranks (the C3 / C5 sharding at world 4; gloo, the ranks share the one leased GPU)
          "ss4_overlap": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS4),
+         "ss8": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS8),
          "ms4": (run_multi_scale, MS_GRAPHS, MS_RANKS4)}
 RCCL_CASES = {"ss_rccl1", "ms_rccl1"}

@@ -99,6 +99,77 @@ def test_whole_graph_dp_matches_single_process(world):
         np.testing.assert_array_equal(res[0][2], r[2])
 
 
+def _deferred_worker(rank, world, port, q):
+    """The sync-free DP step (DataParallel.plan / put_count / take_count, what Trainer.train_step does when
+    the caller passes no n_global): no all_gather, the gradient of this rank's loss SUM and its particle
+    count go through ONE sum all-reduce, the count scales the reduced gradient afterwards."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sgnn_amd.train import DataParallel, split_batch
+
+    def no_gather(*a, **k):
+        raise AssertionError("the deferred DP step must not gather the counts")
+    dist.all_gather = no_gather
+    dp = DataParallel()
+    mine = [_graphs()[i] for i in split_batch(list(range(len(GRAPH_DIMS))), rank, world)]
+    n_local = sum(g[0].shape[0] for g in mine)
+    inv, off, deferred = dp.plan(n_local, None, None)
+    assert deferred and inv == 1.0 and off == rank * DataParallel.RANK_NOISE_STRIDE
+    flat, loss = _oracle_grads(mine, inv)
+    comm = torch.zeros(flat.numel() + 8)
+    comm[:flat.numel()] = flat
+    tail = comm[flat.numel():]
+    tail[0] = loss
+    dp.put_count(tail, n_local)
+    dp.allreduce_(comm)
+    n_global = dp.take_count(comm[:flat.numel()], tail)
+    q.put((rank, int(n_global), comm[:flat.numel()].numpy().copy(), float(tail[0] / n_global)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_deferred_count_dp_matches_single_process(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_deferred_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    graphs = _graphs()
+    n_total = sum(g[0].shape[0] for g in graphs)
+    ref_flat, ref_loss = _oracle_grads(graphs, 1.0 / n_total)
+    for rank, n_global, flat, loss in res:
+        assert n_global == n_total
+        np.testing.assert_allclose(flat, ref_flat.numpy(), rtol=1e-4, atol=1e-7)
+        assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss)
+    for r in res[1:]:
+        np.testing.assert_array_equal(res[0][2], r[2])
+
+
+def test_count_slots_are_exact_for_large_counts():
+    """put_count splits the count into two float slots (hi * 2^20 + lo), so the summed count stays
+    exact in fp32 far past 2^24 particles (C5: 8 ranks x ~1 M)."""
+    from sgnn_amd.train import DataParallel
+    dp = DataParallel()
+    tails = []
+    for n in (1_000_003, 999_999_937, 5, (1 << 40) + 12345):
+        t = torch.zeros(8)
+        dp.put_count(t, n)
+        tails.append((n, t))
+    tot = torch.zeros(8)
+    for _, t in tails:
+        tot += t
+    g = torch.ones(4)
+    cnt = dp.take_count(g, tot)
+    n_sum = sum(n for n, _ in tails)
+    assert int(tot[6].double() * 2 ** 20 + tot[7].double()) == n_sum
+    assert abs(float(cnt) - n_sum) <= 1e-7 * n_sum
+
+
 def _layout_worker(rank, world, port, q):
     """Ragged, changing per-rank counts: rank 0 repeats n, rank 1 changes it
     every step.  Every step = layout (one all_gather) + one gradient-sized

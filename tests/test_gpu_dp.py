@@ -13,7 +13,10 @@ error, at most 2 lr per step).  `ss_rccl1`: the same single-scale step on a one-
 group with the overlapped per-layer bucket all-reduces forced on (async collectives from the side
 stream, handles waited before Adam): the collective path C3 / C5 use, on real RCCL; `ms_overlap` /
 `ms_rccl1`: the multi-scale trainer's per-block buckets the same way; `ss4_overlap` / `ms4`: four ranks
-(one graph each), the single-scale one with the overlapped bucket all-reduces."""
+(one graph each), the single-scale one with the overlapped bucket all-reduces; `ss8`: C3 at its own
+shape -- eight ranks, one real-size Taylor graph each (the 8-graph global batch), overlapped buckets.
+Every case calls train_step without n_global: the ranks' counts ride in the gradient all-reduce
+(train.DataParallel.plan), no per-step gather."""
 import os
 import socket
 import subprocess
@@ -36,7 +39,8 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("case", ["ss", "ms", "ss_overlap", "ss_rccl1", "ms_overlap", "ms_rccl1", "ss4_overlap", "ms4"])
+@pytest.mark.parametrize("case", ["ss", "ms", "ss_overlap", "ss_rccl1", "ms_overlap", "ms_rccl1", "ss4_overlap", "ms4",
+                                  "ss8"])
 def test_two_ranks_match_one_process(case, tmp_path):
     from tests.dp_cases import CASES, LR, STEPS
     run, _, ranks = CASES[case]
@@ -46,7 +50,7 @@ def test_two_ranks_match_one_process(case, tmp_path):
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_dp_child.py"), case, str(r),
                                str(world), port, outs[r]], cwd=ROOT, env=env) for r in range(world)]
     try:
-        codes = [p.wait(timeout=100) for p in procs]
+        codes = [p.wait(timeout=100 + 20 * world) for p in procs]
     finally:
         for p in procs:
             if p.poll() is None:
