@@ -198,6 +198,13 @@ def forward_case(name, pos_seq, npe, types_, dim, T, H, L, R, ntypes=1, emb=9, s
             out["rollout_predicted"] = ro["predicted_rollout"]
             out["rollout_strain"] = ro["predicted_strain"]
             out["rollout_rmse_position"] = ro["rmse_position"]
+            # teacher-forced rollout (evaluate.py:140-143): every step's window ends with ground truth
+            ro1 = ref_eval.rollout(sim, torch.tensor(pos_seq), pt, torch.tensor(n), strains,
+                                   nsteps=pos_seq.shape[1] - T, particle_dim=dim, device="cpu",
+                                   input_sequence_length=T, inference_mode="one_step")
+            out["onestep_predicted"] = ro1["predicted_rollout"]
+            out["onestep_strain"] = ro1["predicted_strain"]
+            out["onestep_rmse_position"] = ro1["rmse_position"]
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **out)
     print(f"{name}: N={pos_seq.shape[0]} E={out['edge_index'].shape[1]} -> {os.path.getsize(path)/1e3:.0f} KB")
@@ -315,10 +322,13 @@ def main(only=None):
         return multi_scale_train_case("ms_train2d", synthetic.lattice_2d(16, 12, x0=-1.75), 6, 64, 2, 3, 2,
                                       2.0, seed=6)
     T = 11
-    # 1) tiny 2D, reference default radius 0.6, per-layer latents + 3-step rollout
+    # 1) tiny 2D, reference default radius 0.6, per-layer latents + 3-step rollout (autoregressive and
+    #    one_step)
     seq = synthetic.trajectory(synthetic.lattice_2d(10, 8), T + 3, seed=1)
     forward_case("tiny2d_r06", seq, [seq.shape[0]], np.zeros(seq.shape[0]), 2, T, 64, 5, 0.6,
                  latents=True, rollout_frames=3)
+    if only == "tiny2d":
+        return
     # 2) two examples overlapping in space: edges must never cross examples
     a = synthetic.trajectory(synthetic.lattice_2d(10, 8), T, seed=2)
     b = synthetic.trajectory(synthetic.lattice_2d(12, 6, x0=0.5, y0=-9.5), T, seed=3)

@@ -69,6 +69,26 @@ def test_rollout_matches_reference():
     _close(out["predicted_strain"], z["rollout_strain"], atol=4 * ATOL, what="rollout strain")
 
 
+def test_one_step_rollout_matches_reference():
+    """evaluate.rollout(..., inference_mode='one_step') -- ONE sgnn_rollout_one_step call -- against the
+    reference's own teacher-forced rollout (evaluate.py:140-143; golden onestep_* arrays)."""
+    from sgnn_amd import evaluate
+    z = golden("tiny2d_r06")
+    hp = hparams(z)
+    sim = product_sim(z)
+    pos = torch.from_numpy(z["positions"]).cuda()
+    n = pos.shape[0]
+    strains = torch.zeros(pos.shape[1], n, device="cuda")
+    out = evaluate.rollout(sim, pos, torch.zeros(n, dtype=torch.long, device="cuda"), torch.tensor(n),
+                           strains, nsteps=pos.shape[1] - hp["T"], particle_dim=hp["dim"], device="cuda",
+                           input_sequence_length=hp["T"], inference_mode="one_step")
+    scale = float(np.max(z["acc_std"]))
+    _close(out["predicted_rollout"], z["onestep_predicted"], atol=4 * ATOL * scale, rtol=1e-6,
+           what="one_step rollout positions")
+    _close(out["predicted_strain"], z["onestep_strain"], atol=4 * ATOL, what="one_step rollout strain")
+    np.testing.assert_allclose(out["rmse_position"], z["onestep_rmse_position"], rtol=1e-3, atol=1e-7)
+
+
 def _lattice_case(nx, ny, radius, seed, n_ex=1):
     from sgnn_amd import synthetic
     seqs = [synthetic.trajectory(synthetic.lattice_2d(nx, ny, x0=0.25 + 0.1 * k), 11, seed=seed + k)
