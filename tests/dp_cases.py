@@ -82,11 +82,17 @@ def run_single_scale(graph_ids, overlap=False, force=False):
     return _result(tr, losses, sim)
 
 
-def run_multi_scale(graph_ids, overlap=False, force=False):
+def run_multi_scale(graph_ids, overlap=False, force=False, global_ids=None):
     """STEPS MultiScaleTrainer steps on `graph_ids` (one static graph each,
     merged block-diagonally when a process holds several).  overlap: the
     per-block gradient buckets go out asynchronously from the side stream
-    during the backward (as run_single_scale)."""
+    during the backward (as run_single_scale).  global_ids: the whole global
+    batch (every rank's graphs in rank order): (n_global, particle_offset) are
+    then passed host-side, as train() does, so the 1/N_global scaling sits
+    inside the backward exactly as in the one-process run -- these small 2D
+    multi-scale graphs are too ill-conditioned in fp32 for the deferred count
+    path's different rounding (its scaling after the sum all-reduce) to stay
+    inside the gradient bound; the single-scale cases exercise that path."""
     from sgnn_amd.multi_scale import MultiScaleSimulator
     from sgnn_amd.multi_scale.ms_training import MultiScaleTrainer
     from sgnn_amd.multi_scale.multi_scale_graph import build_static_multi_scale_graph
@@ -102,10 +108,17 @@ def run_multi_scale(graph_ids, overlap=False, force=False):
         tr.dp.host_staging = False
         tr.dp.force_overlap = force
         assert tr.dp.world == 1 or tr.dp.overlaps_buckets()
+    kw = {}
+    if global_ids is not None:
+        sizes = {g: MS_GRAPHS[g][0] * MS_GRAPHS[g][1] for g in global_ids}
+        first = global_ids.index(graph_ids[0])
+        kw = dict(n_global=sum(sizes.values()), particle_offset=sum(sizes[g] for g in global_ids[:first]))
     losses = []
     for s in range(STEPS):
         pos, nxt, strain, noise = _cat([wins[g][s] for g in graph_ids])
-        out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), noise=noise.cuda())
+        if kw:
+            assert sum(MS_GRAPHS[g][0] * MS_GRAPHS[g][1] for g in graph_ids) == pos.shape[0]
+        out = tr.train_step(pos.cuda(), nxt.cuda(), strain.cuda(), noise=noise.cuda(), **kw)
         losses.append(float(out["loss"]))
     torch.cuda.synchronize()
     return _result(tr, losses, sim)
@@ -125,17 +138,17 @@ def run_single_scale_rccl(graph_ids):
     return run_single_scale(graph_ids, overlap=True, force=dist.is_initialized())
 
 
-def run_multi_scale_overlap(graph_ids):
-    return run_multi_scale(graph_ids, overlap=True)
+def run_multi_scale_overlap(graph_ids, global_ids=None):
+    return run_multi_scale(graph_ids, overlap=True, global_ids=global_ids)
 
 
-def run_multi_scale_rccl(graph_ids):
+def run_multi_scale_rccl(graph_ids, global_ids=None):
     """The multi-scale trainer's per-block buckets on a one-rank RCCL (nccl) group (C5's collective
     path), as run_single_scale_rccl."""
     import torch.distributed as dist
     if dist.is_initialized():
         assert dist.get_backend() == "nccl"
-    return run_multi_scale(graph_ids, overlap=True, force=dist.is_initialized())
+    return run_multi_scale(graph_ids, overlap=True, force=dist.is_initialized(), global_ids=global_ids)
 
 
 CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, MS_GRAPHS, MS_RANKS),
@@ -148,3 +161,4 @@ CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, 
          "ss8": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS8),
          "ms4": (run_multi_scale, MS_GRAPHS, MS_RANKS4)}
 RCCL_CASES = {"ss_rccl1", "ms_rccl1"}
+MS_CASES = {"ms", "ms_overlap", "ms_rccl1", "ms4"}   # run(..., global_ids=...): host-side counts

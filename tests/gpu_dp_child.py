@@ -15,14 +15,14 @@ def main():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     import torch
     import torch.distributed as dist
-    from tests.dp_cases import CASES, RCCL_CASES
+    from tests.dp_cases import CASES, MS_CASES, RCCL_CASES
     if case in RCCL_CASES:   # RCCL (backend "nccl" on ROCm), one rank on the one GPU
         torch.cuda.set_device(0)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     run, _, ranks = CASES[case]
-    res = run(ranks[rank])
+    res = run(ranks[rank], global_ids=sum(ranks, [])) if case in MS_CASES else run(ranks[rank])
     torch.save(res, out)
     dist.barrier()
     dist.destroy_process_group()
