@@ -45,31 +45,39 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps())
 
 
+OBJDIR = os.path.join(LIBDIR, "obj")   # per-source objects (git- and gpurun-ignored): incremental rebuilds
+
+
 def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB) -> str:
     """Compile every csrc/*.hip for gfx950 and link `lib`.  `defines` (e.g.
-    SGNN_PROBE) are for experiment builds linked to another path."""
+    SGNN_PROBE) are for experiment builds linked to another path.  A source is
+    recompiled when it, any header, or this script is newer than its object."""
     if not force and not defines and lib == LIB and not needs_build():
         return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(OBJDIR, exist_ok=True)
     objs = []
     procs = []
-    tag = "".join("_" + d.lower() for d in defines)
+    tag = "".join("_" + d.lower().replace("=", "_") for d in defines)
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(ROOT, "include", "sgnn.h"), __file__]
+    newest_header = max(os.path.getmtime(h) for h in headers)
     for src in sources():
-        obj = os.path.join(LIBDIR, os.path.basename(src) + tag + ".o")
-        cmd = [HIPCC, *flags_for(src), *[f"-D{d}" for d in defines], "-c", src, "-o", obj,
+        obj = os.path.join(OBJDIR, os.path.basename(src) + tag + ".o")
+        objs.append(obj)
+        if (not force and os.path.exists(obj) and os.path.getmtime(obj) > os.path.getmtime(src)
+                and os.path.getmtime(obj) > newest_header):
+            continue
+        cmd = [HIPCC, *flags_for(src), *[f"-D{d}" for d in defines], "-c", src, "-o", obj + ".tmp",
                "-I", os.path.join(ROOT, "include")]
         if verbose:
             print(" ".join(cmd))
-        procs.append(subprocess.Popen(cmd))
-        objs.append(obj)
-    for p in procs:
+        procs.append((subprocess.Popen(cmd), obj))
+    for p, obj in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
+        os.replace(obj + ".tmp", obj)
     tmp = lib + ".tmp"
     subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs])
     os.replace(tmp, lib)
-    for o in objs:
-        os.remove(o)
     return lib
 
 

@@ -57,9 +57,10 @@ for r in range(reps):
     outs.append(pred.cpu().numpy())
     nt = path[1]
     err = np.abs(pred[:, -1].cpu().numpy() - ref_strain.numpy())
-    bad = np.nonzero(err > 2e-4 + 1e-4 * np.abs(ref_strain.numpy()))[0]
+    bad = np.nonzero(~(err <= 2e-4 + 1e-4 * np.abs(ref_strain.numpy())))[0]   # NaN counts as bad
+    nonfin = int((~np.isfinite(pred.cpu().numpy())).any(axis=1).sum())
     print(f"rep {r}: path {path}, timeout {ws.step_timeout()}, edges {ws.step_edges()}, bad particles {bad.size} "
-          f"max err {err.max():.3e}", flush=True)
+          f"max err {np.nanmax(err):.3e} nonfinite {nonfin}", flush=True)
     if bad.size and os.environ.get("DUMP_BAD") and not os.path.exists(os.environ["DUMP_BAD"] + "_e0.npy"):
         wsd = sim._workspace(n, 11, torch.device("cuda", 0))
         nHd = 5 * 2 * n * 64
