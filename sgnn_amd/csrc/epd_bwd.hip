@@ -2294,7 +2294,14 @@ const float* mid_w(const sgnn_mlp* m) { return m->nlin == 3 ? m->w2 : nullptr; }
 extern "C" int64_t sgnn_bwd_slab_floats(int32_t kind, int32_t hidden, int32_t feat, int32_t nlin) {
   if (kind < 0 || kind > SGNN_SLAB_ENC_EDGE || (nlin != 2 && nlin != 3) || hidden <= 0) return -1;
   const int64_t fpad = 32 * ((feat + 31) / 32);
-  return slab_nmat_floats(kind, hidden, fpad, nlin) + slab_nvec_floats(kind, hidden, nlin);
+  int64_t f = slab_nmat_floats(kind, hidden, fpad, nlin) + slab_nvec_floats(kind, hidden, nlin);
+  // the slab stride an odd multiple of 256 B: the slab reduction reads one 128-B segment from each of
+  // 512 slabs at a time, and strides that are multiples of 2-4 KB (round 5's) pile those reads onto few
+  // HBM channels.  Same-box A/B, ms/step: C2 training 1.937 -> 1.911, C3 1.919 -> 1.910, C5 494.5 -> 492.4
+  // (profiles/r06_ab_slab_stride.txt)
+  f = 64 * ((f + 63) / 64);
+  if ((f / 64) % 2 == 0) f += 64;
+  return f;
 }
 
 extern "C" int64_t sgnn_bwd_scratch_floats(int32_t kind, int32_t hidden, int64_t nitems, int32_t nlin) {

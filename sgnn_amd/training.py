@@ -473,6 +473,10 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
                               ws.rowptr.data_ptr(), ws.send.data_ptr(), ws.recv.data_ptr(), n,
                               ws.edge_cap, ctypes.byref(pk.enc_edge), ws.e0t.data_ptr(),
                               ctypes.byref(sv), s), "sgnn_encode_edges")
+    # x0, u, v of layer 0 come from the side stream.  The launch stream's wait is queued BEFORE the
+    # transpose below goes to the side stream: queued after it, the first edge layer started only once the
+    # transpose had finished (C2 trace, round 6: ~93 us idle on the launch stream)
+    main.wait_event(ev["encn"])
     # sender-sorted transpose of the new graph (for dV) on the side stream,
     # overlapping the forward layers; train_backward waits for it
     side.wait_event(ev["graph"])
@@ -481,7 +485,6 @@ def train_forward(epd: nn.Module, radius: float, inp: engine.StepInputs, tw: Tra
           "sgnn_transpose_csr")
     ev["tcsr"].record(side)
     nl = len(pk.edge)
-    main.wait_event(ev["encn"])          # x0, u, v of layer 0
     for k in range(nl):
         sv = _saves(h=tw.e_h[k], yhat=tw.e_yh[k], rstd=tw.e_rstd[k], h2=tw.e_h2[k])
         with _Timer(timers, "k_edge_layer(train)"):

@@ -26,6 +26,8 @@ elif sys.argv[1] == "one":   # child: one bench leg on one library
     torch.cuda.set_device(dev)
     if sys.argv[3] in ("train", "train-c3"):   # the C2 / C3 training step (kernel = the edge backward)
         r = bench.bench_train(sys.argv[3], 20, 5, 1, 0, dev, 0, 0)
+    elif sys.argv[3] == "c5":                  # the C5 multi-scale training step
+        r = bench.bench_ms_train("c5", 3, 1, 1, 0, dev, 0, 0)
     else:
         r = bench.bench_rollout(sys.argv[3], 20, 5, 1, 0, dev, 0, 0)
     print(json.dumps({"lib": sys.argv[2], "workload": sys.argv[3], "ms_per_step": r["ms_per_step"],
