@@ -55,7 +55,11 @@ typedef struct sgnn_mlp {
 
 /* Optional activation saves of the training forward (NULL pointer / NULL
  * struct = inference).  Edge tensors use the 32-edge tiled layout of e0t;
- * node tensors are row-major [N][H]; rstd is one float per item. */
+ * node tensors are row-major [N][H]; rstd is one float per item.
+ * sgnn_edge_layer / sgnn_edge_layer_bwd at hidden 128 with nlin 3: yhat and h2
+ * may both be NULL (h and rstd given) -- the backward then forms them again
+ * from h with the forward's own arithmetic (bit-identical), two [E][H] tensors
+ * less per layer; its scratch (sgnn_bwd_scratch_floats) holds the recomputed h2. */
 typedef struct sgnn_saves {
   float* h;     /* post-ReLU hidden of the MLP's first Linear */
   float* yhat;  /* LayerNorm-normalised (pre-affine) output */

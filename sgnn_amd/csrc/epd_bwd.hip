@@ -302,6 +302,9 @@ struct EdgeBwdArgs {
   int de0_accumulate;
   float* slab;
   int64_t slab_stride;
+  // hidden 128, nlin 3 with yh == NULL: the middle / last Linear's biases (the forward's h2 and yhat are
+  // recomputed from h in k_edge_items instead of saved)
+  const float *bm = nullptr, *bl = nullptr;
 };
 
 // W1E: this layer's dE0 / dW1e products run in-layer (de0t != NULL, the
@@ -1779,6 +1782,7 @@ void k_wgrad_half(WgradOp op, int nslab) {
 struct EdgeItemsArgs {
   EdgeBwdArgs b;
   float *dy_out, *d2_out;  // tiled scratch
+  float* h2_out;           // tiled scratch: the recomputed h2 (b.yh == NULL), B operand of dW_last
 };
 
 // (templated on TH; at H = 64 the fused k_edge_bwd measured faster: the
@@ -1813,6 +1817,18 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
   // per-tile products reads LDS instead of L2
   float* wlt = gam + H + kWaves * 32 * ldh;
   if (GW) stage_matrix_t(wlt, ldh, a.wl, H, H, H, H, H);
+  // recompute mode (round 6; hidden 128, nlin 3, a.yh == NULL): the forward's h2 = relu(Wm h1 + bm) and
+  // yhat = LN-normalised(Wl h2 + bl) are formed again from the saved h1 with the forward's own functions
+  // (mlp_tail, acc_layernorm_save: same operands, same MFMA order, so bit for bit the forward's values),
+  // instead of being saved: two [E][H] tensors less per block (C5: ~6 GB per block)
+  const bool rc = GW && NL == 3 && a.yh == nullptr;
+  float* vbm = wlt + H * ldh;
+  float* vbl = vbm + H;
+  if (rc) {
+    stage_vec(vbm, a.bm, H, H);
+    stage_vec(vbl, a.bl, H, H);
+  }
+  const float* hs2 = rc ? p.h2_out : a.hs2;
   __syncthreads();
   const int l = lane_id(), j = l & 31, w = wave_id();
   float* sl = gam + H + w * 32 * ldh;
@@ -1835,7 +1851,20 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
       f32x16 dm[TH], yh[TH];
       load_row_clayout<TH>(dm, a.dagg + (int64_t)rv * H);
       zero_if<TH>(dm, !valid);
-      load_tiled<TH>(yh, a.yh + tile * (32 * H));
+      if constexpr (GW && NL == 3) {
+        if (rc) {
+          f32x16 h1[TH], h2r[TH], y[TH];
+          load_tiled<TH>(h1, a.hs + tile * (32 * H));
+          mlp_tail<TH, 3, TH, true>(y, h2r, h1, a.wm, H, vbm, a.wl, H, vbl);
+          float rs_fwd;
+          acc_layernorm_save<TH>(y, gam, gam, yh, rs_fwd);   // (the affine output y is not used)
+          store_tiled<TH>(p.h2_out + tile * (32 * H), h2r);
+        } else {
+          load_tiled<TH>(yh, a.yh + tile * (32 * H));
+        }
+      } else {
+        load_tiled<TH>(yh, a.yh + tile * (32 * H));
+      }
       acc_layernorm_bwd<TH>(dm, yh, a.rstd[ec], gam, dy);
       zero_if<TH>(dy, !valid);
       wave_colsum<TH>(s_db, sl, dm, nvalid);
@@ -1852,7 +1881,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_items(EdgeItemsArgs p) {
       f32x16 d2[TH], act[TH];
       zero<TH>(d2);
       matvec_t<TH, TH, false>(d2, GW ? wlt : WlT, ldh, dy);
-      load_tiled<TH>(act, a.hs2 + tile * (32 * H));
+      load_tiled<TH>(act, hs2 + tile * (32 * H));   // (recompute mode: stored by this lane just above)
       relu_mask<TH>(d2, act, valid);
       store_tiled<TH>(p.d2_out + tile * (32 * H), d2);
       matvec_t<TH, TH, GW>(dh, WmT, ldl, d2);
@@ -2244,7 +2273,8 @@ WgradOp wg(const float* A, int a_tiled, int a_ld, int64_t a_len, const float* B,
 }
 
 constexpr size_t kItemsLds = 4 * (128 + (size_t)kWaves * 32 * (128 + 4));  // gamma + wave slices
-constexpr size_t kItemsLdsW = kItemsLds + 4 * (size_t)128 * (128 + 4);    // + the last Linear's W^T image
+constexpr size_t kItemsLdsW = kItemsLds + 4 * (size_t)128 * (128 + 4) + 4 * 2 * 128;  // + the last Linear's
+                                                                                       // W^T image + bm, bl
 
 // LDS bytes per kind: weight images (H = 64 only) + vectors + the two
 // [128 items][H+4] operand images of the outer products.
@@ -2279,6 +2309,8 @@ int check_bwd_mlp(const sgnn_mlp* m, const char* what) {
 
 const float* last_w(const sgnn_mlp* m) { return m->nlin == 3 ? m->w3 : m->w2; }
 const float* mid_w(const sgnn_mlp* m) { return m->nlin == 3 ? m->w2 : nullptr; }
+const float* last_b(const sgnn_mlp* m) { return m->nlin == 3 ? m->b3 : m->b2; }
+const float* mid_b(const sgnn_mlp* m) { return m->nlin == 3 ? m->b2 : nullptr; }
 
 #define SGNN_BWD_DISPATCH(H, NL, CALL)                                    \
   do {                                                                    \
@@ -2309,7 +2341,7 @@ extern "C" int64_t sgnn_bwd_scratch_floats(int32_t kind, int32_t hidden, int64_t
   const int64_t H = hidden, pad = 32 * ((nitems + 31) / 32);
   (void)nlin;
   switch (kind) {
-    case SGNN_SLAB_EDGE: return 2 * pad * H;                // dy, d2 (tiled)
+    case SGNN_SLAB_EDGE: return 3 * pad * H;                // dy, d2, recomputed h2 (tiled)
     case SGNN_SLAB_NODE: return 3 * nitems * H;             // dy, d2, dh
     case SGNN_SLAB_UV: return 2 * nitems * H;               // dU, dV
     case SGNN_SLAB_ENC_EDGE: return 4 * pad * H + pad * 32; // dy, d2, dh, h1 (tiled) + features
@@ -2324,13 +2356,17 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
                                    int32_t de0_accumulate, float* slab, int32_t nslab,
                                    float* scratch, int64_t edge_cap, void* stream) {
   using namespace sgnn;
-  if (!edge_fn || !dagg || !rowptr || !send || !recv || !saves || !saves->h || !saves->yhat ||
+  if (!edge_fn || !dagg || !rowptr || !send || !recv || !saves || !saves->h ||
       !saves->rstd || !e0t || !du || !cin || !cout || !dh_rows || !slab || nslab < 1 || n <= 0 ||
       (!de0t && edge_fn->hidden == 128))
     return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: bad arguments");
   int st = check_bwd_mlp(edge_fn, "edge_layer_bwd: edge MLP");
   if (st) return st;
-  if (edge_fn->nlin == 3 && !saves->h2) return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: saves->h2");
+  // recompute mode: yhat and h2 both NULL, hidden 128 with nlin 3 only (include/sgnn.h, sgnn_saves)
+  const bool rc = !saves->yhat;
+  if (rc && !(edge_fn->hidden == 128 && edge_fn->nlin == 3 && !saves->h2))
+    return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: saves->yhat NULL only at hidden 128, nlin 3, with h2 NULL");
+  if (!rc && edge_fn->nlin == 3 && !saves->h2) return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: saves->h2");
   const int H = edge_fn->hidden;
   if (H == 64 && n * H * 4 >= (int64_t)kBufRecords)
     return set_error(SGNN_ERR_UNSUPPORTED, "edge_layer_bwd: at most 8M nodes per launch at H = 64");
@@ -2338,15 +2374,19 @@ extern "C" int sgnn_edge_layer_bwd(const float* dagg, const int32_t* rowptr, con
                 e_scale, last_w(edge_fn), mid_w(edge_fn), edge_fn->w1 + 2 * H, edge_fn->ln_g, du,
                 cin, cout, dh_rows, de0t, de0_accumulate, slab,
                 sgnn_bwd_slab_floats(SGNN_SLAB_EDGE, H, 0, edge_fn->nlin)};
+  if (rc) {
+    a.bm = mid_b(edge_fn);
+    a.bl = last_b(edge_fn);
+  }
   if (H == 128) {
     if (!scratch || edge_cap < 1) return set_error(SGNN_ERR_INVALID, "edge_layer_bwd: H=128 needs scratch");
     const int nl = edge_fn->nlin;
     const int64_t pad = 32 * ((edge_cap + 31) / 32);
-    EdgeItemsArgs p{a, scratch, scratch + pad * H};
+    EdgeItemsArgs p{a, scratch, scratch + pad * H, scratch + 2 * pad * H};
     const int64_t tl = pad * H;   // floats of one tiled [edge_cap][H] array
     const int64_t vb = slab_nmat_floats(SGNN_SLAB_EDGE, H, 0, nl), W = kWaves, ss = a.slab_stride;
     const int32_t* Edev = rowptr + n;
-    const float* hl = nl == 3 ? saves->h2 : saves->h;
+    const float* hl = nl == 3 ? (rc ? p.h2_out : saves->h2) : saves->h;
     if (nl == 3) launch_bwd(k_edge_items<4, 3>, nslab, kItemsLdsW, stream, p);
     else launch_bwd(k_edge_items<4, 2>, nslab, kItemsLdsW, stream, p);
     run_wgrad<4, 4, 1>(wg(p.dy_out, 1, 0, tl, hl, 1, 0, tl, slab, 0, H, vb, ss, nslab, 0, Edev), nslab, stream);

@@ -361,12 +361,12 @@ void k_edge_layer(EdgeLayerArgs a) {
     if (TRAIN) store_tiled<TH>(a.sv.h + tile * (32 * H), hacc);
     f32x16 y[TH], h2[TH];
     mlp_tail<TH, NL, TH, GW>(y, h2, hacc, a.wm, H, bm, W2, ldw2, b2);
-    if (TRAIN && NL == 3) store_tiled<TH>(a.sv.h2 + tile * (32 * H), h2);
+    if (TRAIN && NL == 3 && a.sv.h2) store_tiled<TH>(a.sv.h2 + tile * (32 * H), h2);
     if (TRAIN) {
       f32x16 yh[TH];
       float rs;
       acc_layernorm_save<TH>(y, g, bb, yh, rs);
-      store_tiled<TH>(a.sv.yhat + tile * (32 * H), yh);
+      if (a.sv.yhat) store_tiled<TH>(a.sv.yhat + tile * (32 * H), yh);   // (NULL: recomputed in the backward)
       if (h == 0 && valid) a.sv.rstd[e] = rs;
     } else {
       acc_layernorm<TH>(y, g, bb);
@@ -745,8 +745,14 @@ extern "C" int sgnn_edge_layer(const float* u, const float* v, const float* e0t,
   EdgeLayerArgs a{u, v, e0t, e_scale, rowptr, send, recv, n, edge_fn->w1 + 2 * H, last_w(edge_fn),
                   last_b(edge_fn), edge_fn->ln_g, edge_fn->ln_b, agg, cin, cout, {},
                   mid_w(edge_fn), mid_b(edge_fn)};
-  const bool train = want_saves(saves);
-  if ((st = check_train(train, edge_fn, saves, "edge_layer: nmlp_layers = 2 training needs saves->h2"))) return st;
+  // training saves; at hidden 128 with nmlp_layers 2, yhat and h2 may both be NULL (the backward recomputes
+  // them from h: include/sgnn.h, sgnn_saves)
+  const bool train = saves != nullptr && (saves->yhat != nullptr || saves->h != nullptr);
+  const bool rc = train && !saves->yhat;
+  if (rc && !(H == 128 && edge_fn->nlin == 3 && !saves->h2))
+    return set_error(SGNN_ERR_INVALID, "edge_layer: saves->yhat NULL only at hidden 128, nmlp_layers 2, with h2 NULL");
+  if (!rc && (st = check_train(train, edge_fn, saves, "edge_layer: nmlp_layers = 2 training needs saves->h2")))
+    return st;
   if (train) {
     if (!saves->h || !saves->rstd) return set_error(SGNN_ERR_INVALID, "edge_layer: saves");
     a.sv = *saves;

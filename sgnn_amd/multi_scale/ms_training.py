@@ -68,8 +68,11 @@ class MSTrainWorkspace:
         self.ee_h2 = {k: (e(tl[k]) if two else None) for k in EDGE_TYPES}
         kb = self.kinds
         self.e_h = [e(tl[kb[b]]) for b in range(self.nb)]
-        self.e_h2 = [e(tl[kb[b]]) if two else None for b in range(self.nb)]
-        self.e_yh = [e(tl[kb[b]]) for b in range(self.nb)]
+        # hidden 128, nmlp 2: the edge backward forms h2 and yhat again from h (bit-identical to the
+        # forward's), so the blocks keep one [E][H] activation instead of three
+        rc = H == 128 and two
+        self.e_h2 = [e(tl[kb[b]]) if two and not rc else None for b in range(self.nb)]
+        self.e_yh = [None if rc else e(tl[kb[b]]) for b in range(self.nb)]
         self.e_rstd = [e(cap[kb[b]]) for b in range(self.nb)]
         self.n_agg = [e(n, H) for _ in range(self.nb)]
         self.n_h = [e(n, H) for _ in range(self.nb)]

@@ -11,12 +11,15 @@ import torch
 LR = 1e-3
 STEPS = 2
 # single scale: the real Taylor-bar sizes (120/160/200 x 40 lattices = 4,800 / 6,400 / 8,000 particles)
-SS_GRAPHS = [(120, 40), (160, 40), (200, 40), (100, 40), (160, 40), (200, 40), (120, 40), (160, 40)]
+SS_GRAPHS = [(120, 40), (160, 40), (200, 40), (100, 40), (160, 40), (200, 40), (120, 40), (160, 40),
+             (250, 100), (250, 100)]
 SS_RANKS = [[0, 1], [2]]          # rank 0 holds two graphs (4,800 + 6,400), rank 1 one (8,000)
 SS_RANKS4 = [[0], [1], [2], [3]]  # four ranks, one graph each (4,800 / 6,400 / 8,000 / 4,000)
 # C3 at its own shape (BASELINE configs[2], train.py:257-273): a global batch of 8 real-size Taylor graphs,
 # one whole graph per rank, 8 ranks -- 4,800 / 6,400 / 8,000 / 4,000 / 6,400 / 8,000 / 4,800 / 6,400
 SS_RANKS8 = [[g] for g in range(8)]
+# the C2 graph size split over two ranks: 250 x 100 = 25,000 particles each (C2 is 250 x 200 = 50,000)
+SS_RANKS_C2 = [[8], [9]]
 # multi scale (nmlp_layers 2, two scales): one graph per rank, unequal sizes
 MS_GRAPHS = [(30, 14), (36, 12), (28, 15), (33, 12)]
 MS_RANKS = [[0], [1]]
@@ -159,6 +162,7 @@ CASES = {"ss": (run_single_scale, SS_GRAPHS, SS_RANKS), "ms": (run_multi_scale, 
          # four ranks (the C3 / C5 sharding at world 4; gloo, the ranks share the one leased GPU)
          "ss4_overlap": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS4),
          "ss8": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS8),
+         "ss_c2": (run_single_scale_overlap, SS_GRAPHS, SS_RANKS_C2),
          "ms4": (run_multi_scale, MS_GRAPHS, MS_RANKS4)}
 RCCL_CASES = {"ss_rccl1", "ms_rccl1"}
 MS_CASES = {"ms", "ms_overlap", "ms_rccl1", "ms4"}   # run(..., global_ids=...): host-side counts

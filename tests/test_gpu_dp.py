@@ -14,7 +14,8 @@ group with the overlapped per-layer bucket all-reduces forced on (async collecti
 stream, handles waited before Adam): the collective path C3 / C5 use, on real RCCL; `ms_overlap` /
 `ms_rccl1`: the multi-scale trainer's per-block buckets the same way; `ss4_overlap` / `ms4`: four ranks
 (one graph each), the single-scale one with the overlapped bucket all-reduces; `ss8`: C3 at its own
-shape -- eight ranks, one real-size Taylor graph each (the 8-graph global batch), overlapped buckets.
+shape -- eight ranks, one real-size Taylor graph each (the 8-graph global batch), overlapped buckets;
+`ss_c2`: the C2 graph size (50,000 particles) as two 25,000-particle ranks.
 Every case calls train_step without n_global: the ranks' counts ride in the gradient all-reduce
 (train.DataParallel.plan), no per-step gather."""
 import os
@@ -40,7 +41,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("case", ["ss", "ms", "ss_overlap", "ss_rccl1", "ms_overlap", "ms_rccl1", "ss4_overlap", "ms4",
-                                  "ss8"])
+                                  "ss8", "ss_c2"])
 def test_two_ranks_match_one_process(case, tmp_path):
     from tests.dp_cases import CASES, LR, STEPS
     run, _, ranks = CASES[case]
