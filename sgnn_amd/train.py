@@ -70,6 +70,9 @@ class DataParallel:
         # test hook: the overlapped bucket path on a one-rank RCCL group (tests/test_gpu_dp.py: RCCL refuses
         # two ranks on one device, so the box's one GPU runs the collectives' stream logic at world size 1)
         self.force_overlap = False
+        # test / trace hook: the deferred-count path (below) on a one-rank group (tools/dp_sync_trace.py)
+        self.force_deferred = False
+        self._count_src = {}
 
     def layout(self, n_local: int, device) -> Tuple[int, int]:
         """(N_global, offset): the particle count over all ranks (the mean
@@ -102,7 +105,7 @@ class DataParallel:
 
     def plan(self, n_local: int, n_global: Optional[int], particle_offset: Optional[int]):
         """(inv_count for the backward kernels, particle offset, deferred) of one step."""
-        if self.world == 1:
+        if self.world == 1 and not self.force_deferred:
             return 1.0 / (n_global or n_local), particle_offset or 0, False
         off = self.rank * self.RANK_NOISE_STRIDE if particle_offset is None else particle_offset
         if n_global is None:
@@ -111,8 +114,16 @@ class DataParallel:
 
     def put_count(self, loss_tail: torch.Tensor, n_local: int) -> None:
         """This rank's particle count into the all-reduced tail (queued after the backward's writes)."""
-        loss_tail[self.COUNT_HI] = float(n_local >> 20)
-        loss_tail[self.COUNT_LO] = float(n_local & ((1 << 20) - 1))
+        # a device-to-device copy from a per-count cached tensor: assigning Python floats to device
+        # elements is a synchronous host-to-device copy, which waited ~0.8 ms for the backward to drain
+        # (tools/dp_sync_trace.py, profiles/r06_dp_sync_trace.txt)
+        key = (n_local, loss_tail.device)
+        src = self._count_src.get(key)
+        if src is None:
+            src = torch.tensor([float(n_local >> 20), float(n_local & ((1 << 20) - 1))],
+                               dtype=loss_tail.dtype).to(loss_tail.device)
+            self._count_src[key] = src
+        loss_tail[self.COUNT_HI:self.COUNT_LO + 1].copy_(src, non_blocking=True)
 
     def take_count(self, grad: torch.Tensor, loss_tail: torch.Tensor) -> torch.Tensor:
         """After the all-reduce: N_global as a device scalar; the gradient scaled by 1/N_global in place."""
@@ -134,7 +145,7 @@ class DataParallel:
 
     def allreduce_(self, *tensors: torch.Tensor) -> None:
         """SUM all-reduce (RCCL over xGMI on MI355X; gloo in CPU tests)."""
-        if self.world == 1:
+        if self.world == 1 and not (self.force_overlap or self.force_deferred):
             return
         for t in tensors:
             if self.host_staging and t.is_cuda:
