@@ -131,6 +131,32 @@ template <int TH, int TK, bool G = false>
 SGNN_DEV void mfma_from_acc(f32x16 (&acc)[TH], const float* wl, int ld, int kbase,
                             const f32x16 (&x)[TK]) {
   const WRows<TH, G> W(wl, ld);
+  if constexpr (G) {
+    // Global (L2) weights: the next k-group's rows are requested before this group's 4 TH MFMAs, so
+    // each group's load latency hides under the previous group's products (the compiler's own
+    // schedule issued every group's loads right in front of its MFMAs and waited on them: one L2
+    // round trip per 16 MFMAs).  Same products in the same order: bit-identical results.
+    constexpr int NG = 4 * TK;
+    f32x4 w[2][TH];
+#pragma unroll
+    for (int t = 0; t < TH; ++t) w[0][t] = W.get(t, kbase);
+#pragma unroll
+    for (int s = 0; s < NG; ++s) {
+      const int tk = s >> 2, g = s & 3;
+      if (s + 1 < NG) {
+#pragma unroll
+        for (int t = 0; t < TH; ++t) w[(s + 1) & 1][t] = W.get(t, kbase + 32 * ((s + 1) >> 2) + 8 * ((s + 1) & 3));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int t = 0; t < TH; ++t) acc[t] = mfma32(w[s & 1][t][c], x[tk][4 * g + c], acc[t]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return;
+  }
 #pragma unroll
   for (int tk = 0; tk < TK; ++tk) {
 #pragma unroll

@@ -162,20 +162,30 @@ SGNN_DEV void matvec_t(f32x16 (&acc)[TH], const float* w, int ld, const f32x16 (
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(w), (short)0, 0x7ffffff0, 0x00020000);
     const int voff = 4 * (4 * h * ld + l);
+    // one k-group (4 k-steps x TH tiles) of weights in flight ahead of the group being multiplied (the
+    // compiler's own schedule waited one L2 round trip per TH MFMAs); same products, same order
+    constexpr int NG = 4 * TK;
+    float wv[2][4][TH];
+    auto fetch = [&](float (&dst)[4][TH], int s) {
 #pragma unroll
-    for (int tk = 0; tk < TK; ++tk)
+      for (int c = 0; c < 4; ++c) {
+        const int soff = 4 * (32 * (s >> 2) + 8 * (s & 3) + c) * ld;
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+        for (int t = 0; t < TH; ++t)
+          dst[c][t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff + 128 * t, soff, 0));
+      }
+    };
+    fetch(wv[0], 0);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int soff = 4 * (32 * tk + 8 * g + c) * ld;
-          float wv[TH];
+    for (int s = 0; s < NG; ++s) {
+      if (s + 1 < NG) fetch(wv[(s + 1) & 1], s + 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int t = 0; t < TH; ++t)
-            wv[t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff + 128 * t, soff, 0));
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int t = 0; t < TH; ++t) acc[t] = mfma32(wv[t], x[tk][4 * g + c], acc[t]);
-        }
+        for (int t = 0; t < TH; ++t) acc[t] = mfma32(wv[s & 1][c][t], x[s >> 2][4 * (s & 3) + c], acc[t]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 
