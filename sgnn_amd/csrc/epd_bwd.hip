@@ -162,8 +162,26 @@ SGNN_DEV void matvec_t(f32x16 (&acc)[TH], const float* w, int ld, const f32x16 (
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(w), (short)0, 0x7ffffff0, 0x00020000);
     const int voff = 4 * (4 * h * ld + l);
-    // one k-group (4 k-steps x TH tiles) of weights in flight ahead of the group being multiplied (the
-    // compiler's own schedule waited one L2 round trip per TH MFMAs); same products, same order
+    if constexpr (TH < 4) {
+      // H = 64 (k_uv_bwd64: two waves per SIMD hide the round trip; the prefetch registers spilled
+      // there, C2 training +0.5-1 %, profiles/r06_ab_gw_prefetch.txt): one group at a time
+#pragma unroll
+      for (int s = 0; s < 4 * TK; ++s)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float wv[TH];
+#pragma unroll
+          for (int t = 0; t < TH; ++t)
+            wv[t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                rs, voff + 128 * t, 4 * (32 * (s >> 2) + 8 * (s & 3) + c) * ld, 0));
+#pragma unroll
+          for (int t = 0; t < TH; ++t) acc[t] = mfma32(wv[t], x[s >> 2][4 * (s & 3) + c], acc[t]);
+        }
+      return;
+    }
+    // H = 128 (one wave per SIMD): one k-group (4 k-steps x TH tiles) of weights in flight ahead of the
+    // group being multiplied (the compiler's own schedule waited one L2 round trip per TH MFMAs); same
+    // products, same order
     constexpr int NG = 4 * TK;
     float wv[2][4][TH];
     auto fetch = [&](float (&dst)[4][TH], int s) {
