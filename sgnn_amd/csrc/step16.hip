@@ -577,14 +577,40 @@ struct EdgePhase {
       const int h0 = next_item(0);
       if (h0 >= 0) load_pos(h0);
     }
+    // e0 rows in HBM (two node sub-tiles): the next item's rows are requested before this item's product,
+    // so their L2 round trip hides under its MFMAs (LDS rows need no lookahead)
+    f32x4 xn[KQ];
+    if constexpr (!FIRST) {
+      if (e0_hbm) {
+        const int h0 = next_item(0);
+        if (h0 >= 0) ld_e0(xn, h0);
+      }
+    }
 #pragma unroll
     for (int sl = 0; sl < kPre; ++sl) {
       hook(sl);
       const int hs = item_half(sl);
       if (hs < 0) continue;
       f32x4 x[KQ];
-      if constexpr (FIRST) encode_item(x, hs, sl);
-      else ld_e0(x, hs);
+      if constexpr (FIRST) {
+        encode_item(x, hs, sl);
+      } else if (e0_hbm) {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) x[q] = xn[q];
+        int hn = -2;
+#pragma unroll
+        for (int k = sl + 1; k < kPre; ++k) {
+          const int h = item_half(k);
+          if (h >= 0) {
+            hn = h;
+            break;
+          }
+          if (h == -2) break;
+        }
+        if (hn >= 0) ld_e0(xn, hn);
+      } else {
+        ld_e0(x, hs);
+      }
       constexpr int kLast = kPre - 1;
       f32x4(&dst)[KQ] = pre[DONOR ? (sl == 0 ? kLast : sl - 1) : sl];
 #pragma unroll
