@@ -742,15 +742,17 @@ def bench_ms_train(workload, steps, warmup, world, rank, device, seed, cpu_steps
     dt = max_over_ranks(dt, world, device)
     kstats = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in timers.items()}
     eb = ms_block_edges(edges, L)
-    # edge backward per edge: last (+ middle) Linear W^T dy and dW, W1e^T dh and dW1e
-    flops_bwd = eb / (L + 2) * (8 + (4 if nmlp == 2 else 0)) * H * H
+    # edge backward per edge: last (+ middle) Linear W^T dy and dW, W1e^T dh and dW1e; at H = 128 with
+    # nmlp_layers 2 the items kernel also re-forms h2 = relu(Wm h1 + bm) and Wl h2 (the forward's values,
+    # not saved: DESIGN.md 8.4), 4 H^2 more that it executes
+    flops_bwd = eb / (L + 2) * (8 + (4 if nmlp == 2 else 0) + (4 if (H == 128 and nmlp == 2) else 0)) * H * H
     dom = "k_edge_bwd"
     # H = 128: one sgnn_edge_layer_bwd call = the per-edge items kernel + one split-K weight-gradient
     # GEMM per Linear (3 at nmlp_layers 2)
     # (exact kernel names as rocprofv3 lists them: the profile summary's per-launch bytes and time
     # of the composite come from the same names)
     kname = "k_edge_bwd64" if (H == 64 and nmlp == 1) else \
-        (f"k_edge_items<{H // 32}, {nmlp + 1}> + {nmlp + 1} k_wgrad_half<{H // 32}, 1, 8>" if H == 128 else
+        (f"k_edge_items<{H // 32}, {nmlp + 1}> + {nmlp + 1} k_wgrad_full<1>" if H == 128 else
          f"k_edge_items<{H // 32}, {nmlp + 1}> + {nmlp + 1} k_wgrad<{H // 32}, {H // 32}>")
     res = {
         "metric": "particle-steps/sec (multi-scale training fwd+bwd+Adam)",

@@ -1806,6 +1806,80 @@ void k_wgrad_half(WgradOp op, int nslab) {
   }
 }
 
+// The 128 x 128 weight-gradient GEMM with ONE workgroup per slab forming all 128 rows: the B operand of a
+// chunk is read from HBM once instead of once per row half (k_wgrad_half: A + 2 B per chunk; C5's edge
+// GEMMs ran at ~4.4 TB/s).  Sixteen waves (four per SIMD, as two k_wgrad_half workgroups), one 32 x 32
+// output tile each; the [64 items][128 + 4] images of A and B (67.6 KB).  Same products in the same order
+// as k_wgrad_half (every tile over the chunk's 64 items in order, chunks in order; the column sums by
+// waves 0-7 over the same item partition, waves w and w + 4 added in that order), so the slabs are
+// bit-identical to the half-row form.
+template <int TAG>
+__global__ __launch_bounds__(1024) void k_wgrad_full(WgradOp op, int nslab) {
+  constexpr int NWV = 16, NTH = 64 * NWV;
+  constexpr int U = 128, ld = U + 4;
+  constexpr int RPW = kHalfChunk / 8;     // items per column-sum wave (waves 0-7, as k_wgrad_half)
+  extern __shared__ float lds[];
+  float* imA = lds;
+  float* imB = imA + kHalfChunk * ld;
+  const int l = lane_id(), w = (int)threadIdx.x / 64;
+  const int slab = (int)blockIdx.x;
+  const int tu = w >> 2, tv = w & 3;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  float cs0 = 0.0f, cs1 = 0.0f;
+  const int64_t nitems = op.nitems_dev ? (int64_t)*op.nitems_dev : op.nitems;
+  const int64_t nch = (nitems + kHalfChunk - 1) / kHalfChunk;
+  const int64_t c0 = nch * slab / nslab, c1 = nch * (slab + 1) / nslab;
+  ChunkRegs<U, NTH> ra, rb;
+  if (c0 < c1) {
+    fetch_sub<U, U, NTH>(ra, op.A, op.a_tiled, op.a_ld, 0, c0 * kHalfChunk, nitems, op.a_len);
+    fetch_sub<U, U, NTH>(rb, op.B, op.b_tiled, op.b_ld, 0, c0 * kHalfChunk, nitems, op.b_len);
+  }
+  for (int64_t c = c0; c < c1; ++c) {
+    put_sub<U, NTH>(imA, ra, op.a_tiled);
+    put_sub<U, NTH>(imB, rb, op.b_tiled);
+    __syncthreads();
+    if (c + 1 < c1) {   // the next chunk's loads fly under this chunk's MFMAs
+      fetch_sub<U, U, NTH>(ra, op.A, op.a_tiled, op.a_ld, 0, (c + 1) * kHalfChunk, nitems, op.a_len);
+      fetch_sub<U, U, NTH>(rb, op.B, op.b_tiled, op.b_ld, 0, (c + 1) * kHalfChunk, nitems, op.b_len);
+    }
+    mfma_outer<kHalfChunk>(acc, imA, ld, 32 * tu, imB, ld, 32 * tv);
+    if (op.colsum && w < 8) {
+      const float* sl = imA + w * RPW * ld;
+#pragma unroll
+      for (int it = 0; it < RPW; ++it) {
+        cs0 += sl[it * ld + l];
+        cs1 += sl[it * ld + 64 + l];
+      }
+    }
+    __syncthreads();
+  }
+  {
+    const int64_t o = slab * op.slab_stride + (int64_t)(32 * tu) * op.dst_ld + 32 * tv;
+#ifdef SGNN_DEBUG_BOUNDS
+    int64_t hi = o + 31 * (int64_t)op.dst_ld + 31;
+    SGNN_BOUNDS(hi, 0, op.dst_len, "wgrad slab tile");
+#endif
+    store_tile_rowmajor(op.dst + o, op.dst_ld, acc);
+  }
+  if (op.colsum) {
+    if (w >= kWaves && w < 8) {
+      lds[(w - kWaves) * 128 + l] = cs0;
+      lds[(w - kWaves) * 128 + 64 + l] = cs1;
+    }
+    __syncthreads();
+    if (w < kWaves) {
+      cs0 += lds[w * 128 + l];
+      cs1 += lds[w * 128 + 64 + l];
+      int64_t o = slab * op.slab_stride + w * 128 + l;
+      SGNN_BOUNDS(o, 0, op.colsum_len - 64, "wgrad column sums");
+      op.colsum[o] = cs0;
+      op.colsum[o + 64] = cs1;
+    }
+  }
+}
+
 // ---- edge layer, H = 128 ---------------------------------------------------
 struct EdgeItemsArgs {
   EdgeBwdArgs b;
@@ -2281,6 +2355,16 @@ void launch_bwd(K kernel, int nslab, size_t lds, void* stream, const A& a) {
 template <int TU, int TV, int TAG = 0>
 void run_wgrad(const WgradOp& op, int nslab, void* stream) {
   static_assert(TU == 4, "weight-gradient GEMMs of 128-row gradients (the H = 128 backward)");
+#ifndef SGNN_WGRAD_FULL
+#define SGNN_WGRAD_FULL 1
+#endif
+  if (SGNN_WGRAD_FULL && TV == 4) {   // 128 x 128: one full-row workgroup (16 waves) per slab
+    const size_t lds = 4 * (size_t)kHalfChunk * 2 * (128 + 4);
+    auto kern = k_wgrad_full<TAG>;
+    set_lds(kern, lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nslab), dim3(1024), lds, static_cast<hipStream_t>(stream), op, nslab);
+    return;
+  }
   // two half-row workgroups per slab, two per CU
   constexpr int NWV = TV == 4 ? 8 : 4;
   const size_t lds = 4 * (size_t)kHalfChunk * ((64 + 4) + (32 * TV + 4));
