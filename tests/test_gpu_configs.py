@@ -13,8 +13,10 @@
   C5  multi-scale 3D, L = 10, H = 128, nmlp_layers = 2: forward and gradients
       on 9,600 particles against the float64 multi-scale oracle; at 1M
       particles the hierarchy and the three static edge lists are bit-exact
-      against the oracle and the training step is finite and bitwise
-      deterministic.
+      against the oracle, the training step is finite and bitwise
+      deterministic, its gradient agrees with central differences of its own
+      loss (to 5e-4 of |g|), and the fused forward equals the width-generic
+      autograd path's on every particle.
 
 Why float64 oracles: at L = 10 the edge latent enters the last block scaled
 by 2^9 and the fp32 oracle's own rounding error grows with depth (measured
@@ -298,7 +300,9 @@ def test_c5_full_1m_hierarchy_bit_exact_and_training_deterministic():
     """C5 at its full per-GPU size (100^3 = 1,000,000 particles): the GPU
     hierarchy and g2m/m2m/m2g edge lists equal the oracle's bit for bit; two
     training steps on the same inputs (lr = 0) give bitwise-identical finite
-    gradients and losses."""
+    gradients and losses; the gradient against central differences of the
+    step's own loss along it; the fused forward against the width-generic
+    path (independent kernels) on the same window."""
     from oracle import multi_scale_oracle as MO
     from sgnn_amd import synthetic
     from sgnn_amd.multi_scale import build_static_multi_scale_graph
@@ -323,6 +327,7 @@ def test_c5_full_1m_hierarchy_bit_exact_and_training_deterministic():
     strain = torch.zeros(n, device="cuda")
     noise = torch.zeros_like(pos)
     tr = MultiScaleTrainer(sim, lr_init=0.0)
+    w_init = tr.flat.param.clone()   # the schedule's + 1e-6 (train.py:276-278) moves the weights after step 2
     res = []
     for _ in range(2):
         out = tr.train_step(pos, nxt, strain, noise=noise)
@@ -330,5 +335,39 @@ def test_c5_full_1m_hierarchy_bit_exact_and_training_deterministic():
         res.append((float(out["loss"]), tr.flat.grad.clone()))
     assert np.isfinite(res[0][0]) and torch.isfinite(res[0][1]).all()
     assert res[0][0] == res[1][0] and torch.equal(res[0][1], res[1][1])
-    del tr, sim, res
+    # Full-size checks of the fused chain against independent arithmetic (no CPU oracle finishes at 1M):
+    # (1) the gradient along its own direction u = g / |g| against central differences of the step's loss at
+    #     the SAME weights (restored first: the LR schedule's + 1e-6 floor, train.py:276-278, moved them after
+    #     the second step), L(w + eps u) - L(w - eps u) over 2 eps.  Each step's loss is formed before its Adam
+    #     update, and the weights are reset before every evaluation.  Measured at 1M (tools/exp_fd_c5_1m.py):
+    #     -4.8e-4 of |g| at eps 5e-3, -1.2e-4 at 2.5e-3, converging as eps^2 (-4.8e-6 at 3.1e-4); per tensor
+    #     the same (the largest, the late M2M edge-MLP first Linears under the 2^k latent, -8e-3 -> 2e-3).
+    loss0, grad = res[0]
+    gnorm = float(grad.norm())
+    assert gnorm > 0.0
+    u = grad / gnorm
+    flat = tr.flat.param
+    fd = []
+    for eps in (5e-3, 2.5e-3):
+        flat.copy_(w_init).add_(u, alpha=eps)
+        lp = float(tr.train_step(pos, nxt, strain, noise=noise)["loss"])
+        flat.copy_(w_init).add_(u, alpha=-eps)
+        lm = float(tr.train_step(pos, nxt, strain, noise=noise)["loss"])
+        fd.append((lp - lm) / (2 * eps))
+    flat.copy_(w_init)
+    print(f"C5 1M: |g| = {gnorm:.6e}, central differences " + " / ".join(f"{v:.6e}" for v in fd))
+    assert abs(fd[0] - gnorm) <= 2e-3 * gnorm and abs(fd[1] - gnorm) <= 5e-4 * gnorm, (gnorm, fd)
+    # (2) the fused forward (k_encode_*, k_edge_layer, k_node_layer at H = 128, nmlp 2) against the
+    #     width-generic path (autograd.hip: MFMA GEMMs, gathers, LayerNorm and CSR sums of their own) on the
+    #     same 1M-particle window: every predicted acceleration and strain.
+    with torch.no_grad():
+        _, pred_fused, _ = sim._run(pos, None)
+        inp, use_emb = sim._step_inputs(pos, None)
+        pred_gen = sim._generic_pred(inp, use_emb)
+    torch.cuda.synchronize()
+    scale = float(pred_gen.abs().max())
+    err = float((pred_fused - pred_gen).abs().max())
+    print(f"C5 1M forward: fused vs generic max|d| = {err:.3e} (max|pred| {scale:.3e})")
+    assert torch.isfinite(pred_fused).all() and err <= 1e-3 * scale + 1e-5, (err, scale)
+    del tr, sim, res, grad, u
     _free()
